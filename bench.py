@@ -1,0 +1,356 @@
+#!/usr/bin/env python3
+"""TEMPI-MI355X headline benchmark (driver contract: one JSON line on rank 0).
+
+Metric (BASELINE.json): MPI_Pack/Unpack GB/s vs HBM peak. One STEP = one
+MPI_Pack + one MPI_Unpack, through libtempi.so, of one object of config 2
+(2D/3D subarray sweep, 1 MiB - 1 GiB objects on one MI355X). The default
+object is the bench-mpi-pack type of config 1 (MPI_Type_vector(1024, 512,
+1024, MPI_BYTE), /root/reference/bin/bench_mpi_pack.cpp) scaled to a 1 GiB
+packed size: MPI_Type_create_subarray({2^21, 1024}, {2^21, 512}, {0, 0}),
+extent 2 GiB (>> the 256 MiB Infinity Cache, so HBM is what is measured).
+
+value = algorithmic bytes moved by all ranks / max-over-ranks wall time, where
+one pack or unpack of P payload bytes moves 2P (read P + write P; SURVEY
+8(d)). N > 1 (torchrun): every rank packs its own object on its own GPU, no
+collective on the data path (weak scaling, replicas).
+
+Other modes (not the driver's line):
+  --sweep FILE   the config-2 sweep (block 1 B - 4 KiB, 2D and 3D, 1 MiB -
+                 1 GiB), one JSON record per point, written to FILE
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+METRIC = "MPI_Pack/Unpack GB/s vs HBM peak; 3D halo-exchange µs/iter at 1–8 GPUs"
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--rows", type=int, default=2 * 1024 * 1024)
+    p.add_argument("--pitch", type=int, default=1024)
+    p.add_argument("--block", type=int, default=512)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=8.0)
+    p.add_argument("--traffic", action="store_true",
+                   help="run rocprofv3 FETCH_SIZE / WRITE_SIZE passes (child processes) for roofline.traffic")
+    p.add_argument("--sweep", default=None, help="run the config-2 sweep and write JSON records here")
+    p.add_argument("--inner", action="store_true", help=argparse.SUPPRESS)  # child for --traffic
+    return p.parse_args()
+
+
+def dist_setup(args):
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    pg = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        pg = dist
+    return rank, world, local, pg
+
+
+def barrier(pg):
+    if pg is not None:
+        pg.barrier()
+
+
+def allreduce_max(pg, x):
+    if pg is None:
+        return x
+    import torch
+
+    t = torch.tensor([x], dtype=torch.float64)
+    pg.all_reduce(t, op=pg.ReduceOp.MAX)
+    return float(t.item())
+
+
+def allreduce_sum(pg, x):
+    if pg is None:
+        return x
+    import torch
+
+    t = torch.tensor([x], dtype=torch.float64)
+    pg.all_reduce(t, op=pg.ReduceOp.SUM)
+    return float(t.item())
+
+
+def make_2d(mpi, rows, pitch, block):
+    t = mpi.Type_create_subarray([rows, pitch], [rows, block], [0, 0], mpi.ORDER_C, mpi.BYTE)
+    return mpi.Type_commit(t)
+
+
+def cpu_baseline(mpi, pitch, block, seconds):
+    """Host MPI (MPICH) MPI_Pack + MPI_Unpack on host buffers, one pinned core:
+    the reference's CPU path (/root/reference/src/pack.cpp:51-54)."""
+    import numpy as np
+
+    rows = max(1, (128 * 1024 * 1024) // block)  # 128 MiB packed sample
+    t = make_2d(mpi, rows, pitch, block)
+    src = (np.arange(rows * pitch, dtype=np.int64) & 0xFF).astype(np.uint8)
+    packed = np.zeros(rows * block, dtype=np.uint8)
+    dst = np.zeros(rows * pitch, dtype=np.uint8)
+    old = os.sched_getaffinity(0)
+    core = sorted(old)[0]
+    os.sched_setaffinity(0, {core})
+    try:
+        mpi.Pack(src.ctypes.data, 1, t, packed.ctypes.data, packed.size, 0)  # warm
+        n = 0
+        t0 = time.perf_counter()
+        while True:
+            mpi.Pack(src.ctypes.data, 1, t, packed.ctypes.data, packed.size, 0)
+            mpi.Unpack(packed.ctypes.data, packed.size, 0, dst.ctypes.data, 1, t)
+            n += 1
+            el = time.perf_counter() - t0
+            if el >= seconds:
+                break
+    finally:
+        os.sched_setaffinity(0, old)
+    mpi.Type_free(t)
+    alg = 4.0 * rows * block * n  # pack + unpack, each reads and writes the payload
+    try:
+        model = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
+    except Exception:
+        model = "unknown"
+    return {
+        "value": round(alg / el / 1e9, 3),
+        "unit": "GB/s",
+        "cores": 1,
+        "kind": "reference",
+        "sample": (f"host MPICH 3.3.2 MPI_Pack+MPI_Unpack (the reference's CPU path for host buffers, "
+                   f"src/pack.cpp:51-54) of subarray({rows}x{pitch} -> {rows}x{block} B), "
+                   f"{rows * block >> 20} MiB packed, {n} pack+unpack pairs in {el:.1f} s, pinned to 1 core "
+                   f"of {model}"),
+    }
+
+
+def run_traffic_passes(args, kernel_substr):
+    """rocprofv3 PMC passes (one counter group per run, child processes),
+    gfx950 correction: FETCH_SIZE reads half of a wide streaming read
+    (MI355X_MICROARCH.md sec. HBM). Returns (read_bytes, write_bytes) per
+    launch of kernels whose name contains kernel_substr, or None."""
+    import csv
+    import glob
+    import shutil
+    import tempfile
+
+    if not shutil.which("rocprofv3"):
+        return None
+    out = {}
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = tempfile.mkdtemp(prefix="tempi_pmc_", dir=os.path.join(ROOT, "gpurun_out") if os.path.isdir(
+            os.path.join(ROOT, "gpurun_out")) else None)
+        cmd = ["timeout", "-s", "KILL", "120", "rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", d,
+               "-o", "pmc", "--", sys.executable, os.path.abspath(__file__), "--inner", "--steps", "3",
+               "--warmup", "1", "--rows", str(args.rows), "--pitch", str(args.pitch), "--block", str(args.block),
+               "--no-cpu-baseline"]
+        r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+        if r.returncode != 0:
+            return None
+        vals = []
+        for f in glob.glob(os.path.join(d, "**", "*counter_collection*.csv"), recursive=True):
+            with open(f) as fh:
+                for row in csv.DictReader(fh):
+                    if kernel_substr in row.get("Kernel_Name", "") and row.get("Counter_Name") == counter:
+                        vals.append(float(row["Counter_Value"]))
+        if not vals:
+            return None
+        out[counter] = sum(vals) / len(vals) * 1024.0  # counters are in KiB
+    return out["FETCH_SIZE"] * 2.0, out["WRITE_SIZE"]
+
+
+def headline(args, mpi, torch, rank, world, pg, dev):
+    rows, pitch, block = args.rows, args.pitch, args.block
+    payload = rows * block
+    t = make_2d(mpi, rows, pitch, block)
+    src = (torch.arange(rows * pitch, dtype=torch.int64, device=dev) & 0xFF).to(torch.uint8)
+    packed = torch.empty(payload, dtype=torch.uint8, device=dev)
+    dst = torch.zeros(rows * pitch, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+
+    def step():
+        mpi.Pack(src.data_ptr(), 1, t, packed.data_ptr(), payload, 0)
+        mpi.Unpack(packed.data_ptr(), payload, 0, dst.data_ptr(), 1, t)
+
+    for _ in range(args.warmup):
+        step()
+    # parity of what is being timed (exact, via strided views)
+    torch.cuda.synchronize()
+    ok = torch.equal(packed.view(rows, block), src.view(rows, pitch)[:, :block]) and torch.equal(
+        dst.view(rows, pitch)[:, :block], src.view(rows, pitch)[:, :block])
+    if not ok:
+        raise SystemExit("bench parity check failed: packed bytes differ from the strided source")
+
+    mpi.reset_counters()
+    mpi.set_kernel_profiling(True)
+    barrier(pg)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    barrier(pg)
+    mpi.set_kernel_profiling(False)
+    kt = mpi.kernel_times()
+    el_max = allreduce_max(pg, el)
+    alg_step = 4.0 * payload  # pack (2P) + unpack (2P)
+    total_alg = allreduce_sum(pg, alg_step * args.steps)
+    value = total_alg / el_max / 1e9
+    mpi.Type_free(t)
+
+    launches = kt["packs"] + kt["unpacks"]
+    avg_ms = (kt["pack_ms"] + kt["unpack_ms"]) / max(launches, 1)
+    alg_launch = 2.0 * payload
+    achieved = alg_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+    rec = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "GB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(el_max / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (byte i = i & 0xFF)",
+        "config": {
+            "workload": (f"config 2 point: MPI_Pack+MPI_Unpack of MPI_Type_create_subarray({{{rows},{pitch}}}, "
+                         f"{{{rows},{block}}}, {{0,0}}, MPI_BYTE), count 1 (bench-mpi-pack's vector(1024,512,1024) "
+                         f"scaled to {payload >> 20} MiB packed), device buffers, per rank"),
+            "packed_bytes": payload,
+            "extent_bytes": rows * pitch,
+            "block_bytes": block,
+            "stride_bytes": pitch,
+            "parallelism": f"replicas{world}",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": None,
+            "kernel": "pack_kernel<16,1> / unpack_kernel<16,1> (libtempi_hip.so)",
+            "algorithmic_bytes_per_launch": int(alg_launch),
+            "avg_launch_ms": round(avg_ms, 4),
+            "pack_avg_ms": round(kt["pack_ms"] / max(kt["packs"], 1), 4),
+            "unpack_avg_ms": round(kt["unpack_ms"] / max(kt["unpacks"], 1), 4),
+            "timed_launches": launches,
+        },
+    }
+    return rec
+
+
+def sweep(args, mpi, torch, dev, path):
+    """Config-2 sweep: 2D subarray and 3D subarray, block 1 B - 4 KiB."""
+    recs = []
+    blocks = [1, 2, 3, 4, 8, 12, 16, 24, 32, 64, 128, 256, 512, 1024, 2048, 4096]
+    sizes = [1 << 20, 16 << 20, 256 << 20, 1 << 30]
+    for packed_target in sizes:
+        for bl in blocks:
+            strides = sorted({2 * bl, bl + 16} | ({512} if bl <= 256 else set()))
+            for st in strides:
+                for dims in (2, 3):
+                    rows = packed_target // bl
+                    if dims == 2:
+                        t = mpi.Type_create_subarray([rows, st], [rows, bl], [0, 0], mpi.ORDER_C, mpi.BYTE)
+                        extent = rows * st
+                        shape = f"2d rows={rows} stride={st}"
+                    else:
+                        y = max(1, int(rows ** 0.5))
+                        z = max(1, rows // y)
+                        rows = y * z
+                        Y = y + 3
+                        t = mpi.Type_create_subarray([z + 2, Y, st], [z, y, bl], [1, 2, 0], mpi.ORDER_C, mpi.BYTE)
+                        extent = (z + 2) * Y * st
+                        shape = f"3d {z}x{y} rows pitch={st} ypad=3"
+                    if extent > (12 << 30):
+                        mpi.Type_free(t)
+                        continue
+                    t = mpi.Type_commit(t)
+                    payload = rows * bl
+                    src = torch.empty(extent, dtype=torch.uint8, device=dev)
+                    pk = torch.empty(payload, dtype=torch.uint8, device=dev)
+                    torch.cuda.synchronize()
+                    reps = max(3, min(50, int(2e9 / max(payload, 1))))
+                    mpi.Pack(src.data_ptr(), 1, t, pk.data_ptr(), payload, 0)
+                    mpi.Unpack(pk.data_ptr(), payload, 0, src.data_ptr(), 1, t)
+                    mpi.reset_counters()
+                    mpi.set_kernel_profiling(True)
+                    t0 = time.perf_counter()
+                    for _ in range(reps):
+                        mpi.Pack(src.data_ptr(), 1, t, pk.data_ptr(), payload, 0)
+                    t1 = time.perf_counter()
+                    for _ in range(reps):
+                        mpi.Unpack(pk.data_ptr(), payload, 0, src.data_ptr(), 1, t)
+                    t2 = time.perf_counter()
+                    mpi.set_kernel_profiling(False)
+                    kt = mpi.kernel_times()
+                    pk_ms = kt["pack_ms"] / reps
+                    up_ms = kt["unpack_ms"] / reps
+                    rec = {"shape": shape, "block": bl, "stride": st, "packed": payload, "extent": extent,
+                           "pack_kernel_ms": pk_ms, "unpack_kernel_ms": up_ms,
+                           "pack_api_ms": (t1 - t0) / reps * 1e3, "unpack_api_ms": (t2 - t1) / reps * 1e3,
+                           "pack_alg_gbs": 2 * payload / (pk_ms * 1e-3) / 1e9,
+                           "unpack_alg_gbs": 2 * payload / (up_ms * 1e-3) / 1e9}
+                    recs.append(rec)
+                    print(json.dumps(rec), flush=True)
+                    mpi.Type_free(t)
+                    del src, pk
+    with open(path, "w") as f:
+        json.dump(recs, f, indent=1)
+
+
+def main():
+    args = parse()
+    rank, world, local, pg = dist_setup(args)
+    import torch
+
+    import tempi_amd
+
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    mpi = tempi_amd.get_mpi()
+    mpi.Init()
+    try:
+        assert mpi.gpu_available(), "libtempi.so found no GPU"
+        if args.sweep:
+            sweep(args, mpi, torch, dev, args.sweep)
+            return
+        rec = headline(args, mpi, torch, rank, world, pg, dev)
+        if args.inner:
+            return
+        if rank == 0 and world == 1:
+            if args.traffic:
+                tr = run_traffic_passes(args, "pack_kernel")
+                if tr:
+                    rec["roofline"]["traffic"] = int(tr[0] + tr[1])
+                    rec["roofline"]["traffic_read"] = int(tr[0])
+                    rec["roofline"]["traffic_write"] = int(tr[1])
+            if not args.no_cpu_baseline:
+                rec["cpu_baseline"] = cpu_baseline(mpi, args.pitch, args.block, args.cpu_seconds)
+        if rank == 0:
+            print(json.dumps(rec), flush=True)
+    finally:
+        mpi.Finalize()
+        if pg is not None:
+            pg.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,70 @@
+/*
+ * include/tempi_ext.h -- TEMPI's own (non-MPI) C entry points in libtempi.so:
+ * introspection for tests and benchmarks, counters, and the MPI ABI constants
+ * of the library TEMPI was built against (so ctypes front ends need no
+ * compiler). Plain integers and pointers only. MPI handles are passed as
+ * int64_t (MPICH's MPI_Datatype / MPI_Comm are int).
+ */
+#ifndef TEMPI_EXT_H
+#define TEMPI_EXT_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TEMPI_EXT_MAX_DIMS 16
+
+/* the canonical form TEMPI derived for a committed datatype
+   (the reference's StridedBlock: /root/reference/include/strided_block.hpp) */
+typedef struct tempi_type_info {
+  int32_t known;    /* 1 when the handle is in TEMPI's type cache */
+  int32_t valid;    /* 1 when it is a strided block TEMPI packs on the GPU */
+  int32_t ndims;    /* dims above the contiguous block, outermost first */
+  int32_t pad_;
+  int64_t start;    /* byte offset of the first byte from the buffer origin */
+  int64_t block;    /* contiguous bytes */
+  int64_t size, lb, extent;
+  int64_t counts[TEMPI_EXT_MAX_DIMS];
+  int64_t strides[TEMPI_EXT_MAX_DIMS];
+} tempi_type_info;
+
+int tempi_type_describe(int64_t datatype, tempi_type_info *out);
+
+typedef struct tempi_counters_t {
+  uint64_t packs, unpacks, pack_bytes, unpack_bytes, launches;
+  uint64_t lib_packs, lib_unpacks;
+  uint64_t sends, recvs, isends, irecvs;
+  uint64_t send_device, send_oneshot, send_staged, send_ipc;
+  uint64_t lib_sends, lib_recvs;
+} tempi_counters_t;
+void tempi_get_counters(tempi_counters_t *out);
+void tempi_reset_counters(void);
+
+/* Kernel timing of synchronous MPI_Pack / MPI_Unpack: when on, TEMPI
+   brackets each operation's launches with HIP events on its stream and
+   accumulates the elapsed GPU time (read back with tempi_get_kernel_times;
+   tempi_reset_counters clears it). */
+typedef struct tempi_kernel_times {
+  double pack_ms, unpack_ms;
+  uint64_t packs, unpacks;
+} tempi_kernel_times;
+void tempi_set_kernel_profiling(int on);
+void tempi_get_kernel_times(tempi_kernel_times *out);
+
+/* the HIP stream (hipStream_t) TEMPI uses on `device`; NULL if none */
+void *tempi_get_stream(int device);
+/* 1 when TEMPI found a GPU at MPI_Init */
+int tempi_gpu_available(void);
+
+/* value of an MPI constant by name (e.g. "MPI_BYTE", "MPI_COMM_WORLD",
+   "MPI_ORDER_C", "sizeof(MPI_Status)"); *found = 0 if unknown */
+int64_t tempi_mpi_constant(const char *name, int *found);
+
+const char *tempi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

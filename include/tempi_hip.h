@@ -1,0 +1,121 @@
+/*
+ * include/tempi_hip.h -- the thin C ABI between TEMPI's C++ host layer
+ * (libtempi.so, the MPI interposer) and the GPU (libtempi_hip.so, hipcc-built
+ * for gfx950). Plain pointers, sizes and integer status codes only: the
+ * interposer never includes a HIP header, and nothing here is CUDA-shaped.
+ *
+ * Status: every function returns 0 on success, otherwise the hipError_t value
+ * (tempi_hip_error_string() names it).
+ *
+ * What each group replaces in the reference:
+ *   pack / unpack kernels   Packer2D/3D launch_pack/launch_unpack
+ *                           (/root/reference/src/internal/packer_2d.cu:21-74,
+ *                            packer_3d.cu:80-116) and the CUDA kernels
+ *                           (/root/reference/include/pack_kernels.cuh:19-120,
+ *                            :350-433), and Packer1D's cudaMemcpyAsync
+ *                           (/root/reference/src/internal/packer_1d.cu:16-49)
+ *   streams / events        /root/reference/src/internal/streams.cpp:19-42,
+ *                           events.cpp:17-83
+ *   memory                  device_allocator / host_allocator
+ *                           (/root/reference/include/allocator_device.hpp:35-53,
+ *                            allocator_host.hpp:31-60)
+ *   pointer attributes      cudaPointerGetAttributes in
+ *                           /root/reference/src/pack.cpp:42-49
+ */
+#ifndef TEMPI_HIP_H
+#define TEMPI_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* maximum number of strided dimensions above the contiguous block (the
+   element count of a Pack call counts as one) */
+#define TEMPI_HIP_MAX_DIMS 5
+
+/* A canonical strided object: `block` contiguous bytes, repeated over `ndims`
+   dimensions listed OUTERMOST FIRST, dimension k having counts[k] elements
+   strides[k] bytes apart (strides may be negative). The packed form is the
+   blocks in row-major (odometer) order, back to back. */
+typedef struct tempi_hip_desc {
+  int64_t block;
+  int32_t ndims;
+  int32_t pad_;
+  int64_t counts[TEMPI_HIP_MAX_DIMS];
+  int64_t strides[TEMPI_HIP_MAX_DIMS];
+} tempi_hip_desc;
+
+/* gather: packed[0 .. bytes) <- strided object whose first byte is `first` */
+int tempi_hip_pack(void *packed, const void *first, const tempi_hip_desc *d,
+                   void *stream);
+/* scatter: strided object whose first byte is `first` <- packed[0 .. bytes) */
+int tempi_hip_unpack(void *first, const void *packed, const tempi_hip_desc *d,
+                     void *stream);
+/* number of packed bytes a descriptor describes */
+int64_t tempi_hip_desc_bytes(const tempi_hip_desc *d);
+/* the word width (1,2,4,8,16) the kernels will use for these pointers */
+int tempi_hip_word_width(const void *packed, const void *first,
+                         const tempi_hip_desc *d);
+
+/* devices */
+int tempi_hip_device_count(int *n);
+int tempi_hip_get_device(int *dev);
+int tempi_hip_set_device(int dev);
+int tempi_hip_device_synchronize(void);
+
+/* pointer classification (reference semantics: "device-accessible" means
+   the GPU can dereference it: device, managed, or mapped pinned host) */
+enum tempi_hip_mem_kind {
+  TEMPI_HIP_MEM_HOST = 0,   /* pageable / unknown host memory */
+  TEMPI_HIP_MEM_DEVICE = 1, /* hipMalloc */
+  TEMPI_HIP_MEM_PINNED = 2, /* registered / hipHostMalloc, mapped */
+  TEMPI_HIP_MEM_MANAGED = 3 /* hipMallocManaged */
+};
+typedef struct tempi_hip_ptrinfo {
+  int kind;           /* tempi_hip_mem_kind */
+  int device;         /* owning device, -1 for host */
+  void *device_ptr;   /* GPU-visible address (NULL when not accessible) */
+} tempi_hip_ptrinfo;
+int tempi_hip_pointer_info(const void *p, tempi_hip_ptrinfo *out);
+
+/* streams and events (opaque handles) */
+int tempi_hip_stream_create(void **stream); /* non-blocking stream */
+int tempi_hip_stream_destroy(void *stream);
+int tempi_hip_stream_synchronize(void *stream);
+int tempi_hip_stream_wait_event(void *stream, void *event);
+/* flags: bit 0 = timing enabled, bit 1 = blocking sync, bit 2 = interprocess */
+int tempi_hip_event_create(void **event, int flags);
+int tempi_hip_event_destroy(void *event);
+int tempi_hip_event_record(void *event, void *stream);
+/* returns 0 when complete, 1 when not ready, otherwise an error */
+int tempi_hip_event_query(void *event);
+int tempi_hip_event_synchronize(void *event);
+int tempi_hip_event_elapsed_ms(float *ms, void *start, void *stop);
+
+/* memory */
+int tempi_hip_malloc(void **p, size_t n);
+int tempi_hip_free(void *p);
+/* pinned, mapped host memory: *host for the CPU, *dev for kernels */
+int tempi_hip_host_alloc(void **host, void **dev, size_t n);
+int tempi_hip_host_free(void *host);
+int tempi_hip_host_register(void *host, size_t n, void **dev);
+int tempi_hip_host_unregister(void *host);
+int tempi_hip_memcpy(void *dst, const void *src, size_t n);
+int tempi_hip_memcpy_async(void *dst, const void *src, size_t n, void *stream);
+int tempi_hip_memset_async(void *dst, int value, size_t n, void *stream);
+
+/* inter-process (same node) device memory: 64-byte opaque handles */
+#define TEMPI_HIP_IPC_HANDLE_BYTES 64
+int tempi_hip_ipc_get_handle(void *handle_out, void *devptr);
+int tempi_hip_ipc_open_handle(void **devptr, const void *handle);
+int tempi_hip_ipc_close_handle(void *devptr);
+
+const char *tempi_hip_error_string(int status);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

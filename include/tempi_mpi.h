@@ -1,0 +1,79 @@
+/*
+ * include/tempi_mpi.h -- THE DROP-IN BOUNDARY: the MPI C entry points that
+ * libtempi.so exports. An unmodified application links `-ltempi` before its
+ * MPI library (or LD_PRELOADs libtempi.so); each call below is handled by
+ * TEMPI when its buffers are GPU-accessible and its datatype canonicalises to
+ * a strided block, and is otherwise forwarded to the next definition in the
+ * link order, found with dlsym(RTLD_NEXT).
+ *
+ * The prototypes are the standard MPI-3 ones from <mpi.h>; the list is the
+ * reference's exported set (/root/reference/include/symbols.hpp:10-174,
+ * `grep 'extern "C"' /root/reference/src`) restricted to the data path, plus
+ * MPI_Init_thread / MPI_Waitall / MPI_Test, which the reference does not
+ * interpose but which must see TEMPI-owned requests.
+ *
+ *   symbol           replaces the reference's        TEMPI behaviour
+ *   MPI_Init         src/init.cpp:22-65              resolve next MPI, env, GPU
+ *   MPI_Init_thread  (not interposed: F8)            same as MPI_Init
+ *   MPI_Finalize     src/finalize.cpp:20-45          drain requests, free pools
+ *   MPI_Type_commit  src/type_commit.cpp:16-114      canonicalise + cache
+ *   MPI_Type_free    src/type_free.cpp:14-27         drop cache entry first
+ *   MPI_Pack         src/pack.cpp:28-68              GPU gather kernel
+ *   MPI_Unpack       src/unpack.cpp:20-59            GPU scatter kernel
+ *   MPI_Send         src/send.cpp:12-17              pack + library send
+ *   MPI_Recv         src/recv.cpp:19-44              library recv + unpack
+ *   MPI_Isend        src/isend.cpp:11-16             async pack -> send
+ *   MPI_Irecv        src/irecv.cpp:11-16             recv -> async unpack
+ *   MPI_Wait         src/wait.cpp:11-16              progress TEMPI requests
+ *   MPI_Waitall      (not interposed: F8)            progress TEMPI requests
+ *   MPI_Test         (not interposed: F8)            progress TEMPI requests
+ *   MPI_Alltoallv    src/alltoallv.cpp:14-68         device-buffer alltoallv
+ *
+ * Not exported (out of scope): MPI_Neighbor_alltoallv (a
+ * pure passthrough in the reference), MPI_Neighbor_alltoallw,
+ * MPI_Dist_graph_create_adjacent / _neighbors, MPI_Comm_rank / _free (rank
+ * placement, a no-op on one node: SURVEY F12). Calls to them reach the MPI
+ * library unchanged.
+ *
+ * Error behaviour: return codes of the library pass through unchanged. Where
+ * TEMPI itself detects an error (a pack that does not fit in outsize) it
+ * raises MPI_ERR_TRUNCATE on the communicator's error handler and returns it
+ * (the reference silently overruns). GPU runtime failures abort with a
+ * message, as the reference does (/root/reference/include/cuda_runtime.hpp:13-20).
+ */
+#ifndef TEMPI_MPI_H
+#define TEMPI_MPI_H
+
+#include <mpi.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+int MPI_Init(int *argc, char ***argv);
+int MPI_Init_thread(int *argc, char ***argv, int required, int *provided);
+int MPI_Finalize(void);
+int MPI_Type_commit(MPI_Datatype *datatype);
+int MPI_Type_free(MPI_Datatype *datatype);
+int MPI_Pack(const void *inbuf, int incount, MPI_Datatype datatype, void *outbuf, int outsize,
+             int *position, MPI_Comm comm);
+int MPI_Unpack(const void *inbuf, int insize, int *position, void *outbuf, int outcount,
+               MPI_Datatype datatype, MPI_Comm comm);
+int MPI_Send(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm);
+int MPI_Recv(void *buf, int count, MPI_Datatype datatype, int source, int tag, MPI_Comm comm,
+             MPI_Status *status);
+int MPI_Isend(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm,
+              MPI_Request *request);
+int MPI_Irecv(void *buf, int count, MPI_Datatype datatype, int source, int tag, MPI_Comm comm,
+              MPI_Request *request);
+int MPI_Wait(MPI_Request *request, MPI_Status *status);
+int MPI_Waitall(int count, MPI_Request array_of_requests[], MPI_Status array_of_statuses[]);
+int MPI_Test(MPI_Request *request, int *flag, MPI_Status *status);
+int MPI_Alltoallv(const void *sendbuf, const int sendcounts[], const int sdispls[],
+                  MPI_Datatype sendtype, void *recvbuf, const int recvcounts[], const int rdispls[],
+                  MPI_Datatype recvtype, MPI_Comm comm);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

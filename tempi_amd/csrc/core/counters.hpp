@@ -1,0 +1,28 @@
+// tempi_amd/csrc/core/counters.hpp -- per-process operation counters, the
+// equivalent of the reference's always-on counters
+// (/root/reference/include/counters.hpp:8-115, dumped at MPI_Finalize by
+// /root/reference/src/internal/counters.cpp:30-121). Read them through
+// tempi_get_counters() (include/tempi_ext.h) or TEMPI_LOG_LEVEL=DEBUG.
+#pragma once
+
+#include <cstdint>
+
+namespace tempi {
+
+struct Counters {
+  uint64_t packs = 0, unpacks = 0;
+  uint64_t pack_bytes = 0, unpack_bytes = 0;
+  uint64_t launches = 0;
+  uint64_t lib_packs = 0, lib_unpacks = 0; // handed to the library
+  uint64_t sends = 0, recvs = 0, isends = 0, irecvs = 0;
+  uint64_t send_device = 0, send_oneshot = 0, send_staged = 0, send_ipc = 0;
+  uint64_t lib_sends = 0, lib_recvs = 0;
+  // kernel time of synchronous MPI_Pack / MPI_Unpack while profiling is on
+  double pack_kernel_ms = 0, unpack_kernel_ms = 0;
+  uint64_t pack_timed = 0, unpack_timed = 0;
+};
+
+extern Counters counters;
+extern bool kernelProfiling;
+
+} // namespace tempi

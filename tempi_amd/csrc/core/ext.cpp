@@ -1,0 +1,117 @@
+// tempi_amd/csrc/core/ext.cpp -- TEMPI's non-MPI entry points
+// (include/tempi_ext.h): type introspection, counters, stream access, and the
+// MPI ABI constants of the library TEMPI was compiled against.
+#include "counters.hpp"
+#include "gpu.hpp"
+#include "state.hpp"
+#include "type_cache.hpp"
+
+#include "tempi_ext.h"
+
+#include <cstring>
+
+#define TEMPI_EXPORT extern "C" __attribute__((visibility("default")))
+
+using namespace tempi;
+
+TEMPI_EXPORT int tempi_type_describe(int64_t datatype, tempi_type_info *out) {
+  std::memset(out, 0, sizeof *out);
+  const TypeRecord *rec = type_lookup(MPI_Datatype(datatype));
+  if (!rec) return 0;
+  out->known = 1;
+  const StridedBlock &sb = rec->desc;
+  out->valid = sb.valid ? 1 : 0;
+  out->start = sb.start;
+  out->block = sb.block;
+  out->size = sb.size;
+  out->lb = sb.lb;
+  out->extent = sb.extent;
+  out->ndims = int32_t(sb.dims.size());
+  if (out->ndims > TEMPI_EXT_MAX_DIMS) {
+    out->ndims = -1;
+    return 0;
+  }
+  for (size_t k = 0; k < sb.dims.size(); ++k) {
+    out->counts[k] = sb.dims[k].count;
+    out->strides[k] = sb.dims[k].stride;
+  }
+  return 1;
+}
+
+TEMPI_EXPORT void tempi_get_counters(tempi_counters_t *o) {
+  const Counters &c = counters;
+  o->packs = c.packs;
+  o->unpacks = c.unpacks;
+  o->pack_bytes = c.pack_bytes;
+  o->unpack_bytes = c.unpack_bytes;
+  o->launches = c.launches;
+  o->lib_packs = c.lib_packs;
+  o->lib_unpacks = c.lib_unpacks;
+  o->sends = c.sends;
+  o->recvs = c.recvs;
+  o->isends = c.isends;
+  o->irecvs = c.irecvs;
+  o->send_device = c.send_device;
+  o->send_oneshot = c.send_oneshot;
+  o->send_staged = c.send_staged;
+  o->send_ipc = c.send_ipc;
+  o->lib_sends = c.lib_sends;
+  o->lib_recvs = c.lib_recvs;
+}
+
+TEMPI_EXPORT void tempi_reset_counters(void) { counters = Counters(); }
+
+TEMPI_EXPORT void tempi_set_kernel_profiling(int on) { kernelProfiling = on != 0; }
+
+TEMPI_EXPORT void tempi_get_kernel_times(tempi_kernel_times *o) {
+  o->pack_ms = counters.pack_kernel_ms;
+  o->unpack_ms = counters.unpack_kernel_ms;
+  o->packs = counters.pack_timed;
+  o->unpacks = counters.unpack_timed;
+}
+
+TEMPI_EXPORT void *tempi_get_stream(int device) { return gpu::available() ? gpu::stream(device) : nullptr; }
+
+TEMPI_EXPORT int tempi_gpu_available(void) { return gpu::available() ? 1 : 0; }
+
+TEMPI_EXPORT const char *tempi_version(void) { return "tempi-mi355x 0.1 (gfx950)"; }
+
+TEMPI_EXPORT int64_t tempi_mpi_constant(const char *name, int *found) {
+  struct C {
+    const char *n;
+    int64_t v;
+  };
+#define H(x) {#x, int64_t(x)}
+#define P(x) {#x, int64_t(reinterpret_cast<intptr_t>(x))}
+  static const C table[] = {
+      H(MPI_SUCCESS), H(MPI_ERR_TRUNCATE), H(MPI_ERR_OTHER), H(MPI_ERR_TYPE),
+      H(MPI_BYTE), H(MPI_CHAR), H(MPI_SHORT), H(MPI_INT), H(MPI_LONG), H(MPI_LONG_LONG),
+      H(MPI_UNSIGNED), H(MPI_FLOAT), H(MPI_DOUBLE), H(MPI_PACKED), H(MPI_INT8_T), H(MPI_INT16_T),
+      H(MPI_INT32_T), H(MPI_INT64_T), H(MPI_UINT8_T), H(MPI_UINT16_T), H(MPI_UINT32_T),
+      H(MPI_UINT64_T), H(MPI_DATATYPE_NULL), H(MPI_COMM_WORLD), H(MPI_COMM_SELF), H(MPI_COMM_NULL),
+      H(MPI_REQUEST_NULL), H(MPI_ORDER_C), H(MPI_ORDER_FORTRAN), H(MPI_ANY_SOURCE), H(MPI_ANY_TAG),
+      H(MPI_PROC_NULL), H(MPI_SUM), H(MPI_MAX), H(MPI_MIN), H(MPI_THREAD_SINGLE),
+      H(MPI_THREAD_FUNNELED), H(MPI_THREAD_SERIALIZED), H(MPI_THREAD_MULTIPLE),
+      H(MPI_MAX_PROCESSOR_NAME), H(MPI_UNDEFINED),
+      P(MPI_STATUS_IGNORE), P(MPI_STATUSES_IGNORE), P(MPI_IN_PLACE),
+      H(MPI_ERRORS_RETURN), H(MPI_ERRORS_ARE_FATAL),
+      {"sizeof(MPI_Status)", int64_t(sizeof(MPI_Status))},
+      {"sizeof(MPI_Aint)", int64_t(sizeof(MPI_Aint))},
+      {"sizeof(MPI_Datatype)", int64_t(sizeof(MPI_Datatype))},
+      {"sizeof(MPI_Comm)", int64_t(sizeof(MPI_Comm))},
+      {"sizeof(MPI_Request)", int64_t(sizeof(MPI_Request))},
+      {"sizeof(MPI_Op)", int64_t(sizeof(MPI_Op))},
+      {"offsetof(MPI_Status,MPI_SOURCE)", int64_t(offsetof(MPI_Status, MPI_SOURCE))},
+      {"offsetof(MPI_Status,MPI_TAG)", int64_t(offsetof(MPI_Status, MPI_TAG))},
+      {"offsetof(MPI_Status,MPI_ERROR)", int64_t(offsetof(MPI_Status, MPI_ERROR))},
+  };
+#undef H
+#undef P
+  for (const C &c : table)
+    if (!std::strcmp(c.n, name)) {
+      if (found) *found = 1;
+      return c.v;
+    }
+  if (found) *found = 0;
+  return 0;
+}

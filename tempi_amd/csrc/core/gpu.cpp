@@ -1,0 +1,91 @@
+// tempi_amd/csrc/core/gpu.cpp -- see gpu.hpp
+#include "gpu.hpp"
+
+#include "log.hpp"
+
+#include <mutex>
+#include <vector>
+
+namespace tempi {
+namespace gpu {
+
+namespace {
+int nDevices = 0;
+std::mutex mtx;
+std::vector<void *> streams;
+std::vector<void *> evStart, evStop;
+} // namespace
+
+bool available() { return nDevices > 0; }
+
+void init() {
+  int n = 0;
+  if (tempi_hip_device_count(&n) != 0) n = 0;
+  nDevices = n;
+  std::lock_guard<std::mutex> g(mtx);
+  streams.assign(size_t(n), nullptr);
+  LOG_DEBUG("visible GPUs: " << n);
+}
+
+void finalize() {
+  std::lock_guard<std::mutex> g(mtx);
+  for (void *s : streams)
+    if (s) tempi_hip_stream_destroy(s);
+  streams.clear();
+  for (auto *v : {&evStart, &evStop}) {
+    for (void *e : *v)
+      if (e) tempi_hip_event_destroy(e);
+    v->clear();
+  }
+}
+
+Ptr classify(const void *p) {
+  Ptr r;
+  if (!nDevices || !p) return r;
+  tempi_hip_ptrinfo info;
+  if (tempi_hip_pointer_info(p, &info) != 0) return r;
+  if (info.kind == TEMPI_HIP_MEM_HOST || !info.device_ptr) return r;
+  r.device_accessible = true;
+  r.host_accessible = info.kind != TEMPI_HIP_MEM_DEVICE;
+  r.device = info.device < 0 ? 0 : info.device;
+  r.dptr = info.device_ptr;
+  return r;
+}
+
+void *stream(int device) {
+  if (device < 0 || device >= nDevices) return nullptr;
+  std::lock_guard<std::mutex> g(mtx);
+  if (!streams[size_t(device)]) {
+    int cur = 0;
+    tempi_hip_get_device(&cur);
+    if (cur != device) tempi_hip_set_device(device);
+    void *s = nullptr;
+    check(tempi_hip_stream_create(&s), "stream create");
+    if (cur != device) tempi_hip_set_device(cur);
+    streams[size_t(device)] = s;
+  }
+  return streams[size_t(device)];
+}
+
+void profiling_events(int device, void **start, void **stop) {
+  *start = *stop = nullptr;
+  if (device < 0 || device >= nDevices) return;
+  std::lock_guard<std::mutex> g(mtx);
+  if (evStart.size() < size_t(nDevices)) {
+    evStart.resize(size_t(nDevices), nullptr);
+    evStop.resize(size_t(nDevices), nullptr);
+  }
+  if (!evStart[size_t(device)]) {
+    check(tempi_hip_event_create(&evStart[size_t(device)], 1), "event create");
+    check(tempi_hip_event_create(&evStop[size_t(device)], 1), "event create");
+  }
+  *start = evStart[size_t(device)];
+  *stop = evStop[size_t(device)];
+}
+
+void check(int status, const char *what) {
+  if (status != 0) LOG_FATAL("HIP error in " << what << ": " << tempi_hip_error_string(status));
+}
+
+} // namespace gpu
+} // namespace tempi

@@ -1,0 +1,279 @@
+// tempi_amd/csrc/core/interpose_core.cpp -- interposed MPI_Init /
+// MPI_Init_thread / MPI_Finalize / MPI_Type_commit / MPI_Type_free /
+// MPI_Pack / MPI_Unpack (declared in include/tempi_mpi.h).
+//
+// Reference behaviour kept: env kill switches first, then dispatch to TEMPI
+// only for committed strided types whose buffers the GPU can reach, else the
+// library (/root/reference/src/pack.cpp:28-68, unpack.cpp:20-59,
+// type_commit.cpp:16-114, type_free.cpp:14-27, init.cpp:22-65).
+// Changed: the pointer test is done on the FIRST BYTE the type touches (the
+// origin itself may lie outside the allocation for offset types), outsize /
+// insize are checked (MPI_ERR_TRUNCATE instead of an overrun), a type with no
+// strided form goes to the library instead of a null packer, and
+// MPI_Init_thread is interposed too (F8).
+#include "counters.hpp"
+#include "env.hpp"
+#include "gpu.hpp"
+#include "log.hpp"
+#include "next_mpi.hpp"
+#include "state.hpp"
+#include "type_cache.hpp"
+
+#include "tempi_mpi.h"
+
+#include <algorithm>
+#include <vector>
+
+#define TEMPI_EXPORT extern "C" __attribute__((visibility("default")))
+
+namespace tempi {
+
+State state;
+Counters counters;
+bool kernelProfiling = false;
+
+int raise_error(MPI_Comm comm, int code) {
+  MPI_Comm_call_errhandler(comm, code);
+  return code;
+}
+
+void async_init();
+void async_finalize();
+void transport_init();
+void transport_finalize();
+
+void init_after_mpi() {
+  if (env.noTempi) return;
+  MPI_Comm_rank(MPI_COMM_WORLD, &state.worldRank);
+  MPI_Comm_size(MPI_COMM_WORLD, &state.worldSize);
+  logRank = state.worldRank;
+  gpu::init();
+  types_init();
+  state.active = true;
+  transport_init();
+  async_init();
+  LOG_DEBUG("TEMPI active: rank " << state.worldRank << "/" << state.worldSize
+                                  << ", GPU " << (gpu::available() ? "yes" : "no"));
+}
+
+void finalize_before_mpi() {
+  if (!state.active) return;
+  async_finalize();
+  transport_finalize();
+  LOG_DEBUG("counters: packs=" << counters.packs << " unpacks=" << counters.unpacks
+                               << " launches=" << counters.launches << " lib_packs="
+                               << counters.lib_packs << " sends=" << counters.sends);
+  types_finalize();
+  gpu::finalize();
+  state.active = false;
+}
+
+namespace {
+
+// run fn on the stream of `device`, with that device current, and wait for
+// it (MPI_Pack / MPI_Unpack are synchronous: /root/reference/src/internal/
+// packer_2d.cu:101-118). With kernel profiling on, HIP events bracket the
+// launches on that stream and their elapsed time is accumulated.
+template <typename F> int on_device(int device, bool pack, F &&fn) {
+  int cur = 0;
+  tempi_hip_get_device(&cur);
+  if (cur != device) tempi_hip_set_device(device);
+  void *s = gpu::stream(device);
+  void *ev0 = nullptr, *ev1 = nullptr;
+  if (kernelProfiling) gpu::profiling_events(device, &ev0, &ev1);
+  if (ev0) tempi_hip_event_record(ev0, s);
+  int e = fn(s);
+  if (ev1) tempi_hip_event_record(ev1, s);
+  if (e == 0) e = tempi_hip_stream_synchronize(s);
+  if (e == 0 && ev0 && ev1) {
+    float ms = 0;
+    if (tempi_hip_event_elapsed_ms(&ms, ev0, ev1) == 0) {
+      if (pack) {
+        counters.pack_kernel_ms += ms;
+        counters.pack_timed++;
+      } else {
+        counters.unpack_kernel_ms += ms;
+        counters.unpack_timed++;
+      }
+    }
+  }
+  if (cur != device) tempi_hip_set_device(cur);
+  return e;
+}
+
+// byte span [lo, hi) relative to the origin touched by `n` elements
+void touched_span(MPI_Datatype t, int n, int64_t *lo, int64_t *hi) {
+  MPI_Aint tlb, text, lb, ext;
+  MPI_Type_get_true_extent(t, &tlb, &text);
+  MPI_Type_get_extent(t, &lb, &ext);
+  const int64_t d = int64_t(n - 1) * int64_t(ext);
+  *lo = int64_t(tlb) + (d < 0 ? d : 0);
+  *hi = int64_t(tlb) + int64_t(text) + (d > 0 ? d : 0);
+}
+
+// The library handles datatypes TEMPI cannot pack (irregular indexed,
+// struct, darray). When one side lives in device-only memory and the library
+// is not GPU-aware (MPICH here), the touched bytes travel through host memory
+// around the library call; host-reachable sides are used in place.
+int library_pack(const void *inbuf, int incount, MPI_Datatype t, void *outbuf, int outsize,
+                 int *position, MPI_Comm comm) {
+  counters.lib_packs++;
+  int64_t lo, hi;
+  touched_span(t, incount, &lo, &hi);
+  const gpu::Ptr in = gpu::classify(static_cast<const char *>(inbuf) + lo);
+  const gpu::Ptr out = gpu::classify(static_cast<char *>(outbuf) + *position);
+  if ((!in.device_accessible || in.host_accessible) && (!out.device_accessible || out.host_accessible))
+    return next.MPI_Pack(inbuf, incount, t, outbuf, outsize, position, comm);
+  std::vector<char> hin, hout;
+  const char *src = static_cast<const char *>(inbuf);
+  if (in.device_accessible && !in.host_accessible) {
+    hin.resize(size_t(hi - lo));
+    gpu::check(tempi_hip_memcpy(hin.data(), src + lo, size_t(hi - lo)), "library pack D2H");
+    src = hin.data() - lo;
+  }
+  int size = 0;
+  MPI_Pack_size(incount, t, comm, &size);
+  if (!(out.device_accessible && !out.host_accessible))
+    return next.MPI_Pack(src, incount, t, outbuf, outsize, position, comm);
+  hout.resize(size_t(size > 0 ? size : 1));
+  int pos = 0;
+  const int rc = next.MPI_Pack(src, incount, t, hout.data(), size, &pos, comm);
+  if (rc != MPI_SUCCESS) return rc;
+  if (int64_t(*position) + pos > outsize) return raise_error(comm, MPI_ERR_TRUNCATE);
+  gpu::check(tempi_hip_memcpy(static_cast<char *>(outbuf) + *position, hout.data(), size_t(pos)),
+             "library pack H2D");
+  *position += pos;
+  return MPI_SUCCESS;
+}
+
+int library_unpack(const void *inbuf, int insize, int *position, void *outbuf, int outcount,
+                   MPI_Datatype t, MPI_Comm comm) {
+  counters.lib_unpacks++;
+  int64_t lo, hi;
+  touched_span(t, outcount, &lo, &hi);
+  const gpu::Ptr in = gpu::classify(static_cast<const char *>(inbuf) + *position);
+  const gpu::Ptr out = gpu::classify(static_cast<char *>(outbuf) + lo);
+  if ((!in.device_accessible || in.host_accessible) && (!out.device_accessible || out.host_accessible))
+    return next.MPI_Unpack(inbuf, insize, position, outbuf, outcount, t, comm);
+  int size = 0;
+  MPI_Pack_size(outcount, t, comm, &size);
+  std::vector<char> hin, hout;
+  const char *src = static_cast<const char *>(inbuf);
+  int srcsize = insize, pos = *position;
+  if (in.device_accessible && !in.host_accessible) {
+    const int64_t n = std::min<int64_t>(size, int64_t(insize) - *position);
+    if (n < 0) return raise_error(comm, MPI_ERR_TRUNCATE);
+    hin.resize(size_t(n > 0 ? n : 1));
+    gpu::check(tempi_hip_memcpy(hin.data(), src + *position, size_t(n)), "library unpack D2H");
+    src = hin.data();
+    srcsize = int(n);
+    pos = 0;
+  }
+  char *dst = static_cast<char *>(outbuf);
+  const bool stageOut = out.device_accessible && !out.host_accessible;
+  if (stageOut) { // read-modify-write: bytes between blocks keep their values
+    hout.resize(size_t(hi - lo));
+    gpu::check(tempi_hip_memcpy(hout.data(), dst + lo, size_t(hi - lo)), "library unpack D2H");
+    dst = hout.data() - lo;
+  }
+  const int before = pos;
+  const int rc = next.MPI_Unpack(src, srcsize, &pos, dst, outcount, t, comm);
+  if (rc != MPI_SUCCESS) return rc;
+  if (stageOut)
+    gpu::check(tempi_hip_memcpy(static_cast<char *>(outbuf) + lo, hout.data(), size_t(hi - lo)),
+               "library unpack H2D");
+  *position += pos - before;
+  return MPI_SUCCESS;
+}
+
+} // namespace
+} // namespace tempi
+
+using namespace tempi;
+
+TEMPI_EXPORT int MPI_Init(int *argc, char ***argv) {
+  resolve_next();
+  read_environment();
+  const int rc = next.MPI_Init(argc, argv);
+  if (rc == MPI_SUCCESS) init_after_mpi();
+  return rc;
+}
+
+TEMPI_EXPORT int MPI_Init_thread(int *argc, char ***argv, int required, int *provided) {
+  resolve_next();
+  read_environment();
+  const int rc = next.MPI_Init_thread(argc, argv, required, provided);
+  if (rc == MPI_SUCCESS) init_after_mpi();
+  return rc;
+}
+
+TEMPI_EXPORT int MPI_Finalize(void) {
+  resolve_next();
+  finalize_before_mpi();
+  return next.MPI_Finalize();
+}
+
+TEMPI_EXPORT int MPI_Type_commit(MPI_Datatype *datatype) {
+  resolve_next();
+  const int rc = next.MPI_Type_commit(datatype);
+  if (rc != MPI_SUCCESS || !state.active || env.noTypeCommit) return rc;
+  type_commit(*datatype);
+  return rc;
+}
+
+TEMPI_EXPORT int MPI_Type_free(MPI_Datatype *datatype) {
+  resolve_next();
+  // the library may hand the handle out again: forget it first
+  if (state.active && !env.noTypeCommit) type_release(*datatype);
+  return next.MPI_Type_free(datatype);
+}
+
+TEMPI_EXPORT int MPI_Pack(const void *inbuf, int incount, MPI_Datatype datatype, void *outbuf,
+                          int outsize, int *position, MPI_Comm comm) {
+  resolve_next();
+  if (!state.active || env.noPack || incount <= 0 || !position)
+    return next.MPI_Pack(inbuf, incount, datatype, outbuf, outsize, position, comm);
+  const TypeRecord *rec = type_lookup(datatype);
+  if (!rec || !rec->packer || rec->desc.size == 0)
+    return library_pack(inbuf, incount, datatype, outbuf, outsize, position, comm);
+  const char *first = static_cast<const char *>(inbuf) + rec->desc.start;
+  const gpu::Ptr src = gpu::classify(first);
+  const gpu::Ptr dst = gpu::classify(static_cast<char *>(outbuf) + *position);
+  if (!src.device_accessible || !dst.device_accessible)
+    return library_pack(inbuf, incount, datatype, outbuf, outsize, position, comm);
+  const int64_t bytes = rec->packer->packed_bytes(incount);
+  if (*position < 0 || int64_t(*position) + bytes > int64_t(outsize))
+    return raise_error(comm, MPI_ERR_TRUNCATE);
+  const char *origin = static_cast<const char *>(src.dptr) - rec->desc.start;
+  const int e = on_device(src.device, true, [&](void *s) {
+    return rec->packer->pack_async(dst.dptr, origin, incount, s);
+  });
+  gpu::check(e, "MPI_Pack");
+  *position += int(bytes);
+  return MPI_SUCCESS;
+}
+
+TEMPI_EXPORT int MPI_Unpack(const void *inbuf, int insize, int *position, void *outbuf, int outcount,
+                            MPI_Datatype datatype, MPI_Comm comm) {
+  resolve_next();
+  if (!state.active || env.noPack || outcount <= 0 || !position)
+    return next.MPI_Unpack(inbuf, insize, position, outbuf, outcount, datatype, comm);
+  const TypeRecord *rec = type_lookup(datatype);
+  if (!rec || !rec->packer || rec->desc.size == 0)
+    return library_unpack(inbuf, insize, position, outbuf, outcount, datatype, comm);
+  char *first = static_cast<char *>(outbuf) + rec->desc.start;
+  const gpu::Ptr dst = gpu::classify(first);
+  const gpu::Ptr src = gpu::classify(static_cast<const char *>(inbuf) + *position);
+  if (!src.device_accessible || !dst.device_accessible)
+    return library_unpack(inbuf, insize, position, outbuf, outcount, datatype, comm);
+  const int64_t bytes = rec->packer->packed_bytes(outcount);
+  if (*position < 0 || int64_t(*position) + bytes > int64_t(insize))
+    return raise_error(comm, MPI_ERR_TRUNCATE);
+  char *origin = static_cast<char *>(dst.dptr) - rec->desc.start;
+  const int e = on_device(dst.device, false, [&](void *s) {
+    return rec->packer->unpack_async(origin, src.dptr, outcount, s);
+  });
+  gpu::check(e, "MPI_Unpack");
+  *position += int(bytes);
+  return MPI_SUCCESS;
+}

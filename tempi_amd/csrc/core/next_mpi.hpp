@@ -1,0 +1,44 @@
+// tempi_amd/csrc/core/next_mpi.hpp -- the MPI library underneath TEMPI.
+//
+// Every MPI symbol TEMPI exports is resolved to the NEXT definition in the
+// dynamic-link search order with dlsym(RTLD_NEXT, ...), as the reference does
+// (/root/reference/src/internal/symbols.cpp:14-51) -- not through PMPI, so
+// TEMPI chains with PMPI tools. When RTLD_NEXT finds nothing (libtempi was
+// dlopen'ed after the MPI library, e.g. from Python), the MPI library named by
+// TEMPI_MPI_LIBRARY (default libmpi.so.12) is searched directly. A definition
+// that lives in libtempi itself is never accepted (no self-recursion).
+#pragma once
+
+#include <mpi.h>
+
+#define TEMPI_NEXT_FUNCS(X)                                                    \
+  X(MPI_Init)                                                                  \
+  X(MPI_Init_thread)                                                           \
+  X(MPI_Finalize)                                                              \
+  X(MPI_Type_commit)                                                           \
+  X(MPI_Type_free)                                                             \
+  X(MPI_Pack)                                                                  \
+  X(MPI_Unpack)                                                                \
+  X(MPI_Send)                                                                  \
+  X(MPI_Recv)                                                                  \
+  X(MPI_Isend)                                                                 \
+  X(MPI_Irecv)                                                                 \
+  X(MPI_Wait)                                                                  \
+  X(MPI_Waitall)                                                               \
+  X(MPI_Test)                                                                  \
+  X(MPI_Alltoallv)
+
+namespace tempi {
+
+struct NextMPI {
+#define TEMPI_X(f) decltype(&::f) f = nullptr;
+  TEMPI_NEXT_FUNCS(TEMPI_X)
+#undef TEMPI_X
+};
+
+extern NextMPI next;
+
+// idempotent; aborts if a symbol cannot be found anywhere
+void resolve_next();
+
+} // namespace tempi

@@ -1,0 +1,69 @@
+// tempi_amd/csrc/core/packer.cpp -- see packer.hpp
+#include "packer.hpp"
+
+#include "counters.hpp"
+#include "tempi_hip.h"
+
+#include <vector>
+
+namespace tempi {
+
+namespace {
+
+// issue one launch per index of the outermost dims until the rest fits
+int issue(bool pack, char *packed, char *first, int64_t block, const Dim *dims, int nd,
+          void *stream) {
+  if (nd <= TEMPI_HIP_MAX_DIMS) {
+    tempi_hip_desc d{};
+    d.block = block;
+    d.ndims = nd;
+    for (int k = 0; k < nd; ++k) {
+      d.counts[k] = dims[k].count;
+      d.strides[k] = dims[k].stride;
+    }
+    counters.launches++;
+    return pack ? tempi_hip_pack(packed, first, &d, stream) : tempi_hip_unpack(first, packed, &d, stream);
+  }
+  int64_t inner = block;
+  for (int k = 1; k < nd; ++k) inner *= dims[k].count;
+  for (int64_t i = 0; i < dims[0].count; ++i) {
+    if (int e = issue(pack, packed + i * inner, first + i * dims[0].stride, block, dims + 1, nd - 1, stream))
+      return e;
+  }
+  return 0;
+}
+
+} // namespace
+
+int Packer::launch(bool pack, char *packed, char *origin, int64_t count, void *stream) const {
+  if (count <= 0 || sb_.size == 0) return 0;
+  std::vector<Dim> dims;
+  dims.reserve(sb_.dims.size() + 1);
+  if (count > 1) dims.push_back(Dim{count, sb_.extent});
+  dims.insert(dims.end(), sb_.dims.begin(), sb_.dims.end());
+  StridedBlock tmp;
+  tmp.block = sb_.block;
+  tmp.dims = dims;
+  simplify(tmp); // the count dimension may merge (e.g. dense types)
+  const int64_t bytes = packed_bytes(count);
+  if (pack) {
+    counters.packs++;
+    counters.pack_bytes += uint64_t(bytes);
+  } else {
+    counters.unpacks++;
+    counters.unpack_bytes += uint64_t(bytes);
+  }
+  return issue(pack, packed, origin + sb_.start, tmp.block, tmp.dims.data(), int(tmp.dims.size()), stream);
+}
+
+int Packer::pack_async(void *packed, const void *origin, int64_t count, void *stream) const {
+  return launch(true, static_cast<char *>(packed), const_cast<char *>(static_cast<const char *>(origin)),
+                count, stream);
+}
+
+int Packer::unpack_async(void *origin, const void *packed, int64_t count, void *stream) const {
+  return launch(false, const_cast<char *>(static_cast<const char *>(packed)), static_cast<char *>(origin),
+                count, stream);
+}
+
+} // namespace tempi

@@ -1,0 +1,37 @@
+// tempi_amd/csrc/core/packer.hpp -- pack / unpack of `count` elements of a
+// canonical type on a TEMPI stream.
+//
+// Replaces the reference's Packer hierarchy (/root/reference/include/
+// packer.hpp:14-49, packer_1d/2d/3d): one object serves every
+// dimensionality, because the element count is folded in as the outermost
+// dimension (stride = extent) and the GPU layer handles any rank up to
+// TEMPI_HIP_MAX_DIMS; deeper types are issued as several launches.
+#pragma once
+
+#include "types.hpp"
+
+#include <cstdint>
+
+namespace tempi {
+
+struct PackStats;
+
+class Packer {
+public:
+  explicit Packer(const StridedBlock &sb) : sb_(sb) {}
+
+  int64_t packed_bytes(int64_t count) const { return sb_.size * count; }
+
+  // enqueue: packed[0..bytes) <- `count` elements at `origin` (GPU-visible
+  // addresses). Returns 0 or a tempi_hip status.
+  int pack_async(void *packed, const void *origin, int64_t count, void *stream) const;
+  int unpack_async(void *origin, const void *packed, int64_t count, void *stream) const;
+
+  const StridedBlock &desc() const { return sb_; }
+
+private:
+  int launch(bool pack, char *packed, char *origin, int64_t count, void *stream) const;
+  StridedBlock sb_;
+};
+
+} // namespace tempi

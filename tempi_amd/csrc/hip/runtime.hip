@@ -1,0 +1,154 @@
+// tempi_amd/csrc/hip/runtime.hip -- HIP runtime half of the C ABI in
+// include/tempi_hip.h: devices, pointer classification, streams, events,
+// device / pinned-mapped host memory and IPC handles. The C++ interposer
+// (libtempi.so) reaches the GPU only through these.
+//
+// Reference counterparts: streams_init (/root/reference/src/internal/
+// streams.cpp:19-28, two non-blocking streams), the event pool flags
+// (/root/reference/src/internal/events.cpp:64-65), the allocators'
+// cudaMalloc / cudaHostRegister(Mapped) (/root/reference/include/
+// allocator_device.hpp:35-43, allocator_host.hpp:31-49), and the pointer test
+// of MPI_Pack (/root/reference/src/pack.cpp:42-49).
+#include <hip/hip_runtime.h>
+
+#include "tempi_hip.h"
+
+#include <cstring>
+
+#define RET(expr) return int(expr)
+
+extern "C" {
+
+int tempi_hip_device_count(int *n) {
+  hipError_t e = hipGetDeviceCount(n);
+  if (e != hipSuccess) {
+    *n = 0;
+    (void)hipGetLastError();
+  }
+  return int(e);
+}
+int tempi_hip_get_device(int *dev) { RET(hipGetDevice(dev)); }
+int tempi_hip_set_device(int dev) { RET(hipSetDevice(dev)); }
+int tempi_hip_device_synchronize(void) { RET(hipDeviceSynchronize()); }
+
+int tempi_hip_pointer_info(const void *p, tempi_hip_ptrinfo *out) {
+  out->kind = TEMPI_HIP_MEM_HOST;
+  out->device = -1;
+  out->device_ptr = nullptr;
+  if (!p) return 0;
+  hipPointerAttribute_t a;
+  std::memset(&a, 0, sizeof a);
+  hipError_t e = hipPointerGetAttributes(&a, p);
+  if (e != hipSuccess) {
+    (void)hipGetLastError(); // unregistered host memory: not an error for us
+    return 0;
+  }
+  switch (a.type) {
+  case hipMemoryTypeDevice:
+    out->kind = TEMPI_HIP_MEM_DEVICE;
+    break;
+  case hipMemoryTypeHost:
+    out->kind = TEMPI_HIP_MEM_PINNED;
+    break;
+  case hipMemoryTypeManaged:
+  case hipMemoryTypeUnified:
+    out->kind = TEMPI_HIP_MEM_MANAGED;
+    break;
+  default:
+    return 0; // unregistered
+  }
+  out->device = a.device;
+  out->device_ptr = a.devicePointer;
+  if (!out->device_ptr) out->kind = TEMPI_HIP_MEM_HOST;
+  return 0;
+}
+
+int tempi_hip_stream_create(void **stream) {
+  hipStream_t s = nullptr;
+  hipError_t e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+  *stream = s;
+  RET(e);
+}
+int tempi_hip_stream_destroy(void *stream) { RET(hipStreamDestroy(static_cast<hipStream_t>(stream))); }
+int tempi_hip_stream_synchronize(void *stream) {
+  RET(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+}
+int tempi_hip_stream_wait_event(void *stream, void *event) {
+  RET(hipStreamWaitEvent(static_cast<hipStream_t>(stream), static_cast<hipEvent_t>(event), 0));
+}
+
+int tempi_hip_event_create(void **event, int flags) {
+  unsigned f = 0;
+  if (!(flags & 1)) f |= hipEventDisableTiming;
+  if (flags & 2) f |= hipEventBlockingSync;
+  if (flags & 4) f |= hipEventInterprocess | hipEventDisableTiming;
+  hipEvent_t ev = nullptr;
+  hipError_t e = hipEventCreateWithFlags(&ev, f);
+  *event = ev;
+  RET(e);
+}
+int tempi_hip_event_destroy(void *event) { RET(hipEventDestroy(static_cast<hipEvent_t>(event))); }
+int tempi_hip_event_record(void *event, void *stream) {
+  RET(hipEventRecord(static_cast<hipEvent_t>(event), static_cast<hipStream_t>(stream)));
+}
+int tempi_hip_event_query(void *event) {
+  hipError_t e = hipEventQuery(static_cast<hipEvent_t>(event));
+  if (e == hipSuccess) return 0;
+  if (e == hipErrorNotReady) {
+    (void)hipGetLastError();
+    return 1;
+  }
+  return int(e);
+}
+int tempi_hip_event_synchronize(void *event) { RET(hipEventSynchronize(static_cast<hipEvent_t>(event))); }
+int tempi_hip_event_elapsed_ms(float *ms, void *start, void *stop) {
+  RET(hipEventElapsedTime(ms, static_cast<hipEvent_t>(start), static_cast<hipEvent_t>(stop)));
+}
+
+int tempi_hip_malloc(void **p, size_t n) { RET(hipMalloc(p, n ? n : 1)); }
+int tempi_hip_free(void *p) { RET(hipFree(p)); }
+
+int tempi_hip_host_alloc(void **host, void **dev, size_t n) {
+  hipError_t e = hipHostMalloc(host, n ? n : 1, hipHostMallocMapped | hipHostMallocPortable);
+  if (e != hipSuccess) RET(e);
+  RET(hipHostGetDevicePointer(dev, *host, 0));
+}
+int tempi_hip_host_free(void *host) { RET(hipHostFree(host)); }
+int tempi_hip_host_register(void *host, size_t n, void **dev) {
+  hipError_t e = hipHostRegister(host, n, hipHostRegisterMapped | hipHostRegisterPortable);
+  if (e != hipSuccess) RET(e);
+  RET(hipHostGetDevicePointer(dev, host, 0));
+}
+int tempi_hip_host_unregister(void *host) { RET(hipHostUnregister(host)); }
+
+int tempi_hip_memcpy(void *dst, const void *src, size_t n) {
+  RET(hipMemcpy(dst, src, n, hipMemcpyDefault));
+}
+int tempi_hip_memcpy_async(void *dst, const void *src, size_t n, void *stream) {
+  RET(hipMemcpyAsync(dst, src, n, hipMemcpyDefault, static_cast<hipStream_t>(stream)));
+}
+int tempi_hip_memset_async(void *dst, int value, size_t n, void *stream) {
+  RET(hipMemsetAsync(dst, value, n, static_cast<hipStream_t>(stream)));
+}
+
+int tempi_hip_ipc_get_handle(void *handle_out, void *devptr) {
+  static_assert(sizeof(hipIpcMemHandle_t) <= TEMPI_HIP_IPC_HANDLE_BYTES, "ipc handle size");
+  hipIpcMemHandle_t h;
+  std::memset(&h, 0, sizeof h);
+  hipError_t e = hipIpcGetMemHandle(&h, devptr);
+  std::memset(handle_out, 0, TEMPI_HIP_IPC_HANDLE_BYTES);
+  std::memcpy(handle_out, &h, sizeof h);
+  RET(e);
+}
+int tempi_hip_ipc_open_handle(void **devptr, const void *handle) {
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, handle, sizeof h);
+  RET(hipIpcOpenMemHandle(devptr, h, hipIpcMemLazyEnablePeerAccess));
+}
+int tempi_hip_ipc_close_handle(void *devptr) { RET(hipIpcCloseMemHandle(devptr)); }
+
+const char *tempi_hip_error_string(int status) {
+  return hipGetErrorString(static_cast<hipError_t>(status));
+}
+
+} // extern "C"

@@ -1,0 +1,337 @@
+"""ctypes binding of libtempi.so: the MPI C API as TEMPI exports it.
+
+Every call goes through libtempi.so, so interposed functions (MPI_Pack,
+MPI_Send, ...) run TEMPI's code and everything else resolves to the MPI
+library libtempi.so was linked against (MPICH ABI: handles are C ints).
+Buffers are raw addresses (ints): pass ``tensor.data_ptr()`` for GPU memory
+or ``array.ctypes.data`` for host memory.
+"""
+import ctypes
+import os
+
+from . import LIBTEMPI, require_built
+
+_singleton = None
+
+
+class MPIError(RuntimeError):
+    def __init__(self, fn, code):
+        super().__init__(f"{fn} returned MPI error {code}")
+        self.code = code
+
+
+class TypeInfo(ctypes.Structure):
+    _fields_ = [
+        ("known", ctypes.c_int32),
+        ("valid", ctypes.c_int32),
+        ("ndims", ctypes.c_int32),
+        ("pad_", ctypes.c_int32),
+        ("start", ctypes.c_int64),
+        ("block", ctypes.c_int64),
+        ("size", ctypes.c_int64),
+        ("lb", ctypes.c_int64),
+        ("extent", ctypes.c_int64),
+        ("counts", ctypes.c_int64 * 16),
+        ("strides", ctypes.c_int64 * 16),
+    ]
+
+
+_COUNTER_FIELDS = [
+    "packs", "unpacks", "pack_bytes", "unpack_bytes", "launches", "lib_packs", "lib_unpacks",
+    "sends", "recvs", "isends", "irecvs", "send_device", "send_oneshot", "send_staged",
+    "send_ipc", "lib_sends", "lib_recvs",
+]
+
+
+class Counters(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint64) for n in _COUNTER_FIELDS]
+
+
+class KernelTimes(ctypes.Structure):
+    _fields_ = [("pack_ms", ctypes.c_double), ("unpack_ms", ctypes.c_double),
+                ("packs", ctypes.c_uint64), ("unpacks", ctypes.c_uint64)]
+
+
+class MPI:
+    """Thin wrapper: one method per MPI call used by tests / benchmarks."""
+
+    def __init__(self, path=LIBTEMPI):
+        require_built()
+        self.L = ctypes.CDLL(path, mode=os.RTLD_NOW | ctypes.RTLD_GLOBAL)
+        L = self.L
+        L.tempi_mpi_constant.restype = ctypes.c_int64
+        L.tempi_mpi_constant.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)]
+        for name in ("MPI_Datatype", "MPI_Comm", "MPI_Request", "MPI_Aint", "MPI_Op"):
+            assert self.const(f"sizeof({name})") in (4, 8)
+        self.Handle = ctypes.c_int if self.const("sizeof(MPI_Datatype)") == 4 else ctypes.c_int64
+        self.Request = ctypes.c_int if self.const("sizeof(MPI_Request)") == 4 else ctypes.c_int64
+        self.Aint = ctypes.c_int64
+        self.status_size = self.const("sizeof(MPI_Status)")
+        for n in ("BYTE", "CHAR", "SHORT", "INT", "LONG", "FLOAT", "DOUBLE", "PACKED", "INT64_T",
+                  "UINT8_T", "COMM_WORLD", "COMM_SELF", "REQUEST_NULL", "ORDER_C", "ORDER_FORTRAN",
+                  "SUCCESS", "ERR_TRUNCATE", "ANY_SOURCE", "ANY_TAG", "SUM", "MAX", "MIN",
+                  "DATATYPE_NULL", "PROC_NULL"):
+            setattr(self, n, self.const("MPI_" + n))
+        self.STATUS_IGNORE = ctypes.c_void_p(self.const("MPI_STATUS_IGNORE"))
+        self.STATUSES_IGNORE = ctypes.c_void_p(self.const("MPI_STATUSES_IGNORE"))
+        self.IN_PLACE = ctypes.c_void_p(self.const("MPI_IN_PLACE"))
+        L.tempi_type_describe.argtypes = [ctypes.c_int64, ctypes.POINTER(TypeInfo)]
+        L.tempi_get_stream.restype = ctypes.c_void_p
+        L.tempi_get_stream.argtypes = [ctypes.c_int]
+        L.tempi_version.restype = ctypes.c_char_p
+        L.MPI_Wtime.restype = ctypes.c_double
+        self.initialized = False
+
+    # ------------------------------------------------------------- plumbing
+    def const(self, name):
+        found = ctypes.c_int(0)
+        v = self.L.tempi_mpi_constant(name.encode(), ctypes.byref(found))
+        if not found.value:
+            raise KeyError(name)
+        return v
+
+    def _chk(self, fn, rc):
+        if rc != 0:
+            raise MPIError(fn, rc)
+
+    def _call(self, fn, *args):
+        rc = getattr(self.L, fn)(*args)
+        self._chk(fn, rc)
+
+    def h(self, v):
+        return self.Handle(v)
+
+    # ------------------------------------------------------------ lifecycle
+    def Init(self):
+        if not self.initialized:
+            self._call("MPI_Init", None, None)
+            self.initialized = True
+
+    def Finalize(self):
+        if self.initialized:
+            self._call("MPI_Finalize")
+            self.initialized = False
+
+    def Initialized(self):
+        f = ctypes.c_int(0)
+        self._call("MPI_Initialized", ctypes.byref(f))
+        return bool(f.value)
+
+    def Comm_rank(self, comm=None):
+        r = ctypes.c_int()
+        self._call("MPI_Comm_rank", self.h(self.COMM_WORLD if comm is None else comm), ctypes.byref(r))
+        return r.value
+
+    def Comm_size(self, comm=None):
+        r = ctypes.c_int()
+        self._call("MPI_Comm_size", self.h(self.COMM_WORLD if comm is None else comm), ctypes.byref(r))
+        return r.value
+
+    def Barrier(self, comm=None):
+        self._call("MPI_Barrier", self.h(self.COMM_WORLD if comm is None else comm))
+
+    def Wtime(self):
+        return self.L.MPI_Wtime()
+
+    def Allreduce_double(self, value, op=None, comm=None):
+        x = ctypes.c_double(value)
+        y = ctypes.c_double()
+        self._call("MPI_Allreduce", ctypes.byref(x), ctypes.byref(y), 1, self.h(self.DOUBLE),
+                   self.h(self.MAX if op is None else op), self.h(self.COMM_WORLD if comm is None else comm))
+        return y.value
+
+    # ----------------------------------------------------------- datatypes
+    def _newtype(self, fn, *args):
+        out = self.Handle()
+        self._call(fn, *args, ctypes.byref(out))
+        return out.value
+
+    def Type_contiguous(self, n, old):
+        return self._newtype("MPI_Type_contiguous", n, self.h(old))
+
+    def Type_vector(self, n, bl, stride, old):
+        return self._newtype("MPI_Type_vector", n, bl, stride, self.h(old))
+
+    def Type_create_hvector(self, n, bl, stride, old):
+        return self._newtype("MPI_Type_create_hvector", n, bl, self.Aint(stride), self.h(old))
+
+    def Type_create_subarray(self, sizes, subsizes, starts, order, old):
+        n = len(sizes)
+        A = ctypes.c_int * n
+        return self._newtype("MPI_Type_create_subarray", n, A(*sizes), A(*subsizes), A(*starts), order,
+                             self.h(old))
+
+    def Type_create_resized(self, old, lb, extent):
+        return self._newtype("MPI_Type_create_resized", self.h(old), self.Aint(lb), self.Aint(extent))
+
+    def Type_dup(self, old):
+        return self._newtype("MPI_Type_dup", self.h(old))
+
+    def Type_indexed(self, bls, disps, old):
+        n = len(bls)
+        A = ctypes.c_int * max(n, 1)
+        return self._newtype("MPI_Type_indexed", n, A(*bls), A(*disps), self.h(old))
+
+    def Type_create_hindexed(self, bls, disps, old):
+        n = len(bls)
+        return self._newtype("MPI_Type_create_hindexed", n, (ctypes.c_int * max(n, 1))(*bls),
+                             (ctypes.c_int64 * max(n, 1))(*disps), self.h(old))
+
+    def Type_create_indexed_block(self, bl, disps, old):
+        n = len(disps)
+        return self._newtype("MPI_Type_create_indexed_block", n, bl, (ctypes.c_int * max(n, 1))(*disps),
+                             self.h(old))
+
+    def Type_create_hindexed_block(self, bl, disps, old):
+        n = len(disps)
+        return self._newtype("MPI_Type_create_hindexed_block", n, bl, (ctypes.c_int64 * max(n, 1))(*disps),
+                             self.h(old))
+
+    def Type_commit(self, t):
+        x = self.Handle(t)
+        self._call("MPI_Type_commit", ctypes.byref(x))
+        return x.value
+
+    def Type_free(self, t):
+        x = self.Handle(t)
+        self._call("MPI_Type_free", ctypes.byref(x))
+
+    def Type_size(self, t):
+        s = ctypes.c_int()
+        self._call("MPI_Type_size", self.h(t), ctypes.byref(s))
+        return s.value
+
+    def Type_get_extent(self, t):
+        lb, ext = self.Aint(), self.Aint()
+        self._call("MPI_Type_get_extent", self.h(t), ctypes.byref(lb), ctypes.byref(ext))
+        return lb.value, ext.value
+
+    def Type_get_true_extent(self, t):
+        lb, ext = self.Aint(), self.Aint()
+        self._call("MPI_Type_get_true_extent", self.h(t), ctypes.byref(lb), ctypes.byref(ext))
+        return lb.value, ext.value
+
+    # ---------------------------------------------------------- pack path
+    def Pack_size(self, count, t, comm=None):
+        s = ctypes.c_int()
+        self._call("MPI_Pack_size", count, self.h(t), self.h(self.COMM_WORLD if comm is None else comm),
+                   ctypes.byref(s))
+        return s.value
+
+    def Pack(self, inbuf, incount, t, outbuf, outsize, position=0, comm=None):
+        """returns the new position"""
+        pos = ctypes.c_int(position)
+        self._call("MPI_Pack", ctypes.c_void_p(inbuf), incount, self.h(t), ctypes.c_void_p(outbuf), outsize,
+                   ctypes.byref(pos), self.h(self.COMM_WORLD if comm is None else comm))
+        return pos.value
+
+    def Unpack(self, inbuf, insize, position, outbuf, outcount, t, comm=None):
+        pos = ctypes.c_int(position)
+        self._call("MPI_Unpack", ctypes.c_void_p(inbuf), insize, ctypes.byref(pos), ctypes.c_void_p(outbuf),
+                   outcount, self.h(t), self.h(self.COMM_WORLD if comm is None else comm))
+        return pos.value
+
+    def Pack_rc(self, inbuf, incount, t, outbuf, outsize, position=0, comm=None):
+        """MPI_Pack returning (rc, position) without raising"""
+        pos = ctypes.c_int(position)
+        rc = self.L.MPI_Pack(ctypes.c_void_p(inbuf), incount, self.h(t), ctypes.c_void_p(outbuf), outsize,
+                             ctypes.byref(pos), self.h(self.COMM_WORLD if comm is None else comm))
+        return rc, pos.value
+
+    # ------------------------------------------------------ point to point
+    def _status(self):
+        return (ctypes.c_char * self.status_size)()
+
+    def Send(self, buf, count, t, dest, tag, comm=None):
+        self._call("MPI_Send", ctypes.c_void_p(buf), count, self.h(t), dest, tag,
+                   self.h(self.COMM_WORLD if comm is None else comm))
+
+    def Recv(self, buf, count, t, source, tag, comm=None):
+        self._call("MPI_Recv", ctypes.c_void_p(buf), count, self.h(t), source, tag,
+                   self.h(self.COMM_WORLD if comm is None else comm), self.STATUS_IGNORE)
+
+    def Isend(self, buf, count, t, dest, tag, comm=None):
+        r = self.Request()
+        self._call("MPI_Isend", ctypes.c_void_p(buf), count, self.h(t), dest, tag,
+                   self.h(self.COMM_WORLD if comm is None else comm), ctypes.byref(r))
+        return r.value
+
+    def Irecv(self, buf, count, t, source, tag, comm=None):
+        r = self.Request()
+        self._call("MPI_Irecv", ctypes.c_void_p(buf), count, self.h(t), source, tag,
+                   self.h(self.COMM_WORLD if comm is None else comm), ctypes.byref(r))
+        return r.value
+
+    def Wait(self, req):
+        r = self.Request(req)
+        self._call("MPI_Wait", ctypes.byref(r), self.STATUS_IGNORE)
+        return r.value
+
+    def Waitall(self, reqs):
+        n = len(reqs)
+        arr = (self.Request * max(n, 1))(*reqs)
+        self._call("MPI_Waitall", n, arr, self.STATUSES_IGNORE)
+        return list(arr)[:n]
+
+    def Test(self, req):
+        r = self.Request(req)
+        flag = ctypes.c_int(0)
+        self._call("MPI_Test", ctypes.byref(r), ctypes.byref(flag), self.STATUS_IGNORE)
+        return bool(flag.value), r.value
+
+    def Alltoallv(self, sbuf, scounts, sdispls, stype, rbuf, rcounts, rdispls, rtype, comm=None):
+        n = len(scounts)
+        A = ctypes.c_int * n
+        self._call("MPI_Alltoallv", ctypes.c_void_p(sbuf), A(*scounts), A(*sdispls), self.h(stype),
+                   ctypes.c_void_p(rbuf), A(*rcounts), A(*rdispls), self.h(rtype),
+                   self.h(self.COMM_WORLD if comm is None else comm))
+
+    # --------------------------------------------------------------- TEMPI
+    def describe(self, t):
+        info = TypeInfo()
+        self.L.tempi_type_describe(int(t), ctypes.byref(info))
+        if not info.known:
+            return None
+        nd = info.ndims
+        return {
+            "valid": bool(info.valid),
+            "start": info.start,
+            "block": info.block,
+            "counts": [info.counts[k] for k in range(nd)],
+            "strides": [info.strides[k] for k in range(nd)],
+            "size": info.size,
+            "lb": info.lb,
+            "extent": info.extent,
+        }
+
+    def counters(self):
+        c = Counters()
+        self.L.tempi_get_counters(ctypes.byref(c))
+        return {n: getattr(c, n) for n in _COUNTER_FIELDS}
+
+    def reset_counters(self):
+        self.L.tempi_reset_counters()
+
+    def set_kernel_profiling(self, on=True):
+        self.L.tempi_set_kernel_profiling(1 if on else 0)
+
+    def kernel_times(self):
+        k = KernelTimes()
+        self.L.tempi_get_kernel_times(ctypes.byref(k))
+        return {"pack_ms": k.pack_ms, "unpack_ms": k.unpack_ms, "packs": k.packs, "unpacks": k.unpacks}
+
+    def stream(self, device=0):
+        return self.L.tempi_get_stream(device)
+
+    def gpu_available(self):
+        return bool(self.L.tempi_gpu_available())
+
+    def version(self):
+        return self.L.tempi_version().decode()
+
+
+def get():
+    global _singleton
+    if _singleton is None:
+        _singleton = MPI()
+    return _singleton
