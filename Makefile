@@ -18,7 +18,9 @@ HIPFLAGS := --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Iinclude -Wall
 CXXFLAGS := -std=c++17 -O2 -g -fPIC -fvisibility=hidden -Wall -Wextra -Wno-unused-parameter \
             -Iinclude -I$(MPI_HOME)/include
 
-all: $(LIB)/libtempi.so oracle
+APPS := $(LIB)/halo_exchange $(LIB)/pingpong_nd
+
+all: $(LIB)/libtempi.so $(APPS) oracle
 
 build/hip/%.o: tempi_amd/csrc/hip/%.hip include/tempi_hip.h
 	@mkdir -p build/hip
@@ -39,11 +41,16 @@ $(LIB)/libtempi.so: $(CORE_OBJ) $(LIB)/libtempi_hip.so
 	    -static-libstdc++ -static-libgcc -Wl,--exclude-libs,ALL \
 	    -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,$(MPI_HOME)/lib -Wl,--enable-new-dtags
 
+# applications link -ltempi BEFORE the MPI library, like any TEMPI user
+$(LIB)/%: apps/%.cpp $(LIB)/libtempi.so
+	$(HIPCC) --offload-arch=gfx950 -O2 -std=c++17 -I$(MPI_HOME)/include -o $@ $< -L$(LIB) -ltempi -L$(MPI_HOME)/lib -lmpi \
+	    -static-libstdc++ -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,$(MPI_HOME)/lib
+
 oracle:
 	$(MAKE) -s -C oracle all
 
 clean:
-	rm -rf build $(LIB)/*.so
+	rm -rf build $(LIB)/*.so $(APPS)
 	$(MAKE) -s -C oracle clean
 
 .PHONY: all oracle clean

@@ -1,0 +1,284 @@
+// apps/halo_exchange.cpp -- 3D halo exchange through MPI_Isend / MPI_Irecv /
+// MPI_Wait on device buffers with subarray datatypes (config 4).
+//
+// Workload of the reference's bench_isir (/root/reference/bin/
+// bench_halo_exchange.cpp:666-949): a global X*Y*Z grid of nQuants 8-byte
+// quantities, radius 3, 26 neighbours, periodic, decomposed by recursive
+// bisection over the prime factors of the rank count (:679-704), pitched
+// allocations (pitch = bytes rounded up to 512, :727-733), one interior and
+// one exterior MPI_Type_create_subarray per direction (:87-168), 3 substeps
+// per iteration, time = max over ranks per iteration, trimean over iterations.
+//
+// Two deliberate differences: (1) a receive for the exterior halo on side d
+// is matched with the neighbour's send of ITS interior toward -d (tag =
+// direction code of the sender's send + 26 * quantity); the reference matches
+// by list position, which guarantees only equal sizes. (2) --check verifies
+// every halo byte against the value the owning rank wrote.
+//
+// usage: halo_exchange ITERS X [Y Z] [--quants N] [--radius R] [--check]
+// prints one JSON line (rank 0)
+#include <hip/hip_runtime.h>
+#include <mpi.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#define HIPCHECK(x)                                                                                \
+  do {                                                                                             \
+    hipError_t e_ = (x);                                                                           \
+    if (e_ != hipSuccess) {                                                                        \
+      std::fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_));              \
+      MPI_Abort(MPI_COMM_WORLD, 1);                                                                \
+    }                                                                                              \
+  } while (0)
+
+struct I3 {
+  int x, y, z;
+};
+
+static std::vector<int> prime_factors(int n) {
+  std::vector<int> r;
+  while (n % 2 == 0) {
+    r.push_back(2);
+    n /= 2;
+  }
+  for (int i = 3; i * i <= n; i += 2)
+    while (n % i == 0) {
+      r.push_back(i);
+      n /= i;
+    }
+  if (n > 2) r.push_back(n);
+  std::sort(r.begin(), r.end(), [](int a, int b) { return b < a; });
+  return r;
+}
+
+static int dir_code(int dx, int dy, int dz) { // 0..26, 13 = centre
+  return (dz + 1) * 9 + (dy + 1) * 3 + (dx + 1);
+}
+
+// the 8-byte value a rank writes for global cell (x, y, z) of quantity q
+__host__ __device__ static inline uint64_t cell_value(int64_t x, int64_t y, int64_t z, int q) {
+  uint64_t h = uint64_t(x) * 0x9E3779B97F4A7C15ull ^ uint64_t(y) * 0xC2B2AE3D27D4EB4Full ^
+               uint64_t(z) * 0x165667B19E3779F9ull ^ uint64_t(q + 1) * 0x27D4EB2F165667C5ull;
+  h ^= h >> 29;
+  return h * 0xBF58476D1CE4E5B9ull;
+}
+
+__global__ void fill_kernel(uint64_t *buf, size_t pitchWords, int ysize, I3 lcr, I3 origin, I3 global, int r,
+                            int q) {
+  // interior only; the halo starts as a sentinel
+  const int64_t n = int64_t(lcr.x) * lcr.y * lcr.z;
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+    const int x = int(i % lcr.x), y = int((i / lcr.x) % lcr.y), z = int(i / (int64_t(lcr.x) * lcr.y));
+    const int64_t gx = origin.x + x, gy = origin.y + y, gz = origin.z + z;
+    buf[(size_t(z + r) * ysize + size_t(y + r)) * pitchWords + size_t(x + r)] = cell_value(gx, gy, gz, q);
+  }
+}
+
+static double trimean(std::vector<double> v) {
+  if (v.empty()) return 0;
+  std::sort(v.begin(), v.end());
+  auto pct = [&](double p) {
+    const double idx = p * double(v.size() - 1);
+    const size_t lo = size_t(std::floor(idx)), hi = size_t(std::ceil(idx));
+    return v[lo] + (v[hi] - v[lo]) * (idx - double(lo));
+  };
+  return (pct(0.25) + 2 * pct(0.5) + pct(0.75)) / 4;
+}
+
+int main(int argc, char **argv) {
+  MPI_Init(&argc, &argv);
+  int rank, size;
+  MPI_Comm_rank(MPI_COMM_WORLD, &rank);
+  MPI_Comm_size(MPI_COMM_WORLD, &size);
+
+  int nIters = 5, nQuants = 8, radius = 3;
+  bool check = false;
+  std::vector<int> pos;
+  for (int i = 1; i < argc; ++i) {
+    std::string a = argv[i];
+    if (a == "--check")
+      check = true;
+    else if (a == "--quants")
+      nQuants = std::atoi(argv[++i]);
+    else if (a == "--radius")
+      radius = std::atoi(argv[++i]);
+    else
+      pos.push_back(std::atoi(argv[i]));
+  }
+  if (pos.size() != 2 && pos.size() != 4) {
+    if (!rank) std::fprintf(stderr, "usage: %s ITERS X [Y Z] [--quants N] [--radius R] [--check]\n", argv[0]);
+    MPI_Abort(MPI_COMM_WORLD, 1);
+  }
+  nIters = pos[0];
+  I3 global{pos[1], pos.size() == 4 ? pos[2] : pos[1], pos.size() == 4 ? pos[3] : pos[1]};
+
+  // one GPU per rank on the node (ranks beyond the GPU count share)
+  int ndev = 0;
+  HIPCHECK(hipGetDeviceCount(&ndev));
+  {
+    MPI_Comm node;
+    MPI_Comm_split_type(MPI_COMM_WORLD, MPI_COMM_TYPE_SHARED, rank, MPI_INFO_NULL, &node);
+    int lr;
+    MPI_Comm_rank(node, &lr);
+    HIPCHECK(hipSetDevice(lr % ndev));
+    MPI_Comm_free(&node);
+  }
+
+  // recursive bisection (/root/reference/bin/bench_halo_exchange.cpp:679-704)
+  I3 lcr = global, dims{1, 1, 1};
+  for (int f : prime_factors(size)) {
+    if (lcr.z >= lcr.y && lcr.z >= lcr.x) {
+      lcr.z /= f;
+      dims.z *= f;
+    } else if (lcr.y >= lcr.x) {
+      lcr.y /= f;
+      dims.y *= f;
+    } else {
+      lcr.x /= f;
+      dims.x *= f;
+    }
+  }
+  const I3 me{rank % dims.x, (rank / dims.x) % dims.y, rank / (dims.x * dims.y)};
+  const I3 origin{me.x * lcr.x, me.y * lcr.y, me.z * lcr.z};
+  const int q = 8; // bytes per quantity
+  const size_t width = size_t(lcr.x + 2 * radius) * q;
+  const size_t pitch = (width + 511) / 512 * 512;
+  const int ysize = lcr.y + 2 * radius, zsize = lcr.z + 2 * radius;
+  const size_t bufBytes = pitch * size_t(ysize) * size_t(zsize);
+
+  std::vector<char *> bufs(static_cast<size_t>(nQuants));
+  for (int qi = 0; qi < nQuants; ++qi) {
+    HIPCHECK(hipMalloc(&bufs[size_t(qi)], bufBytes));
+    HIPCHECK(hipMemset(bufs[size_t(qi)], 0xEE, bufBytes));
+    hipLaunchKernelGGL(fill_kernel, dim3(1024), dim3(256), 0, 0, reinterpret_cast<uint64_t *>(bufs[size_t(qi)]),
+                       pitch / 8, ysize, lcr, origin, global, radius, qi);
+  }
+  HIPCHECK(hipDeviceSynchronize());
+
+  struct Dir {
+    int dx, dy, dz, nbr;
+    MPI_Datatype interior, exterior;
+    int bytes;
+  };
+  std::vector<Dir> dirs;
+  auto halo_type = [&](int dx, int dy, int dz, bool exterior) {
+    const int d[3] = {dx, dy, dz};
+    const int l[3] = {lcr.x, lcr.y, lcr.z};
+    int p[3], e[3];
+    for (int k = 0; k < 3; ++k) {
+      if (d[k] == -1)
+        p[k] = exterior ? 0 : radius;
+      else if (d[k] == 1)
+        p[k] = l[k] + (exterior ? radius : 0);
+      else
+        p[k] = radius;
+      e[k] = d[k] == 0 ? l[k] : radius;
+    }
+    int sizes[3] = {p[2] + e[2], ysize, int(pitch)};
+    int subs[3] = {e[2], e[1], e[0] * q};
+    int starts[3] = {p[2], p[1], p[0] * q};
+    MPI_Datatype t;
+    MPI_Type_create_subarray(3, sizes, subs, starts, MPI_ORDER_C, MPI_BYTE, &t);
+    MPI_Type_commit(&t);
+    return t;
+  };
+  for (int dz = -1; dz <= 1; ++dz)
+    for (int dy = -1; dy <= 1; ++dy)
+      for (int dx = -1; dx <= 1; ++dx) {
+        if (!dx && !dy && !dz) continue;
+        I3 n{(me.x + dx + dims.x) % dims.x, (me.y + dy + dims.y) % dims.y, (me.z + dz + dims.z) % dims.z};
+        Dir D{dx, dy, dz, n.x + n.y * dims.x + n.z * dims.x * dims.y, halo_type(dx, dy, dz, false),
+              halo_type(dx, dy, dz, true), 0};
+        MPI_Type_size(D.interior, &D.bytes);
+        dirs.push_back(D);
+      }
+
+  // per-peer traffic for the xGMI roofline
+  std::vector<double> peerBytes(size_t(size), 0);
+  double bytesPerIter = 0;
+  for (const Dir &D : dirs) {
+    bytesPerIter += double(D.bytes) * nQuants * 3;
+    if (D.nbr != rank) peerBytes[size_t(D.nbr)] += double(D.bytes) * nQuants * 3;
+  }
+  const double maxLink = *std::max_element(peerBytes.begin(), peerBytes.end());
+
+  std::vector<double> times;
+  std::vector<MPI_Request> reqs(dirs.size() * 2 * size_t(nQuants));
+  const int warm = 1;
+  for (int it = 0; it < nIters + warm; ++it) {
+    double exch = 0;
+    for (int sub = 0; sub < 3; ++sub) {
+      MPI_Barrier(MPI_COMM_WORLD);
+      const double t0 = MPI_Wtime();
+      size_t ri = 0;
+      for (int qi = 0; qi < nQuants; ++qi)
+        for (const Dir &D : dirs)
+          MPI_Isend(bufs[size_t(qi)], 1, D.interior, D.nbr, dir_code(D.dx, D.dy, D.dz) + 27 * qi, MPI_COMM_WORLD,
+                    &reqs[ri++]);
+      for (int qi = 0; qi < nQuants; ++qi)
+        for (const Dir &D : dirs)
+          MPI_Irecv(bufs[size_t(qi)], 1, D.exterior, D.nbr, dir_code(-D.dx, -D.dy, -D.dz) + 27 * qi,
+                    MPI_COMM_WORLD, &reqs[ri++]);
+      for (MPI_Request &r : reqs) MPI_Wait(&r, MPI_STATUS_IGNORE);
+      exch += MPI_Wtime() - t0;
+    }
+    MPI_Allreduce(MPI_IN_PLACE, &exch, 1, MPI_DOUBLE, MPI_MAX, MPI_COMM_WORLD);
+    if (it >= warm) times.push_back(exch);
+  }
+
+  long long errors = 0;
+  if (check) {
+    std::vector<uint64_t> h(static_cast<size_t>(bufBytes / 8));
+    for (int qi = 0; qi < nQuants; ++qi) {
+      HIPCHECK(hipMemcpy(h.data(), bufs[size_t(qi)], bufBytes, hipMemcpyDeviceToHost));
+      for (int z = 0; z < zsize; ++z)
+        for (int y = 0; y < ysize; ++y)
+          for (int x = 0; x < lcr.x + 2 * radius; ++x) {
+            const bool inX = x >= radius && x < radius + lcr.x, inY = y >= radius && y < radius + lcr.y,
+                       inZ = z >= radius && z < radius + lcr.z;
+            // every cell (interior and all 26 halo regions) must hold the
+            // owner's value; only the 8 "edges of edges" are all set too
+            const int64_t gx = (origin.x + x - radius + global.x) % global.x;
+            const int64_t gy = (origin.y + y - radius + global.y) % global.y;
+            const int64_t gz = (origin.z + z - radius + global.z) % global.z;
+            (void)inX;
+            (void)inY;
+            (void)inZ;
+            const uint64_t got = h[(size_t(z) * ysize + size_t(y)) * (pitch / 8) + size_t(x)];
+            if (got != cell_value(gx, gy, gz, qi)) ++errors;
+          }
+    }
+    MPI_Allreduce(MPI_IN_PLACE, &errors, 1, MPI_LONG_LONG, MPI_SUM, MPI_COMM_WORLD);
+  }
+
+  double maxLinkAll = maxLink;
+  MPI_Allreduce(MPI_IN_PLACE, &maxLinkAll, 1, MPI_DOUBLE, MPI_MAX, MPI_COMM_WORLD);
+  double totalBytes = bytesPerIter;
+  MPI_Allreduce(MPI_IN_PLACE, &totalBytes, 1, MPI_DOUBLE, MPI_SUM, MPI_COMM_WORLD);
+  const double tIter = trimean(times);
+  if (rank == 0) {
+    std::printf("{\"ranks\": %d, \"global\": [%d, %d, %d], \"dims\": [%d, %d, %d], \"lcr\": [%d, %d, %d], "
+                "\"quants\": %d, \"radius\": %d, \"iters\": %d, \"us_per_iter\": %.2f, \"us_min\": %.2f, "
+                "\"payload_bytes_per_iter_per_rank0\": %.0f, \"total_bytes_per_iter\": %.0f, "
+                "\"max_peer_bytes_per_iter\": %.0f, \"aggregate_GBps\": %.2f, \"busiest_link_GBps\": %.2f, "
+                "\"checked\": %s, \"errors\": %lld}\n",
+                size, global.x, global.y, global.z, dims.x, dims.y, dims.z, lcr.x, lcr.y, lcr.z, nQuants, radius,
+                nIters, tIter * 1e6, *std::min_element(times.begin(), times.end()) * 1e6, bytesPerIter, totalBytes,
+                maxLinkAll, totalBytes / tIter / 1e9, maxLinkAll / tIter / 1e9, check ? "true" : "false", errors);
+    std::fflush(stdout);
+  }
+  for (Dir &D : dirs) {
+    MPI_Type_free(&D.interior);
+    MPI_Type_free(&D.exterior);
+  }
+  for (char *b : bufs) HIPCHECK(hipFree(b));
+  MPI_Finalize();
+  return errors ? 3 : 0;
+}

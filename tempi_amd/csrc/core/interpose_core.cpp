@@ -17,6 +17,8 @@
 #include "log.hpp"
 #include "next_mpi.hpp"
 #include "state.hpp"
+#include "p2p.hpp"
+#include "topology.hpp"
 #include "type_cache.hpp"
 
 #include "tempi_mpi.h"
@@ -37,10 +39,6 @@ int raise_error(MPI_Comm comm, int code) {
   return code;
 }
 
-void async_init();
-void async_finalize();
-void transport_init();
-void transport_finalize();
 
 void init_after_mpi() {
   if (env.noTempi) return;
@@ -50,16 +48,16 @@ void init_after_mpi() {
   gpu::init();
   types_init();
   state.active = true;
-  transport_init();
-  async_init();
+  topology::init();
+  p2p::init();
   LOG_DEBUG("TEMPI active: rank " << state.worldRank << "/" << state.worldSize
                                   << ", GPU " << (gpu::available() ? "yes" : "no"));
 }
 
 void finalize_before_mpi() {
   if (!state.active) return;
-  async_finalize();
-  transport_finalize();
+  p2p::finalize();
+  topology::finalize();
   LOG_DEBUG("counters: packs=" << counters.packs << " unpacks=" << counters.unpacks
                                << " launches=" << counters.launches << " lib_packs="
                                << counters.lib_packs << " sends=" << counters.sends);
@@ -228,9 +226,9 @@ TEMPI_EXPORT int MPI_Type_free(MPI_Datatype *datatype) {
   return next.MPI_Type_free(datatype);
 }
 
-TEMPI_EXPORT int MPI_Pack(const void *inbuf, int incount, MPI_Datatype datatype, void *outbuf,
-                          int outsize, int *position, MPI_Comm comm) {
-  resolve_next();
+namespace tempi {
+int pack(const void *inbuf, int incount, MPI_Datatype datatype, void *outbuf, int outsize, int *position,
+         MPI_Comm comm) {
   if (!state.active || env.noPack || incount <= 0 || !position)
     return next.MPI_Pack(inbuf, incount, datatype, outbuf, outsize, position, comm);
   const TypeRecord *rec = type_lookup(datatype);
@@ -253,9 +251,8 @@ TEMPI_EXPORT int MPI_Pack(const void *inbuf, int incount, MPI_Datatype datatype,
   return MPI_SUCCESS;
 }
 
-TEMPI_EXPORT int MPI_Unpack(const void *inbuf, int insize, int *position, void *outbuf, int outcount,
-                            MPI_Datatype datatype, MPI_Comm comm) {
-  resolve_next();
+int unpack(const void *inbuf, int insize, int *position, void *outbuf, int outcount, MPI_Datatype datatype,
+           MPI_Comm comm) {
   if (!state.active || env.noPack || outcount <= 0 || !position)
     return next.MPI_Unpack(inbuf, insize, position, outbuf, outcount, datatype, comm);
   const TypeRecord *rec = type_lookup(datatype);
@@ -276,4 +273,17 @@ TEMPI_EXPORT int MPI_Unpack(const void *inbuf, int insize, int *position, void *
   gpu::check(e, "MPI_Unpack");
   *position += int(bytes);
   return MPI_SUCCESS;
+}
+} // namespace tempi
+
+TEMPI_EXPORT int MPI_Pack(const void *inbuf, int incount, MPI_Datatype datatype, void *outbuf,
+                          int outsize, int *position, MPI_Comm comm) {
+  resolve_next();
+  return tempi::pack(inbuf, incount, datatype, outbuf, outsize, position, comm);
+}
+
+TEMPI_EXPORT int MPI_Unpack(const void *inbuf, int insize, int *position, void *outbuf, int outcount,
+                            MPI_Datatype datatype, MPI_Comm comm) {
+  resolve_next();
+  return tempi::unpack(inbuf, insize, position, outbuf, outcount, datatype, comm);
 }

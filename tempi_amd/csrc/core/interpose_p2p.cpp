@@ -1,0 +1,121 @@
+// tempi_amd/csrc/core/interpose_p2p.cpp -- interposed MPI_Send / MPI_Recv /
+// MPI_Isend / MPI_Irecv / MPI_Wait / MPI_Waitall / MPI_Test (include/
+// tempi_mpi.h). Device buffers go through tempi::p2p (p2p.hpp); host buffers
+// go to the library, as in the reference (/root/reference/src/send.cpp:12-17,
+// recv.cpp:19-44, isend.cpp:11-16, irecv.cpp:11-16, wait.cpp:11-16), except
+// that requests TEMPI owns are understood by MPI_Waitall and MPI_Test too
+// (SURVEY F8), and library waits keep TEMPI operations progressing.
+#include "counters.hpp"
+#include "next_mpi.hpp"
+#include "p2p.hpp"
+#include "state.hpp"
+
+#include "tempi_mpi.h"
+
+#include <vector>
+
+#define TEMPI_EXPORT extern "C" __attribute__((visibility("default")))
+
+using namespace tempi;
+
+TEMPI_EXPORT int MPI_Send(const void *buf, int count, MPI_Datatype datatype, int dest, int tag,
+                          MPI_Comm comm) {
+  resolve_next();
+  if (!p2p::handles(buf, count, datatype, dest)) {
+    counters.lib_sends++;
+    return next.MPI_Send(buf, count, datatype, dest, tag, comm);
+  }
+  counters.sends++;
+  MPI_Request r;
+  int rc = p2p::isend(buf, count, datatype, dest, tag, comm, &r);
+  if (rc != MPI_SUCCESS) return rc;
+  return p2p::wait(&r, MPI_STATUS_IGNORE);
+}
+
+TEMPI_EXPORT int MPI_Recv(void *buf, int count, MPI_Datatype datatype, int source, int tag, MPI_Comm comm,
+                          MPI_Status *status) {
+  resolve_next();
+  if (p2p::handles(buf, count, datatype, source)) {
+    counters.recvs++;
+    MPI_Request r;
+    int rc = p2p::irecv(buf, count, datatype, source, tag, comm, &r);
+    if (rc != MPI_SUCCESS) return rc;
+    return p2p::wait(&r, status);
+  }
+  bool handled = false;
+  const int rc = p2p::recv_host_ipc_aware(buf, count, datatype, source, tag, comm, status, &handled);
+  if (handled) return rc;
+  counters.lib_recvs++;
+  return next.MPI_Recv(buf, count, datatype, source, tag, comm, status);
+}
+
+TEMPI_EXPORT int MPI_Isend(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm,
+                           MPI_Request *request) {
+  resolve_next();
+  if (p2p::handles(buf, count, datatype, dest))
+    return p2p::isend(buf, count, datatype, dest, tag, comm, request);
+  if (state.active) p2p::progress();
+  counters.lib_sends++;
+  return next.MPI_Isend(buf, count, datatype, dest, tag, comm, request);
+}
+
+TEMPI_EXPORT int MPI_Irecv(void *buf, int count, MPI_Datatype datatype, int source, int tag, MPI_Comm comm,
+                           MPI_Request *request) {
+  resolve_next();
+  if (p2p::handles(buf, count, datatype, source))
+    return p2p::irecv(buf, count, datatype, source, tag, comm, request);
+  if (state.active) p2p::progress();
+  counters.lib_recvs++;
+  return next.MPI_Irecv(buf, count, datatype, source, tag, comm, request);
+}
+
+TEMPI_EXPORT int MPI_Wait(MPI_Request *request, MPI_Status *status) {
+  resolve_next();
+  if (!state.active) return next.MPI_Wait(request, status);
+  if (p2p::is_tempi_request(*request)) return p2p::wait(request, status);
+  if (!p2p::busy()) return next.MPI_Wait(request, status);
+  for (;;) { // a library request, while TEMPI operations are in flight
+    int flag = 0;
+    const int rc = next.MPI_Test(request, &flag, status);
+    if (rc != MPI_SUCCESS || flag) return rc;
+    p2p::progress();
+  }
+}
+
+TEMPI_EXPORT int MPI_Test(MPI_Request *request, int *flag, MPI_Status *status) {
+  resolve_next();
+  if (!state.active) return next.MPI_Test(request, flag, status);
+  if (p2p::is_tempi_request(*request)) return p2p::test(request, flag, status);
+  if (p2p::busy()) p2p::progress();
+  return next.MPI_Test(request, flag, status);
+}
+
+TEMPI_EXPORT int MPI_Waitall(int count, MPI_Request requests[], MPI_Status statuses[]) {
+  resolve_next();
+  if (!state.active) return next.MPI_Waitall(count, requests, statuses);
+  bool any = false;
+  for (int i = 0; i < count && !any; ++i) any = p2p::is_tempi_request(requests[i]);
+  if (!any && !p2p::busy()) return next.MPI_Waitall(count, requests, statuses);
+  std::vector<char> done(size_t(count), 0);
+  int remaining = count;
+  int err = MPI_SUCCESS;
+  while (remaining) {
+    p2p::progress();
+    for (int i = 0; i < count; ++i) {
+      if (done[size_t(i)]) continue;
+      MPI_Status *st = statuses == MPI_STATUSES_IGNORE ? MPI_STATUS_IGNORE : &statuses[i];
+      int flag = 0;
+      const int rc = p2p::is_tempi_request(requests[i]) ? p2p::test(&requests[i], &flag, st)
+                                                        : next.MPI_Test(&requests[i], &flag, st);
+      if (rc != MPI_SUCCESS) {
+        err = MPI_ERR_IN_STATUS;
+        flag = 1;
+      }
+      if (flag) {
+        done[size_t(i)] = 1;
+        --remaining;
+      }
+    }
+  }
+  return err;
+}

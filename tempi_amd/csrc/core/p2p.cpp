@@ -1,0 +1,554 @@
+// tempi_amd/csrc/core/p2p.cpp -- see p2p.hpp
+#include "p2p.hpp"
+
+#include "alloc.hpp"
+#include "counters.hpp"
+#include "env.hpp"
+#include "gpu.hpp"
+#include "log.hpp"
+#include "next_mpi.hpp"
+#include "state.hpp"
+#include "topology.hpp"
+#include "type_cache.hpp"
+
+#include <chrono>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <unistd.h>
+#include <vector>
+
+namespace tempi {
+namespace p2p {
+
+enum class Method { ONESHOT, STAGED, DEVICE, IPC, LIBPACK };
+
+namespace {
+
+constexpr uint64_t kMagic0 = 0x54454d5049495043ull; // "TEMPIIPC"
+constexpr uint64_t kMagic1 = 0x9e3779b97f4a7c15ull;
+
+struct IpcDesc {
+  uint64_t magic[2];
+  uint64_t slabId;
+  uint64_t offset;
+  int64_t bytes;
+  int32_t senderWorld;
+  int32_t senderPid;
+  int32_t ackTag;
+  int32_t pad;
+  uint64_t rawPtr; // valid inside the sender's own process
+  unsigned char handle[TEMPI_HIP_IPC_HANDLE_BYTES];
+};
+static_assert(sizeof(IpcDesc) == 128, "descriptor size");
+
+MPI_Comm ctrlComm = MPI_COMM_NULL; // private duplicate of MPI_COMM_WORLD for acks
+int tagUb = 32767;
+bool gpuAwareLibrary = false;
+int64_t ipcMinBytes = 64 * 1024;
+
+// acks the sender is waiting for before reusing a device slab
+struct PendingAck {
+  MPI_Request req;
+  Slab *slab;
+};
+std::vector<PendingAck> pendingAcks;
+
+// peer slabs mapped into this process: (world rank, slab id) -> base
+std::map<std::pair<int, uint64_t>, void *> ipcOpen;
+
+int64_t pack_size(int count, MPI_Datatype dt, MPI_Comm comm) {
+  int s = 0;
+  MPI_Pack_size(count, dt, comm, &s);
+  return s;
+}
+
+Method choose(int64_t bytes, bool colocated) {
+  switch (env.datatype) {
+  case DatatypeMethod::ONESHOT:
+    return Method::ONESHOT;
+  case DatatypeMethod::STAGED:
+    return Method::STAGED;
+  case DatatypeMethod::DEVICE:
+    if (gpuAwareLibrary) return Method::DEVICE;
+    return colocated ? Method::IPC : Method::STAGED;
+  case DatatypeMethod::IPC:
+    return colocated ? Method::IPC : Method::ONESHOT;
+  case DatatypeMethod::AUTO:
+  default:
+    if (colocated && bytes >= ipcMinBytes) return Method::IPC;
+    return Method::ONESHOT;
+  }
+}
+
+void *peer_pointer(const IpcDesc &d) {
+  if (d.senderPid == int32_t(getpid())) return reinterpret_cast<void *>(d.rawPtr);
+  auto key = std::make_pair(int(d.senderWorld), d.slabId);
+  auto it = ipcOpen.find(key);
+  if (it != ipcOpen.end()) return it->second;
+  void *p = nullptr;
+  gpu::check(tempi_hip_ipc_open_handle(&p, d.handle), "ipc open handle");
+  ipcOpen[key] = p;
+  return p;
+}
+
+void send_ack(const IpcDesc &d) {
+  static char dummy = 0;
+  MPI_Request r;
+  next.MPI_Isend(&dummy, 0, MPI_BYTE, d.senderWorld, d.ackTag, ctrlComm, &r);
+  MPI_Request_free(&r);
+}
+
+// ---------------------------------------------------------------- operations
+
+struct Op {
+  virtual ~Op() {}
+  virtual bool step() = 0; // true when complete
+  virtual void status(MPI_Status *s) const = 0;
+  bool done = false;
+};
+
+void *make_event() {
+  void *e = nullptr;
+  gpu::check(tempi_hip_event_create(&e, 0), "event create");
+  return e;
+}
+
+struct IsendOp : Op {
+  Packer packer;
+  const char *origin; // GPU-visible
+  int count, dest, tag, device;
+  MPI_Datatype dt;
+  MPI_Comm comm;
+  Method method;
+  int64_t bytes;
+  Slab *dslab = nullptr, *hslab = nullptr;
+  void *event = nullptr;
+  MPI_Request lib = MPI_REQUEST_NULL;
+  IpcDesc desc{};
+  enum { PACKING, SENDING } st = PACKING;
+
+  IsendOp(const TypeRecord &rec, const char *o, int c, MPI_Datatype d, int de, int t, MPI_Comm cm, int dev,
+          Method m, int64_t b)
+      : packer(rec.desc), origin(o), count(c), dest(de), tag(t), device(dev), dt(d), comm(cm), method(m), bytes(b) {
+    void *s = gpu::stream(device);
+    int e = 0;
+    if (method == Method::ONESHOT) {
+      hslab = pinned_pool().get(size_t(bytes), device);
+      e = packer.pack_async(hslab->dev, origin, count, s);
+    } else {
+      dslab = device_pool().get(size_t(bytes), device);
+      e = packer.pack_async(dslab->dev, origin, count, s);
+      if (!e && method == Method::STAGED) {
+        hslab = pinned_pool().get(size_t(bytes), device);
+        e = tempi_hip_memcpy_async(hslab->host, dslab->dev, size_t(bytes), s);
+      }
+    }
+    gpu::check(e, "isend pack");
+    event = make_event();
+    gpu::check(tempi_hip_event_record(event, s), "event record");
+  }
+  ~IsendOp() override {
+    if (event) tempi_hip_event_destroy(event);
+  }
+
+  void start_send() {
+    switch (method) {
+    case Method::ONESHOT:
+    case Method::STAGED:
+      next.MPI_Isend(hslab->host, int(bytes), MPI_PACKED, dest, tag, comm, &lib);
+      break;
+    case Method::DEVICE:
+      next.MPI_Isend(dslab->dev, int(bytes), MPI_PACKED, dest, tag, comm, &lib);
+      break;
+    case Method::IPC: {
+      desc.magic[0] = kMagic0;
+      desc.magic[1] = kMagic1;
+      desc.slabId = dslab->id;
+      desc.offset = 0;
+      desc.bytes = bytes;
+      desc.senderWorld = state.worldRank;
+      desc.senderPid = int32_t(getpid());
+      desc.ackTag = int32_t(dslab->id % uint32_t(tagUb));
+      desc.rawPtr = reinterpret_cast<uint64_t>(dslab->dev);
+      std::memcpy(desc.handle, slab_ipc_handle(dslab), sizeof desc.handle);
+      // the ack comes from the receiver on the private communicator
+      const int peer = topology::world_rank(comm, dest);
+      PendingAck pa{MPI_REQUEST_NULL, dslab};
+      static char sink;
+      next.MPI_Irecv(&sink, 0, MPI_BYTE, peer, desc.ackTag, ctrlComm, &pa.req);
+      pendingAcks.push_back(pa);
+      dslab = nullptr; // owned by the pending ack now
+      next.MPI_Isend(&desc, int(sizeof desc), MPI_PACKED, dest, tag, comm, &lib);
+      break;
+    }
+    default:
+      break;
+    }
+  }
+
+  bool step() override {
+    if (done) return true;
+    if (st == PACKING) {
+      const int q = tempi_hip_event_query(event);
+      if (q == 1) return false;
+      gpu::check(q, "isend event");
+      start_send();
+      st = SENDING;
+    }
+    int flag = 0;
+    next.MPI_Test(&lib, &flag, MPI_STATUS_IGNORE);
+    if (!flag) return false;
+    if (dslab) device_pool().put(dslab);
+    if (hslab) pinned_pool().put(hslab);
+    dslab = hslab = nullptr;
+    done = true;
+    return true;
+  }
+  void status(MPI_Status *s) const override {
+    if (s != MPI_STATUS_IGNORE) {
+      s->MPI_SOURCE = MPI_ANY_SOURCE;
+      s->MPI_TAG = MPI_ANY_TAG;
+      s->MPI_ERROR = MPI_SUCCESS;
+      MPI_Status_set_elements(s, dt, 0);
+    }
+  }
+};
+
+struct IrecvOp : Op {
+  Packer packer;
+  char *origin; // GPU-visible
+  int count, device;
+  MPI_Datatype dt;
+  MPI_Comm comm;
+  int64_t bytes;
+  Slab *hslab = nullptr;
+  void *event = nullptr;
+  MPI_Request lib = MPI_REQUEST_NULL;
+  MPI_Status libStatus{};
+  IpcDesc desc{};
+  bool ipc = false;
+  int64_t elems = 0;
+  enum { RECEIVING, UNPACKING } st = RECEIVING;
+
+  IrecvOp(const TypeRecord &rec, char *o, int c, MPI_Datatype d, int source, int tag, MPI_Comm cm, int dev,
+          int64_t b)
+      : packer(rec.desc), origin(o), count(c), device(dev), dt(d), comm(cm), bytes(b) {
+    const size_t cap = std::max<size_t>(size_t(bytes), sizeof(IpcDesc));
+    hslab = pinned_pool().get(cap, device);
+    next.MPI_Irecv(hslab->host, int(cap), MPI_PACKED, source, tag, comm, &lib);
+  }
+  ~IrecvOp() override {
+    if (event) tempi_hip_event_destroy(event);
+  }
+
+  bool step() override {
+    if (done) return true;
+    if (st == RECEIVING) {
+      int flag = 0;
+      next.MPI_Test(&lib, &flag, &libStatus);
+      if (!flag) return false;
+      int n = 0;
+      MPI_Get_count(&libStatus, MPI_PACKED, &n);
+      void *s = gpu::stream(device);
+      const unsigned char *hb = static_cast<const unsigned char *>(hslab->host);
+      IpcDesc d;
+      std::memcpy(&d, hb, std::min<size_t>(sizeof d, size_t(n)));
+      if (size_t(n) == sizeof(IpcDesc) && d.magic[0] == kMagic0 && d.magic[1] == kMagic1) {
+        ipc = true;
+        desc = d;
+        const char *peer = static_cast<const char *>(peer_pointer(d)) + d.offset;
+        elems = packer.desc().size ? d.bytes / packer.desc().size : 0;
+        if (d.bytes > bytes) LOG_FATAL("message truncated: " << d.bytes << " B into " << bytes);
+        gpu::check(packer.unpack_async(origin, peer, elems, s), "irecv ipc unpack");
+      } else {
+        if (int64_t(n) > bytes) LOG_FATAL("message truncated: " << n << " B into " << bytes);
+        elems = packer.desc().size ? n / packer.desc().size : 0;
+        gpu::check(packer.unpack_async(origin, hslab->dev, elems, s), "irecv unpack");
+      }
+      event = make_event();
+      gpu::check(tempi_hip_event_record(event, s), "event record");
+      st = UNPACKING;
+    }
+    const int q = tempi_hip_event_query(event);
+    if (q == 1) return false;
+    gpu::check(q, "irecv event");
+    if (ipc) send_ack(desc);
+    pinned_pool().put(hslab);
+    hslab = nullptr;
+    done = true;
+    return true;
+  }
+  void status(MPI_Status *s) const override {
+    if (s != MPI_STATUS_IGNORE) {
+      *s = libStatus;
+      s->MPI_ERROR = MPI_SUCCESS;
+      MPI_Status_set_elements(s, dt, int(elems));
+    }
+  }
+};
+
+// library-packed transfer of a device buffer whose type TEMPI cannot pack
+// (the touched span is staged through host memory by MPI_Pack/MPI_Unpack)
+struct LibIsendOp : Op {
+  std::vector<char> buf;
+  MPI_Request lib = MPI_REQUEST_NULL;
+  MPI_Datatype dt;
+  LibIsendOp(const void *b, int c, MPI_Datatype d, int dest, int tag, MPI_Comm comm) : dt(d) {
+    buf.resize(size_t(std::max<int64_t>(pack_size(c, d, comm), 1)));
+    int pos = 0;
+    tempi::pack(b, c, d, buf.data(), int(buf.size()), &pos, comm); // stages device data
+    next.MPI_Isend(buf.data(), pos, MPI_PACKED, dest, tag, comm, &lib);
+  }
+  bool step() override {
+    if (done) return true;
+    int flag = 0;
+    next.MPI_Test(&lib, &flag, MPI_STATUS_IGNORE);
+    return done = flag != 0;
+  }
+  void status(MPI_Status *s) const override {
+    if (s != MPI_STATUS_IGNORE) {
+      s->MPI_ERROR = MPI_SUCCESS;
+      MPI_Status_set_elements(s, dt, 0);
+    }
+  }
+};
+
+struct LibIrecvOp : Op {
+  std::vector<char> buf;
+  void *user;
+  int count;
+  MPI_Datatype dt;
+  MPI_Comm comm;
+  MPI_Request lib = MPI_REQUEST_NULL;
+  MPI_Status libStatus{};
+  int elems = 0;
+  LibIrecvOp(void *b, int c, MPI_Datatype d, int source, int tag, MPI_Comm cm) : user(b), count(c), dt(d), comm(cm) {
+    buf.resize(size_t(std::max<int64_t>(pack_size(c, d, cm), 1)));
+    next.MPI_Irecv(buf.data(), int(buf.size()), MPI_PACKED, source, tag, comm, &lib);
+  }
+  bool step() override {
+    if (done) return true;
+    int flag = 0;
+    next.MPI_Test(&lib, &flag, &libStatus);
+    if (!flag) return false;
+    int n = 0, size = 0;
+    MPI_Get_count(&libStatus, MPI_PACKED, &n);
+    MPI_Type_size(dt, &size);
+    elems = size ? n / size : 0;
+    int pos = 0;
+    tempi::unpack(buf.data(), n, &pos, user, elems, dt, comm); // stages device data
+    return done = true;
+  }
+  void status(MPI_Status *s) const override {
+    if (s != MPI_STATUS_IGNORE) {
+      *s = libStatus;
+      s->MPI_ERROR = MPI_SUCCESS;
+      MPI_Status_set_elements(s, dt, elems);
+    }
+  }
+};
+
+// ------------------------------------------------------------- request table
+
+// TEMPI request handles live in [1, 2^26): the top bits of an MPICH handle
+// always encode a non-zero kind, so the library never issues one of these
+// (the reference uses a plain counter that can collide: SURVEY F9)
+constexpr uint32_t kHandleSpace = 1u << 26;
+uint32_t nextHandle = 1;
+std::map<uint32_t, std::unique_ptr<Op>> active; // ordered: creation order
+
+MPI_Request add(std::unique_ptr<Op> op) {
+  while (active.count(nextHandle) || nextHandle == 0) nextHandle = (nextHandle + 1) % kHandleSpace;
+  const uint32_t h = nextHandle;
+  nextHandle = (nextHandle + 1) % kHandleSpace;
+  active[h] = std::move(op);
+  return MPI_Request(h);
+}
+
+} // namespace
+
+void init() {
+  gpuAwareLibrary = std::getenv("TEMPI_MPI_GPU_AWARE") != nullptr;
+  if (const char *s = std::getenv("TEMPI_IPC_MIN_BYTES")) ipcMinBytes = std::atoll(s);
+  MPI_Comm_dup(MPI_COMM_WORLD, &ctrlComm);
+  int flag = 0;
+  int *ub = nullptr;
+  MPI_Comm_get_attr(MPI_COMM_WORLD, MPI_TAG_UB, &ub, &flag);
+  if (flag && ub) tagUb = *ub;
+}
+
+void finalize() {
+  // complete everything the application left behind, then wait (bounded) for
+  // the acks that let us release IPC slabs
+  const auto t0 = std::chrono::steady_clock::now();
+  for (auto &kv : active)
+    while (!kv.second->step()) {
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(30)) {
+        LOG_WARN("request left incomplete at MPI_Finalize");
+        break;
+      }
+    }
+  active.clear();
+  while (!pendingAcks.empty()) {
+    progress();
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(30)) {
+      LOG_WARN(pendingAcks.size() << " IPC slab(s) never acknowledged; abandoning");
+      for (auto &pa : pendingAcks) MPI_Cancel(&pa.req);
+      pendingAcks.clear();
+    }
+  }
+  for (auto &kv : ipcOpen) tempi_hip_ipc_close_handle(kv.second);
+  ipcOpen.clear();
+  if (ctrlComm != MPI_COMM_NULL) MPI_Comm_free(&ctrlComm);
+  device_pool().release_all();
+  pinned_pool().release_all();
+}
+
+bool handles(const void *buf, int count, MPI_Datatype dt, int peer) {
+  if (!state.active || !gpu::available() || count <= 0 || peer == MPI_PROC_NULL) return false;
+  const TypeRecord *rec = type_lookup(dt);
+  if (!rec || rec->desc.size == 0) return false;
+  const int64_t first = rec->desc.valid ? rec->desc.start : 0;
+  return gpu::classify(static_cast<const char *>(buf) + first).device_accessible;
+}
+
+int isend(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Comm comm, MPI_Request *req) {
+  const TypeRecord *rec = type_lookup(dt);
+  progress();
+  counters.isends++;
+  if (!rec->packer) {
+    *req = add(std::make_unique<LibIsendOp>(buf, count, dt, dest, tag, comm));
+    return MPI_SUCCESS;
+  }
+  const gpu::Ptr p = gpu::classify(static_cast<const char *>(buf) + rec->desc.start);
+  const int64_t bytes = pack_size(count, dt, comm);
+  const Method m = choose(bytes, topology::colocated(comm, dest));
+  switch (m) {
+  case Method::ONESHOT: counters.send_oneshot++; break;
+  case Method::STAGED: counters.send_staged++; break;
+  case Method::DEVICE: counters.send_device++; break;
+  case Method::IPC: counters.send_ipc++; break;
+  default: break;
+  }
+  const char *origin = static_cast<const char *>(p.dptr) - rec->desc.start;
+  int cur = 0;
+  tempi_hip_get_device(&cur);
+  if (cur != p.device) tempi_hip_set_device(p.device);
+  *req = add(std::make_unique<IsendOp>(*rec, origin, count, dt, dest, tag, comm, p.device, m, bytes));
+  if (cur != p.device) tempi_hip_set_device(cur);
+  return MPI_SUCCESS;
+}
+
+int irecv(void *buf, int count, MPI_Datatype dt, int source, int tag, MPI_Comm comm, MPI_Request *req) {
+  const TypeRecord *rec = type_lookup(dt);
+  progress();
+  counters.irecvs++;
+  if (!rec->packer) {
+    *req = add(std::make_unique<LibIrecvOp>(buf, count, dt, source, tag, comm));
+    return MPI_SUCCESS;
+  }
+  const gpu::Ptr p = gpu::classify(static_cast<char *>(buf) + rec->desc.start);
+  const int64_t bytes = pack_size(count, dt, comm);
+  char *origin = static_cast<char *>(p.dptr) - rec->desc.start;
+  *req = add(std::make_unique<IrecvOp>(*rec, origin, count, dt, source, tag, comm, p.device, bytes));
+  return MPI_SUCCESS;
+}
+
+bool is_tempi_request(MPI_Request r) {
+  const uint32_t h = uint32_t(r);
+  return h != 0 && h < kHandleSpace && active.count(h);
+}
+
+bool progress() {
+  bool moved = false;
+  for (auto &kv : active)
+    if (!kv.second->done) moved |= kv.second->step();
+  for (size_t i = 0; i < pendingAcks.size();) {
+    int flag = 0;
+    next.MPI_Test(&pendingAcks[i].req, &flag, MPI_STATUS_IGNORE);
+    if (flag) {
+      device_pool().put(pendingAcks[i].slab);
+      pendingAcks[i] = pendingAcks.back();
+      pendingAcks.pop_back();
+      moved = true;
+    } else {
+      ++i;
+    }
+  }
+  return moved;
+}
+
+bool busy() { return !active.empty() || !pendingAcks.empty(); }
+
+int wait(MPI_Request *req, MPI_Status *status) {
+  const uint32_t h = uint32_t(*req);
+  auto it = active.find(h);
+  if (it == active.end()) return next.MPI_Wait(req, status);
+  while (!it->second->done) progress();
+  it->second->status(status);
+  active.erase(it);
+  *req = MPI_REQUEST_NULL;
+  return MPI_SUCCESS;
+}
+
+int test(MPI_Request *req, int *flag, MPI_Status *status) {
+  const uint32_t h = uint32_t(*req);
+  auto it = active.find(h);
+  if (it == active.end()) return next.MPI_Test(req, flag, status);
+  progress();
+  *flag = it->second->done ? 1 : 0;
+  if (*flag) {
+    it->second->status(status);
+    active.erase(it);
+    *req = MPI_REQUEST_NULL;
+  }
+  return MPI_SUCCESS;
+}
+
+int recv_host_ipc_aware(void *buf, int count, MPI_Datatype dt, int source, int tag, MPI_Comm comm,
+                        MPI_Status *status, bool *handled) {
+  *handled = false;
+  if (!state.active || !gpu::available() || source == MPI_PROC_NULL) return MPI_SUCCESS;
+  MPI_Message msg;
+  MPI_Status st;
+  // keep TEMPI operations moving while we wait for the message
+  for (;;) {
+    int flag = 0;
+    MPI_Improbe(source, tag, comm, &flag, &msg, &st);
+    if (flag) break;
+    progress();
+  }
+  *handled = true;
+  int n = 0;
+  MPI_Get_count(&st, MPI_BYTE, &n);
+  if (size_t(n) != sizeof(IpcDesc)) return MPI_Mrecv(buf, count, dt, &msg, status);
+  IpcDesc d;
+  MPI_Mrecv(&d, n, MPI_BYTE, &msg, &st);
+  int size = 0;
+  MPI_Type_size(dt, &size);
+  std::vector<char> packed;
+  int nbytes = n;
+  const char *src = reinterpret_cast<const char *>(&d);
+  if (d.magic[0] == kMagic0 && d.magic[1] == kMagic1) { // pull over IPC
+    packed.resize(size_t(std::max<int64_t>(d.bytes, 1)));
+    gpu::check(tempi_hip_memcpy(packed.data(), static_cast<const char *>(peer_pointer(d)) + d.offset,
+                                size_t(d.bytes)),
+               "ipc pull");
+    send_ack(d);
+    src = packed.data();
+    nbytes = int(d.bytes);
+  }
+  const int elems = size ? nbytes / size : 0;
+  int pos = 0;
+  next.MPI_Unpack(src, nbytes, &pos, buf, elems, dt, comm);
+  if (status != MPI_STATUS_IGNORE) {
+    *status = st;
+    MPI_Status_set_elements(status, dt, elems);
+  }
+  return MPI_SUCCESS;
+}
+
+} // namespace p2p
+} // namespace tempi

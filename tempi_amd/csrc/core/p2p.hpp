@@ -1,0 +1,63 @@
+// tempi_amd/csrc/core/p2p.hpp -- strided point-to-point transfers of device
+// buffers: method selection and the Isend / Irecv state machines.
+//
+// Reference counterparts: the blocking senders (/root/reference/src/internal/
+// sender.cpp:26-328: DEVICE / ONE_SHOT / STAGED, AUTO by model) and the async
+// operations (/root/reference/src/internal/async_operation.cpp:71-521:
+// Isend = pack -> event -> MPI_Start of a persistent send; Irecv = MPI_Irecv ->
+// MPI_Test -> unpack).
+//
+// Methods (TEMPI_DATATYPE_*; every method sends the same wire format, the
+// packed bytes as MPI_PACKED, except IPC):
+//   ONESHOT  the pack kernel writes straight into pinned, mapped host memory,
+//            the library sends it; the receiver's unpack kernel reads the
+//            received pinned buffer directly
+//   STAGED   pack into device memory, copy to pinned host, library send
+//   DEVICE   pack into device memory and hand the device buffer to the library
+//            (needs a GPU-aware MPI: TEMPI_MPI_GPU_AWARE=1). Without one, the
+//            DEVICE choice is carried out by IPC for co-located peers, STAGED
+//            otherwise
+//   IPC      (MI355X-native, intra-node) pack into a device slab, send a
+//            128-byte descriptor (IPC handle + offset) through the library;
+//            the receiver maps the sender's slab and its unpack kernel reads
+//            the packed bytes over xGMI, then acknowledges so the sender can
+//            reuse the slab
+//   AUTO     IPC for co-located peers at >= TEMPI_IPC_MIN_BYTES (64 KiB),
+//            ONESHOT otherwise (with no perf.json the reference would stop
+//            here with LOG_FATAL: SURVEY F10)
+// Receives are adaptive: a TEMPI device receive lands in pinned host memory
+// and recognises an IPC descriptor by size + 16-byte magic, so it works with
+// any sender method. An IPC send needs a TEMPI receive on the other side
+// (device buffer, or a blocking MPI_Recv of any buffer).
+#pragma once
+
+#include <mpi.h>
+
+namespace tempi {
+namespace p2p {
+
+void init();
+void finalize();
+
+// true when TEMPI handles this send / receive (otherwise: library)
+bool handles(const void *buf, int count, MPI_Datatype dt, int peer);
+
+int isend(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Comm comm, MPI_Request *req);
+int irecv(void *buf, int count, MPI_Datatype dt, int source, int tag, MPI_Comm comm, MPI_Request *req);
+
+bool is_tempi_request(MPI_Request r);
+// drive every TEMPI operation one step; returns true if anything moved
+bool progress();
+bool busy(); // active operations or unacknowledged IPC slabs exist
+
+// complete a TEMPI request (blocking); fills status, sets *req to NULL
+int wait(MPI_Request *req, MPI_Status *status);
+// non-blocking: *flag = completion
+int test(MPI_Request *req, int *flag, MPI_Status *status);
+
+// blocking MPI_Recv into a host buffer that may receive an IPC descriptor
+int recv_host_ipc_aware(void *buf, int count, MPI_Datatype dt, int source, int tag, MPI_Comm comm,
+                        MPI_Status *status, bool *handled);
+
+} // namespace p2p
+} // namespace tempi

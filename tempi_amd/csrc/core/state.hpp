@@ -23,4 +23,11 @@ int raise_error(MPI_Comm comm, int code);
 void init_after_mpi();
 void finalize_before_mpi();
 
+// TEMPI's MPI_Pack / MPI_Unpack (GPU kernels, or the library with host
+// staging for types that are not strided blocks)
+int pack(const void *inbuf, int incount, MPI_Datatype datatype, void *outbuf, int outsize, int *position,
+         MPI_Comm comm);
+int unpack(const void *inbuf, int insize, int *position, void *outbuf, int outcount, MPI_Datatype datatype,
+           MPI_Comm comm);
+
 } // namespace tempi

@@ -1,0 +1,26 @@
+// tempi_amd/csrc/core/topology.hpp -- which ranks share this node.
+//
+// The reference allgathers MPI_Get_processor_name at init and per cached
+// communicator (/root/reference/src/internal/topology.cpp:34-90) and answers
+// is_colocated (:191-196). Here: one allgather of host names over
+// MPI_COMM_WORLD at MPI_Init; other communicators are mapped to world ranks
+// with MPI_Group_translate_ranks on demand (no stale per-handle cache). The
+// reference's app/library rank permutation exists only for KaHIP/METIS
+// placement, which is out of scope (identity here: SURVEY F12).
+#pragma once
+
+#include <mpi.h>
+
+namespace tempi {
+namespace topology {
+
+void init();
+void finalize();
+int world_rank(MPI_Comm comm, int rank); // MPI_UNDEFINED if not in world
+bool colocated(MPI_Comm comm, int rank);
+bool colocated_world(int worldRank);
+int node_local_rank(); // this rank's index among the ranks on its node
+int ranks_on_node();
+
+} // namespace topology
+} // namespace tempi

@@ -24,8 +24,11 @@
 //    Montgomery) for words-per-row and every dimension count; offsets are
 //    64-bit (extents of several GiB are fine; the reference's are 32-bit, F6).
 //    One decode per chunk, then an odometer step per row change.
-//  * Grid: 256-thread workgroups (4 waves), grid-stride over chunks, sized to
-//    >= 16 workgroups per CU on 256 CUs; each lane keeps U chunks in flight.
+//  * Grid: 256-thread workgroups (4 waves), up to 65536 of them (256 per CU),
+//    grid-stride beyond; each lane keeps U chunks in flight (U = 2 for 8/16-byte
+//    words). Packed-side accesses are nontemporal, and so are strided-side
+//    ones when the word is 16 bytes: every byte is touched once. Measured on
+//    MI355X (tools/kbench.cpp): +12% over plain loads/stores at 512-byte rows.
 //  * Launches larger than 2^31 words are split on the host.
 #include <hip/hip_runtime.h>
 
@@ -66,10 +69,64 @@ template <> struct Word<4> { typedef uint32_t T; };
 template <> struct Word<8> { typedef uint2 T; };
 template <> struct Word<16> { typedef uint4 T; };
 
-// chunks each lane keeps in flight per grid-stride step
-template <int W> struct Unroll { static constexpr int U = W >= 8 ? 4 : (W == 4 ? 2 : 1); };
+// tuning knobs (defaults are the measured best; tools/kbench.cpp sweeps them)
+#ifndef TEMPI_UNROLL_WIDE
+#define TEMPI_UNROLL_WIDE 2
+#endif
+#ifndef TEMPI_UNROLL_NARROW
+#define TEMPI_UNROLL_NARROW 1
+#endif
+#ifndef TEMPI_MAX_BLOCKS
+#define TEMPI_MAX_BLOCKS 65536
+#endif
+#ifndef TEMPI_BLOCK
+#define TEMPI_BLOCK 256
+#endif
+#ifndef TEMPI_NT
+// 0: plain; 1: nontemporal packed side; 2: nontemporal both sides;
+// 3: packed side always, strided side when its words are 16 bytes (a
+//    narrower word's line is re-read by the next word of the same lane)
+#define TEMPI_NT 3
+#endif
+constexpr bool kNtPacked = TEMPI_NT >= 1;
+template <int W> struct NtStrided { static constexpr bool value = TEMPI_NT == 2 || (TEMPI_NT == 3 && W == 16); };
 
-constexpr int kBlock = 256;
+// chunks each lane keeps in flight per grid-stride step
+template <int W> struct Unroll {
+  static constexpr int U = W >= 8 ? TEMPI_UNROLL_WIDE : (W == 4 ? 2 : TEMPI_UNROLL_NARROW);
+};
+
+constexpr int kBlock = TEMPI_BLOCK;
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+// plain or nontemporal (streaming) access; HIP's uint2/uint4 are structs, so
+// the builtins see their native vector form
+template <typename T> struct NativeOf { typedef T type; };
+template <> struct NativeOf<uint4> { typedef u32x4 type; };
+template <> struct NativeOf<uint2> { typedef u32x2 type; };
+
+template <typename T> __device__ __forceinline__ T ld(const T *p, bool nt) {
+  if (nt) {
+    typedef typename NativeOf<T>::type N;
+    N v = __builtin_nontemporal_load(reinterpret_cast<const N *>(p));
+    T r;
+    __builtin_memcpy(&r, &v, sizeof r);
+    return r;
+  }
+  return *p;
+}
+template <typename T> __device__ __forceinline__ void st(T *p, const T &v, bool nt) {
+  if (nt) {
+    typedef typename NativeOf<T>::type N;
+    N n;
+    __builtin_memcpy(&n, &v, sizeof n);
+    __builtin_nontemporal_store(n, reinterpret_cast<N *>(p));
+  } else {
+    *p = v;
+  }
+}
 
 template <int ND> struct KArgs {
   char *chunk0;   // 16-byte aligned address of packed chunk 0 (<= packed start)
@@ -147,11 +204,11 @@ __device__ void partial_chunk(uint32_t c, const KArgs<ND> &a) {
     const int64_t q = q0 + j;
     if (q < 0 || q >= int64_t(a.nwords)) continue;
     WT *pk = reinterpret_cast<WT *>(a.chunk0 + size_t(c) * 16) + j;
-    WT *st = reinterpret_cast<WT *>(a.strided + word_offset<W, ND>(uint32_t(q), a));
+    WT *sp = reinterpret_cast<WT *>(a.strided + word_offset<W, ND>(uint32_t(q), a));
     if (PACK)
-      *pk = *st;
+      *pk = *sp;
     else
-      *st = *pk;
+      *sp = *pk;
   }
 }
 
@@ -179,7 +236,7 @@ __global__ __launch_bounds__(kBlock) void pack_kernel(const KArgs<ND> a) {
         int64_t off = row_offset<ND>(row, a, dig);
 #pragma unroll
         for (int j = 0; j < CW; ++j) {
-          buf[u].w[j] = *reinterpret_cast<const WT *>(a.strided + off + int64_t(w) * W);
+          buf[u].w[j] = ld(reinterpret_cast<const WT *>(a.strided + off + int64_t(w) * W), NtStrided<W>::value);
           if (j + 1 < CW && ++w == a.wpr) {
             w = 0;
             next_row<ND>(off, dig, a);
@@ -191,7 +248,7 @@ __global__ __launch_bounds__(kBlock) void pack_kernel(const KArgs<ND> a) {
     for (int u = 0; u < U; ++u) {
       const uint32_t c = base + u * kBlock + threadIdx.x;
       if (full[u]) {
-        *reinterpret_cast<uint4 *>(a.chunk0 + size_t(c) * 16) = buf[u].v;
+        st(reinterpret_cast<uint4 *>(a.chunk0 + size_t(c) * 16), buf[u].v, kNtPacked);
       } else if (c < a.nchunks) {
         partial_chunk<W, ND, true>(c, a);
       }
@@ -214,7 +271,7 @@ __global__ __launch_bounds__(kBlock) void unpack_kernel(const KArgs<ND> a) {
       const uint32_t c = base + u * kBlock + threadIdx.x;
       const int64_t q0 = int64_t(c) * CW - a.head;
       full[u] = c < a.nchunks && q0 >= 0 && q0 + CW <= int64_t(a.nwords);
-      if (full[u]) buf[u].v = *reinterpret_cast<const uint4 *>(a.chunk0 + size_t(c) * 16);
+      if (full[u]) buf[u].v = ld(reinterpret_cast<const uint4 *>(a.chunk0 + size_t(c) * 16), kNtPacked);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -228,7 +285,7 @@ __global__ __launch_bounds__(kBlock) void unpack_kernel(const KArgs<ND> a) {
         int64_t off = row_offset<ND>(row, a, dig);
 #pragma unroll
         for (int j = 0; j < CW; ++j) {
-          *reinterpret_cast<WT *>(a.strided + off + int64_t(w) * W) = buf[u].w[j];
+          st(reinterpret_cast<WT *>(a.strided + off + int64_t(w) * W), buf[u].w[j], NtStrided<W>::value);
           if (j + 1 < CW && ++w == a.wpr) {
             w = 0;
             next_row<ND>(off, dig, a);
@@ -326,7 +383,7 @@ int launch_nd(bool pack, char *packed, char *first, const Norm &n, hipStream_t s
   }
   constexpr int U = Unroll<W>::U;
   uint64_t blocks = (uint64_t(a.nchunks) + kBlock * U - 1) / (kBlock * U);
-  if (blocks > 4096) blocks = 4096; // 16 workgroups per CU, grid-stride beyond
+  if (blocks > TEMPI_MAX_BLOCKS) blocks = TEMPI_MAX_BLOCKS; // grid-stride beyond
   if (blocks == 0) return 0;
   if (pack)
     hipLaunchKernelGGL((pack_kernel<W, ND>), dim3(uint32_t(blocks)), dim3(kBlock), 0, s, a);

@@ -1,0 +1,52 @@
+"""Multi-rank GPU transfers through libtempi.so (mpiexec, ranks share the
+box's GPU(s)): every method of the strided Send/Recv/Isend/Irecv path, the
+strided ping-pong app (config 3) and the 3D halo exchange app (config 4),
+all with byte-exact content checks."""
+import json
+import os
+
+import pytest
+
+from tests import mpi_launch
+
+pytestmark = pytest.mark.gpu
+
+LIB = os.path.join(mpi_launch.ROOT, "tempi_amd", "lib")
+METHODS = {
+    "AUTO": {},
+    "ONESHOT": {"TEMPI_DATATYPE_ONESHOT": "1"},
+    "STAGED": {"TEMPI_DATATYPE_STAGED": "1"},
+    "IPC": {"TEMPI_DATATYPE_IPC": "1"},
+    "DEVICE": {"TEMPI_DATATYPE_DEVICE": "1"},  # no GPU-aware MPI here: IPC intra-node
+}
+
+
+def _json_line(out):
+    for line in out.splitlines():
+        if line.startswith("{"):
+            return json.loads(line)
+    raise AssertionError(out[-3000:])
+
+
+@pytest.mark.parametrize("method", list(METHODS))
+def test_p2p_world_device(gpu, method):
+    rc, out = mpi_launch.run(2, mpi_launch.py("p2p_world.py", "--device"), env=METHODS[method], timeout=240)
+    assert rc == 0 and "RESULT errors=0" in out, out[-4000:]
+
+
+@pytest.mark.parametrize("method", list(METHODS))
+@pytest.mark.parametrize("total,block", [(1024, 1), (1024, 8), (1 << 20, 1), (1 << 20, 16), (4 << 20, 256),
+                                         (4 << 20, 512)])
+def test_pingpong_nd(gpu, method, total, block):
+    rc, out = mpi_launch.run(2, [os.path.join(LIB, "pingpong_nd"), "5", str(total), str(block), "--check"],
+                             env=METHODS[method], timeout=240)
+    r = _json_line(out)
+    assert rc == 0 and r["errors"] == 0, out[-3000:]
+
+
+@pytest.mark.parametrize("ranks,grid", [(1, "48"), (2, "48"), (4, "40"), (3, "30"), (1, "128")])
+def test_halo_exchange_content(gpu, ranks, grid):
+    rc, out = mpi_launch.run(ranks, [os.path.join(LIB, "halo_exchange"), "2", grid, "--quants", "2", "--check"],
+                             timeout=300)
+    r = _json_line(out)
+    assert rc == 0 and r["checked"] and r["errors"] == 0, out[-3000:]

@@ -77,8 +77,10 @@ def test_misaligned_position(mpi, gpu, name, prefix, shift):
     c = G.case(name)
     t, temps, basic = typezoo.build(mpi, c["recipe"])
     try:
-        src_raw = dev_pattern(c["buflen"] + 64, gpu)
-        src = src_raw[shift:shift + c["buflen"]].clone()  # same content, new alignment
+        src_raw = torch.zeros(c["buflen"] + 64, dtype=torch.uint8, device=gpu)
+        src = src_raw[shift:shift + c["buflen"]]  # same content at a `shift`-misaligned address
+        src.copy_(dev_pattern(c["buflen"], gpu))
+        assert src.data_ptr() == src_raw.data_ptr() + shift
         base = torch.full((c["pack_size"] + prefix + 64,), 0xA5, dtype=torch.uint8, device=gpu)
         torch.cuda.synchronize()
         outp = base.data_ptr() + shift

@@ -1,0 +1,92 @@
+// tools/kbench.cpp -- kernel microbenchmark for libtempi_hip.so variants.
+//
+// usage: kbench LIB.so REPS SHAPE...   where SHAPE = block:count1:stride1[:count2:stride2]
+//   (dims outermost first after the block, e.g. 512:2097152:1024)
+// Also times hipMemcpyAsync D2D of the same payload (achievable-copy peak).
+// Prints one JSON line per shape: kernel ms (HIP events, back-to-back
+// launches) and algorithmic GB/s (2 x payload per pack or unpack).
+#include "tempi_hip.h"
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <dlfcn.h>
+#include <string>
+#include <vector>
+
+#define SYM(name) auto name = reinterpret_cast<decltype(&::name)>(dlsym(h, #name)); \
+  if (!name) { std::fprintf(stderr, "missing %s\n", #name); return 2; }
+#define CK(x) do { int e_ = (x); if (e_) { std::fprintf(stderr, "%s: error %d\n", #x, e_); return 3; } } while (0)
+
+int main(int argc, char **argv) {
+  if (argc < 4) {
+    std::fprintf(stderr, "usage: %s LIB REPS SHAPE...\n", argv[0]);
+    return 1;
+  }
+  void *h = dlopen(argv[1], RTLD_NOW | RTLD_LOCAL);
+  if (!h) {
+    std::fprintf(stderr, "dlopen: %s\n", dlerror());
+    return 2;
+  }
+  SYM(tempi_hip_pack) SYM(tempi_hip_unpack) SYM(tempi_hip_malloc) SYM(tempi_hip_free)
+  SYM(tempi_hip_stream_create) SYM(tempi_hip_event_create) SYM(tempi_hip_event_record)
+  SYM(tempi_hip_event_synchronize) SYM(tempi_hip_event_elapsed_ms) SYM(tempi_hip_memcpy_async)
+  SYM(tempi_hip_memset_async) SYM(tempi_hip_stream_synchronize) SYM(tempi_hip_desc_bytes)
+  const int reps = std::atoi(argv[2]);
+  void *s, *e0, *e1;
+  CK(tempi_hip_stream_create(&s));
+  CK(tempi_hip_event_create(&e0, 1));
+  CK(tempi_hip_event_create(&e1, 1));
+  for (int a = 3; a < argc; ++a) {
+    std::vector<long long> v;
+    std::string sh = argv[a];
+    size_t p = 0;
+    while (p <= sh.size()) {
+      size_t q = sh.find(':', p);
+      if (q == std::string::npos) q = sh.size();
+      v.push_back(std::atoll(sh.substr(p, q - p).c_str()));
+      p = q + 1;
+    }
+    tempi_hip_desc d{};
+    d.block = v[0];
+    d.ndims = int((v.size() - 1) / 2);
+    long long extent = d.block;
+    for (int k = 0; k < d.ndims; ++k) {
+      d.counts[k] = v[1 + 2 * k];
+      d.strides[k] = v[2 + 2 * k];
+    }
+    // extent: outermost count * stride (enough for positive strides)
+    extent = d.ndims ? d.counts[0] * d.strides[0] : d.block;
+    const long long payload = tempi_hip_desc_bytes(&d);
+    void *strided, *packed;
+    CK(tempi_hip_malloc(&strided, size_t(extent)));
+    CK(tempi_hip_malloc(&packed, size_t(payload)));
+    CK(tempi_hip_memset_async(strided, 1, size_t(extent), s));
+    float ms[3];
+    for (int mode = 0; mode < 3; ++mode) {
+      for (int w = 0; w < 2; ++w) { // warm-up
+        if (mode == 0) CK(tempi_hip_pack(packed, strided, &d, s));
+        if (mode == 1) CK(tempi_hip_unpack(strided, packed, &d, s));
+        if (mode == 2) CK(tempi_hip_memcpy_async(packed, strided, size_t(payload), s));
+      }
+      CK(tempi_hip_event_record(e0, s));
+      for (int r = 0; r < reps; ++r) {
+        if (mode == 0) CK(tempi_hip_pack(packed, strided, &d, s));
+        if (mode == 1) CK(tempi_hip_unpack(strided, packed, &d, s));
+        if (mode == 2) CK(tempi_hip_memcpy_async(packed, strided, size_t(payload), s));
+      }
+      CK(tempi_hip_event_record(e1, s));
+      CK(tempi_hip_event_synchronize(e1));
+      CK(tempi_hip_event_elapsed_ms(&ms[mode], e0, e1));
+      ms[mode] /= float(reps);
+    }
+    auto gbs = [&](float m) { return 2.0 * double(payload) / (double(m) * 1e-3) / 1e9; };
+    std::printf("{\"lib\": \"%s\", \"shape\": \"%s\", \"payload\": %lld, \"pack_ms\": %.4f, \"unpack_ms\": %.4f, "
+                "\"memcpy_ms\": %.4f, \"pack_gbs\": %.1f, \"unpack_gbs\": %.1f, \"memcpy_gbs\": %.1f}\n",
+                argv[1], argv[a], payload, ms[0], ms[1], ms[2], gbs(ms[0]), gbs(ms[1]), gbs(ms[2]));
+    std::fflush(stdout);
+    tempi_hip_free(strided);
+    tempi_hip_free(packed);
+  }
+  return 0;
+}
