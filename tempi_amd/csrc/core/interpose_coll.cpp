@@ -1,0 +1,194 @@
+// tempi_amd/csrc/core/interpose_coll.cpp -- interposed MPI_Alltoallv for
+// device buffers (config 5).
+//
+// Reference: /root/reference/src/alltoallv.cpp:14-68 dispatching to
+// /root/reference/src/internal/alltoallv_impl.cpp:21-258 (host-staged library
+// alltoallv; Isend/Irecv remote-first; host-staged Isend/Irecv; remote-staged
+// / local-direct), restricted there to MPI_COMM_WORLD and byte counts, with
+// buffer sizes computed as sdispls[last] + counts[last].
+// Here: any intra-communicator and any datatype TEMPI knows (predefined or
+// committed, strided or not), sizes from the true extent of every block.
+//   AUTO / REMOTE_FIRST  per-peer MPI_Isend / MPI_Irecv through tempi::p2p,
+//                        remote peers first then ranks in ring order: device
+//                        to device over IPC (xGMI) between co-located ranks,
+//                        ONESHOT (pinned host) otherwise
+//   STAGED               device -> pinned host copy of the touched spans,
+//                        library MPI_Alltoallv on host memory, copy back
+//   ISIR_STAGED          per-peer Isend / Irecv, every transfer host-staged
+//   ISIR_REMOTE_STAGED   IPC for co-located peers, STAGED for the others
+// Messages travel on a private duplicate of the communicator, so they never
+// match the application's own point-to-point traffic.
+#include "alloc.hpp"
+#include "counters.hpp"
+#include "env.hpp"
+#include "gpu.hpp"
+#include "log.hpp"
+#include "next_mpi.hpp"
+#include "p2p.hpp"
+#include "state.hpp"
+#include "topology.hpp"
+#include "type_cache.hpp"
+
+#include "tempi_mpi.h"
+
+#include <algorithm>
+#include <vector>
+
+#define TEMPI_EXPORT extern "C" __attribute__((visibility("default")))
+
+namespace tempi {
+namespace {
+
+// [lo, hi) bytes from buf touched by blocks (counts[i] elements of t at
+// displs[i] * extent)
+bool span(const int *counts, const int *displs, int n, MPI_Datatype t, int64_t *lo, int64_t *hi) {
+  MPI_Aint lb, ext, tlb, text;
+  MPI_Type_get_extent(t, &lb, &ext);
+  MPI_Type_get_true_extent(t, &tlb, &text);
+  bool any = false;
+  *lo = 0;
+  *hi = 0;
+  for (int i = 0; i < n; ++i) {
+    if (counts[i] <= 0) continue;
+    const int64_t b0 = int64_t(displs[i]) * ext;
+    int64_t a = b0 + tlb, b = b0 + tlb + text;
+    const int64_t d = int64_t(counts[i] - 1) * ext;
+    if (d < 0) a += d; else b += d;
+    if (!any || a < *lo) *lo = a;
+    if (!any || b > *hi) *hi = b;
+    any = true;
+  }
+  return any;
+}
+
+int staged(const void *sendbuf, const int *scounts, const int *sdispls, MPI_Datatype stype, void *recvbuf,
+           const int *rcounts, const int *rdispls, MPI_Datatype rtype, MPI_Comm comm, int n) {
+  int64_t slo, shi, rlo, rhi;
+  const bool s = span(scounts, sdispls, n, stype, &slo, &shi);
+  const bool r = span(rcounts, rdispls, n, rtype, &rlo, &rhi);
+  Slab *hs = s ? pinned_pool().get(size_t(shi - slo), 0) : nullptr;
+  Slab *hr = r ? pinned_pool().get(size_t(rhi - rlo), 0) : nullptr;
+  if (s) gpu::check(tempi_hip_memcpy(hs->host, static_cast<const char *>(sendbuf) + slo, size_t(shi - slo)), "a2av D2H");
+  if (r) gpu::check(tempi_hip_memcpy(hr->host, static_cast<char *>(recvbuf) + rlo, size_t(rhi - rlo)), "a2av D2H");
+  const char *hsend = s ? static_cast<const char *>(hs->host) - slo : nullptr;
+  char *hrecv = r ? static_cast<char *>(hr->host) - rlo : nullptr;
+  const int rc = next.MPI_Alltoallv(hsend, scounts, sdispls, stype, hrecv, rcounts, rdispls, rtype, comm);
+  if (r) gpu::check(tempi_hip_memcpy(static_cast<char *>(recvbuf) + rlo, hr->host, size_t(rhi - rlo)), "a2av H2D");
+  if (hs) pinned_pool().put(hs);
+  if (hr) pinned_pool().put(hr);
+  return rc;
+}
+
+int isir(const void *sendbuf, const int *scounts, const int *sdispls, MPI_Datatype stype, void *recvbuf,
+         const int *rcounts, const int *rdispls, MPI_Datatype rtype, MPI_Comm comm, int n, int rank, int local,
+         int remote) {
+  MPI_Aint lb, sext, rext;
+  MPI_Type_get_extent(stype, &lb, &sext);
+  MPI_Type_get_extent(rtype, &lb, &rext);
+  // remote peers first (their transfers are the long pole), then ring order
+  std::vector<int> order;
+  for (int pass = 0; pass < 2; ++pass)
+    for (int k = 1; k <= n; ++k) {
+      const int p = (rank + k) % n;
+      const bool co = topology::colocated(comm, p);
+      if ((pass == 0) == !co) order.push_back(p);
+    }
+  const int tag = 0x3A2A;
+  std::vector<MPI_Request> reqs;
+  for (int p : order)
+    if (rcounts[p] > 0) {
+      MPI_Request r;
+      char *b = static_cast<char *>(recvbuf) + int64_t(rdispls[p]) * rext;
+      if (p2p::handles(b, rcounts[p], rtype, p))
+        p2p::irecv(b, rcounts[p], rtype, p, tag, comm, &r);
+      else
+        next.MPI_Irecv(b, rcounts[p], rtype, p, tag, comm, &r);
+      reqs.push_back(r);
+    }
+  for (int p : order)
+    if (scounts[p] > 0) {
+      MPI_Request r;
+      const char *b = static_cast<const char *>(sendbuf) + int64_t(sdispls[p]) * sext;
+      const int force = topology::colocated(comm, p) ? local : remote;
+      if (p2p::handles(b, scounts[p], stype, p))
+        p2p::isend(b, scounts[p], stype, p, tag, comm, &r, force);
+      else
+        next.MPI_Isend(b, scounts[p], stype, p, tag, comm, &r);
+      reqs.push_back(r);
+    }
+  int err = MPI_SUCCESS;
+  for (MPI_Request &r : reqs) {
+    const int rc = p2p::is_tempi_request(r) ? p2p::wait(&r, MPI_STATUS_IGNORE) : [&] {
+      for (;;) {
+        int flag = 0;
+        const int e = next.MPI_Test(&r, &flag, MPI_STATUS_IGNORE);
+        if (e != MPI_SUCCESS || flag) return e;
+        p2p::progress();
+      }
+    }();
+    if (rc != MPI_SUCCESS) err = rc;
+  }
+  return err;
+}
+
+MPI_Comm worldDup = MPI_COMM_NULL;
+
+} // namespace
+
+void coll_init() { MPI_Comm_dup(MPI_COMM_WORLD, &worldDup); }
+void coll_finalize() {
+  if (worldDup != MPI_COMM_NULL) MPI_Comm_free(&worldDup);
+}
+
+} // namespace tempi
+
+using namespace tempi;
+
+TEMPI_EXPORT int MPI_Alltoallv(const void *sendbuf, const int sendcounts[], const int sdispls[],
+                               MPI_Datatype sendtype, void *recvbuf, const int recvcounts[], const int rdispls[],
+                               MPI_Datatype recvtype, MPI_Comm comm) {
+  resolve_next();
+  auto lib = [&] {
+    return next.MPI_Alltoallv(sendbuf, sendcounts, sdispls, sendtype, recvbuf, recvcounts, rdispls, recvtype,
+                              comm);
+  };
+  if (!state.active || env.alltoallv == AlltoallvMethod::NONE || !gpu::available() || sendbuf == MPI_IN_PLACE)
+    return lib();
+  int inter = 0;
+  MPI_Comm_test_inter(comm, &inter);
+  if (inter) return lib();
+  int n = 0, rank = 0;
+  MPI_Comm_size(comm, &n);
+  MPI_Comm_rank(comm, &rank);
+  int64_t lo, hi;
+  const bool sdev = span(sendcounts, sdispls, n, sendtype, &lo, &hi) &&
+                    gpu::classify(static_cast<const char *>(sendbuf) + lo).device_accessible;
+  const bool rdev = span(recvcounts, rdispls, n, recvtype, &lo, &hi) &&
+                    gpu::classify(static_cast<char *>(recvbuf) + lo).device_accessible;
+  if (!sdev && !rdev) return lib();
+  if (!type_lookup(sendtype) || !type_lookup(recvtype)) return lib(); // uncommitted: let MPI complain
+  MPI_Comm c = comm;
+  if (comm == MPI_COMM_WORLD)
+    c = worldDup;
+  else
+    MPI_Comm_dup(comm, &c);
+  int rc;
+  switch (env.alltoallv) {
+  case AlltoallvMethod::STAGED:
+    rc = staged(sendbuf, sendcounts, sdispls, sendtype, recvbuf, recvcounts, rdispls, recvtype, c, n);
+    break;
+  case AlltoallvMethod::ISIR_STAGED:
+    rc = isir(sendbuf, sendcounts, sdispls, sendtype, recvbuf, recvcounts, rdispls, recvtype, c, n, rank, 1, 1);
+    break;
+  case AlltoallvMethod::ISIR_REMOTE_STAGED:
+    rc = isir(sendbuf, sendcounts, sdispls, sendtype, recvbuf, recvcounts, rdispls, recvtype, c, n, rank, 3, 1);
+    break;
+  case AlltoallvMethod::AUTO:
+  case AlltoallvMethod::REMOTE_FIRST:
+  default:
+    rc = isir(sendbuf, sendcounts, sdispls, sendtype, recvbuf, recvcounts, rdispls, recvtype, c, n, rank, -1, -1);
+    break;
+  }
+  if (c != worldDup) MPI_Comm_free(&c);
+  return rc;
+}

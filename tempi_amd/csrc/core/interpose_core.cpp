@@ -30,6 +30,9 @@
 
 namespace tempi {
 
+void coll_init();
+void coll_finalize();
+
 State state;
 Counters counters;
 bool kernelProfiling = false;
@@ -50,12 +53,14 @@ void init_after_mpi() {
   state.active = true;
   topology::init();
   p2p::init();
+  coll_init();
   LOG_DEBUG("TEMPI active: rank " << state.worldRank << "/" << state.worldSize
                                   << ", GPU " << (gpu::available() ? "yes" : "no"));
 }
 
 void finalize_before_mpi() {
   if (!state.active) return;
+  coll_finalize();
   p2p::finalize();
   topology::finalize();
   LOG_DEBUG("counters: packs=" << counters.packs << " unpacks=" << counters.unpacks

@@ -414,7 +414,8 @@ bool handles(const void *buf, int count, MPI_Datatype dt, int peer) {
   return gpu::classify(static_cast<const char *>(buf) + first).device_accessible;
 }
 
-int isend(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Comm comm, MPI_Request *req) {
+int isend(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Comm comm, MPI_Request *req,
+          int force) {
   const TypeRecord *rec = type_lookup(dt);
   progress();
   counters.isends++;
@@ -424,7 +425,11 @@ int isend(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Co
   }
   const gpu::Ptr p = gpu::classify(static_cast<const char *>(buf) + rec->desc.start);
   const int64_t bytes = pack_size(count, dt, comm);
-  const Method m = choose(bytes, topology::colocated(comm, dest));
+  const bool colocated = topology::colocated(comm, dest);
+  Method m = choose(bytes, colocated);
+  if (force >= 0) m = Method(force);
+  if (m == Method::IPC && !colocated) m = Method::ONESHOT;
+  if (m == Method::DEVICE && !gpuAwareLibrary) m = colocated ? Method::IPC : Method::STAGED;
   switch (m) {
   case Method::ONESHOT: counters.send_oneshot++; break;
   case Method::STAGED: counters.send_staged++; break;

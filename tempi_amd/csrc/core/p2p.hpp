@@ -42,7 +42,10 @@ void finalize();
 // true when TEMPI handles this send / receive (otherwise: library)
 bool handles(const void *buf, int count, MPI_Datatype dt, int peer);
 
-int isend(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Comm comm, MPI_Request *req);
+// force: -1 = choose by TEMPI_DATATYPE_* / AUTO; else a forced method
+// (0 ONESHOT, 1 STAGED, 2 DEVICE, 3 IPC)
+int isend(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Comm comm, MPI_Request *req,
+          int force = -1);
 int irecv(void *buf, int count, MPI_Datatype dt, int source, int tag, MPI_Comm comm, MPI_Request *req);
 
 bool is_tempi_request(MPI_Request r);

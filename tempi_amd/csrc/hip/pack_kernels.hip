@@ -24,9 +24,10 @@
 //    Montgomery) for words-per-row and every dimension count; offsets are
 //    64-bit (extents of several GiB are fine; the reference's are 32-bit, F6).
 //    One decode per chunk, then an odometer step per row change.
-//  * Grid: 256-thread workgroups (4 waves), up to 65536 of them (256 per CU),
-//    grid-stride beyond; each lane keeps U chunks in flight (U = 2 for 8/16-byte
-//    words). Packed-side accesses are nontemporal, and so are strided-side
+//  * Grid: 256-thread workgroups (4 waves), one 16-byte chunk per lane for
+//    16-byte words (a 1 GiB pack is 262144 workgroups: the dispatcher keeps
+//    every CU full and no lane loops), two chunks per lane for 8-byte words;
+//    grid-stride only beyond 2^20 workgroups. Packed-side accesses are nontemporal, and so are strided-side
 //    ones when the word is 16 bytes: every byte is touched once. Measured on
 //    MI355X (tools/kbench.cpp): +12% over plain loads/stores at 512-byte rows.
 //  * Launches larger than 2^31 words are split on the host.
@@ -70,6 +71,9 @@ template <> struct Word<8> { typedef uint2 T; };
 template <> struct Word<16> { typedef uint4 T; };
 
 // tuning knobs (defaults are the measured best; tools/kbench.cpp sweeps them)
+#ifndef TEMPI_UNROLL_16
+#define TEMPI_UNROLL_16 1
+#endif
 #ifndef TEMPI_UNROLL_WIDE
 #define TEMPI_UNROLL_WIDE 2
 #endif
@@ -77,7 +81,7 @@ template <> struct Word<16> { typedef uint4 T; };
 #define TEMPI_UNROLL_NARROW 1
 #endif
 #ifndef TEMPI_MAX_BLOCKS
-#define TEMPI_MAX_BLOCKS 65536
+#define TEMPI_MAX_BLOCKS (1 << 20)
 #endif
 #ifndef TEMPI_BLOCK
 #define TEMPI_BLOCK 256
@@ -93,7 +97,7 @@ template <int W> struct NtStrided { static constexpr bool value = TEMPI_NT == 2 
 
 // chunks each lane keeps in flight per grid-stride step
 template <int W> struct Unroll {
-  static constexpr int U = W >= 8 ? TEMPI_UNROLL_WIDE : (W == 4 ? 2 : TEMPI_UNROLL_NARROW);
+  static constexpr int U = W == 16 ? TEMPI_UNROLL_16 : W == 8 ? TEMPI_UNROLL_WIDE : (W == 4 ? 2 : TEMPI_UNROLL_NARROW);
 };
 
 constexpr int kBlock = TEMPI_BLOCK;

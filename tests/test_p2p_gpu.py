@@ -50,3 +50,15 @@ def test_halo_exchange_content(gpu, ranks, grid):
                              timeout=300)
     r = _json_line(out)
     assert rc == 0 and r["checked"] and r["errors"] == 0, out[-3000:]
+
+
+A2AV = {"AUTO": {}, "STAGED": {"TEMPI_ALLTOALLV_STAGED": "1"}, "ISIR_STAGED": {"TEMPI_ALLTOALLV_ISIR_STAGED": "1"},
+        "ISIR_REMOTE_STAGED": {"TEMPI_ALLTOALLV_ISIR_REMOTE_STAGED": "1"}}
+
+
+@pytest.mark.parametrize("method", list(A2AV))
+@pytest.mark.parametrize("ranks,scale,nnz", [(2, 100000, 2), (4, 1000, 3), (3, 10, 1)])
+def test_alltoallv_device(gpu, method, ranks, scale, nnz):
+    rc, out = mpi_launch.run(ranks, mpi_launch.py("alltoallv.py", "--device", "--scale", str(scale), "--nnz",
+                                                  str(nnz)), env=A2AV[method], timeout=240)
+    assert rc == 0 and "RESULT errors=0" in out, out[-3000:]

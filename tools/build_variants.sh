@@ -10,12 +10,8 @@ build() { # name flags...
     -Wl,-rpath,/opt/rocm/lib &
 }
 build cur
-build u1b128k -DTEMPI_UNROLL_WIDE=1 -DTEMPI_MAX_BLOCKS=131072
-build u1b256k -DTEMPI_UNROLL_WIDE=1 -DTEMPI_MAX_BLOCKS=262144
-build u2b128k -DTEMPI_MAX_BLOCKS=131072
-build u2b32k -DTEMPI_MAX_BLOCKS=32768
-build u4b64k -DTEMPI_UNROLL_WIDE=4 -DTEMPI_MAX_BLOCKS=65536
-build n2 -DTEMPI_UNROLL_NARROW=2
+build u8_1 -DTEMPI_UNROLL_WIDE=1
+build u16_2 -DTEMPI_UNROLL_16=2
 wait
 g++ -O2 -std=c++17 -Iinclude -o tools/_variants/kbench tools/kbench.cpp -ldl
 ls tools/_variants
