@@ -18,7 +18,7 @@ HIPFLAGS := --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Iinclude -Wall
 CXXFLAGS := -std=c++17 -O2 -g -fPIC -fvisibility=hidden -Wall -Wextra -Wno-unused-parameter \
             -Iinclude -I$(MPI_HOME)/include
 
-APPS := $(LIB)/halo_exchange $(LIB)/pingpong_nd
+APPS := $(LIB)/halo_exchange $(LIB)/pingpong_nd $(LIB)/measure_system
 
 all: $(LIB)/libtempi.so $(APPS) oracle
 
@@ -43,7 +43,7 @@ $(LIB)/libtempi.so: $(CORE_OBJ) $(LIB)/libtempi_hip.so
 
 # applications link -ltempi BEFORE the MPI library, like any TEMPI user
 $(LIB)/%: apps/%.cpp $(LIB)/libtempi.so
-	$(HIPCC) --offload-arch=gfx950 -O2 -std=c++17 -I$(MPI_HOME)/include -o $@ $< -L$(LIB) -ltempi -L$(MPI_HOME)/lib -lmpi \
+	$(HIPCC) --offload-arch=gfx950 -O2 -std=c++17 -Iinclude -I$(MPI_HOME)/include -o $@ $< -L$(LIB) -ltempi -L$(MPI_HOME)/lib -lmpi \
 	    -static-libstdc++ -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,$(MPI_HOME)/lib
 
 oracle:

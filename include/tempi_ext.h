@@ -64,6 +64,24 @@ int64_t tempi_mpi_constant(const char *name, int *found);
 
 const char *tempi_version(void);
 
+/* perf model (include the reference's interpolation rules,
+   /root/reference/src/internal/measure_system.cpp:184-293):
+   times[i] = seconds for 2^i bytes; table[r*cols+c] = seconds for 2^(2r+6)
+   bytes in 2^c-byte blocks. +inf when unknown. */
+double tempi_interp_time(const double *times, int n, int64_t bytes);
+double tempi_interp_2d(const double *table, int rows, int cols, int64_t bytes, int64_t block);
+/* 1 when TEMPI_CACHE_DIR/perf.json was loaded at MPI_Init */
+int tempi_perf_loaded(void);
+/* parse + re-emit a perf.json document (schema check); 0 on success */
+int tempi_perf_roundtrip(const char *json_in, char *json_out, int cap);
+/* override TEMPI_DATATYPE_* at run time: 0 AUTO, 1 ONESHOT, 2 DEVICE,
+   3 STAGED, 4 IPC (used by tools/measure_system) */
+void tempi_set_datatype_method(int method);
+
+/* NIST SP 800-90B sec. 5.1 permutation test: 1 when `samples` look IID
+   (tools/measure_system repeats a measurement until they do) */
+int tempi_sp800_90b_iid(const double *samples, int n, int perms, uint64_t seed);
+
 #ifdef __cplusplus
 }
 #endif

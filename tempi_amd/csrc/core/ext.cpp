@@ -2,7 +2,9 @@
 // (include/tempi_ext.h): type introspection, counters, stream access, and the
 // MPI ABI constants of the library TEMPI was compiled against.
 #include "counters.hpp"
+#include "env.hpp"
 #include "gpu.hpp"
+#include "perf_model.hpp"
 #include "state.hpp"
 #include "type_cache.hpp"
 
@@ -114,4 +116,41 @@ TEMPI_EXPORT int64_t tempi_mpi_constant(const char *name, int *found) {
     }
   if (found) *found = 0;
   return 0;
+}
+
+// ---- perf model (reference interpolation rules; tests replay its KATs)
+
+static std::vector<IidTime> curve_of(const double *t, int n) {
+  std::vector<IidTime> v(size_t(n > 0 ? n : 0));
+  for (int i = 0; i < n; ++i) v[size_t(i)].time = t[i];
+  return v;
+}
+
+TEMPI_EXPORT double tempi_interp_time(const double *times, int n, int64_t bytes) {
+  return interp_time(curve_of(times, n), bytes);
+}
+
+TEMPI_EXPORT double tempi_interp_2d(const double *table, int rows, int cols, int64_t bytes, int64_t block) {
+  std::vector<std::vector<IidTime>> a;
+  for (int r = 0; r < rows; ++r) a.push_back(curve_of(table + size_t(r) * size_t(cols), cols));
+  return interp_2d(a, bytes, block);
+}
+
+TEMPI_EXPORT int tempi_perf_loaded(void) { return systemPerformanceLoaded ? 1 : 0; }
+
+TEMPI_EXPORT int tempi_perf_roundtrip(const char *json_in, char *json_out, int cap) {
+  SystemPerformance sp;
+  std::string err;
+  if (!from_json(json_in, &sp, &err)) return -1;
+  const std::string s = to_json(sp);
+  if (int(s.size()) + 1 > cap) return int(s.size()) + 1;
+  std::memcpy(json_out, s.c_str(), s.size() + 1);
+  return 0;
+}
+
+TEMPI_EXPORT void tempi_set_datatype_method(int m) {
+  // 0 AUTO, 1 ONESHOT, 2 DEVICE, 3 STAGED, 4 IPC (as TEMPI_DATATYPE_*)
+  static const DatatypeMethod map[] = {DatatypeMethod::AUTO, DatatypeMethod::ONESHOT, DatatypeMethod::DEVICE,
+                                       DatatypeMethod::STAGED, DatatypeMethod::IPC};
+  if (m >= 0 && m < 5) env.datatype = map[m];
 }

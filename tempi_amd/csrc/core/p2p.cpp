@@ -7,6 +7,7 @@
 #include "gpu.hpp"
 #include "log.hpp"
 #include "next_mpi.hpp"
+#include "perf_model.hpp"
 #include "state.hpp"
 #include "topology.hpp"
 #include "type_cache.hpp"
@@ -15,6 +16,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <tuple>
 #include <memory>
 #include <unistd.h>
 #include <vector>
@@ -64,6 +66,41 @@ int64_t pack_size(int count, MPI_Datatype dt, MPI_Comm comm) {
   return s;
 }
 
+// AUTO with a measured perf.json: the cheapest modelled method, cached per
+// (colocated, bytes, block) as in the reference (/root/reference/src/internal/
+// sender.cpp:251-290, async_operation.cpp:334-389). The DEVICE curve is
+// carried out by IPC between co-located ranks when the library is not
+// GPU-aware (the intra-node GPU-GPU curve is measured through that path).
+std::map<std::tuple<bool, int64_t, int64_t>, Method> modelCache;
+
+bool model_choice(int64_t bytes, bool colocated, int64_t block, Method *out) {
+  if (!systemPerformanceLoaded) return false;
+  const auto key = std::make_tuple(colocated, bytes, block);
+  auto it = modelCache.find(key);
+  if (it != modelCache.end()) {
+    *out = it->second;
+    return true;
+  }
+  const SystemPerformance &sp = systemPerformance;
+  const Opt o = model_oneshot(sp, colocated, bytes, block);
+  const Opt d = model_device(sp, colocated, bytes, block);
+  const Opt s = model_staged(sp, colocated, bytes, block);
+  Method best = Method::ONESHOT;
+  double t = o.ok ? o.v : 1e300;
+  const Method dev = gpuAwareLibrary ? Method::DEVICE : (colocated ? Method::IPC : Method::STAGED);
+  if (d.ok && d.v < t) {
+    best = dev;
+    t = d.v;
+  }
+  if (s.ok && s.v < t) best = Method::STAGED;
+  if (!o.ok && !d.ok && !s.ok) return false;
+  modelCache[key] = best;
+  *out = best;
+  return true;
+}
+
+int64_t modelBlock = 512; // block length of the type being sent (set per call)
+
 Method choose(int64_t bytes, bool colocated) {
   switch (env.datatype) {
   case DatatypeMethod::ONESHOT:
@@ -76,9 +113,12 @@ Method choose(int64_t bytes, bool colocated) {
   case DatatypeMethod::IPC:
     return colocated ? Method::IPC : Method::ONESHOT;
   case DatatypeMethod::AUTO:
-  default:
+  default: {
+    Method m;
+    if (model_choice(bytes, colocated, modelBlock, &m)) return m;
     if (colocated && bytes >= ipcMinBytes) return Method::IPC;
     return Method::ONESHOT;
+  }
   }
 }
 
@@ -371,6 +411,8 @@ MPI_Request add(std::unique_ptr<Op> op) {
 
 void init() {
   gpuAwareLibrary = std::getenv("TEMPI_MPI_GPU_AWARE") != nullptr;
+  systemPerformanceLoaded = import_system_performance(&systemPerformance);
+  modelCache.clear();
   if (const char *s = std::getenv("TEMPI_IPC_MIN_BYTES")) ipcMinBytes = std::atoll(s);
   MPI_Comm_dup(MPI_COMM_WORLD, &ctrlComm);
   int flag = 0;
@@ -426,6 +468,7 @@ int isend(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Co
   const gpu::Ptr p = gpu::classify(static_cast<const char *>(buf) + rec->desc.start);
   const int64_t bytes = pack_size(count, dt, comm);
   const bool colocated = topology::colocated(comm, dest);
+  modelBlock = std::min<int64_t>(std::max<int64_t>(1, rec->desc.block), 512);
   Method m = choose(bytes, colocated);
   if (force >= 0) m = Method(force);
   if (m == Method::IPC && !colocated) m = Method::ONESHOT;

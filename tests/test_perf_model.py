@@ -1,0 +1,101 @@
+"""Perf-model interpolation (tempi_amd/csrc/core/perf_model.cpp) against the
+reference's known-answer tests (/root/reference/test/measure_system.cpp:13-92)
+and the perf.json schema round trip. No GPU needed."""
+import ctypes
+import json
+import math
+
+import pytest
+
+import tempi_amd
+
+L = ctypes.CDLL(tempi_amd.LIBTEMPI)
+L.tempi_interp_time.restype = ctypes.c_double
+L.tempi_interp_time.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.c_int, ctypes.c_int64]
+L.tempi_interp_2d.restype = ctypes.c_double
+L.tempi_interp_2d.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.c_int, ctypes.c_int, ctypes.c_int64,
+                              ctypes.c_int64]
+L.tempi_perf_roundtrip.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int]
+
+
+def t1(v, b):
+    arr = (ctypes.c_double * len(v))(*v)
+    return L.tempi_interp_time(arr, len(v), b)
+
+
+def t2(rows, b, x):
+    flat = [c for r in rows for c in r]
+    arr = (ctypes.c_double * len(flat))(*flat)
+    return L.tempi_interp_2d(arr, len(rows), len(rows[0]), b, x)
+
+
+# /root/reference/test/measure_system.cpp:16-42
+@pytest.mark.parametrize("b,exp", [(1, 2), (2, 4), (3, 6), (5, 10), (7, 14)])
+def test_interp_time_kat(b, exp):
+    assert t1([2, 4, 8, 16], b) == exp
+
+
+A = [[14, 18, 22], [16, 20, 24]]  # rows 64 B, 256 B; cols block 1, 2, 4
+
+
+# /root/reference/test/measure_system.cpp:52-89 (bytes=512 is past the table:
+# the reference reads out of bounds there; we must not, and must
+# still give its answers)
+@pytest.mark.parametrize("b,x,exp", [(64, 1, 14), (160, 1, 15), (256, 1, 16), (64, 2, 18), (256, 2, 20),
+                                     (64, 3, 20), (64, 4, 22), (160, 3, 21), (512, 1, 32), (512, 3, 44)])
+def test_interp_2d_kat(b, x, exp):
+    assert t2(A, b, x) == pytest.approx(exp, rel=0, abs=1e-5)
+
+
+def test_unknown_is_inf():
+    assert math.isinf(L.tempi_interp_time((ctypes.c_double * 1)(), 0, 100))
+
+
+def test_interp_time_beyond_table_scales():
+    assert t1([2, 4, 8, 16], 32) == pytest.approx(64)  # 16 s for 8 B, scaled linearly
+
+
+def test_perf_json_roundtrip():
+    doc = {"cudaKernelLaunch": 3.5e-6,
+           "intraNodeCpuCpuPingpong": [{"time": 1e-6, "iid": True}, {"time": 2e-6, "iid": False}],
+           "intraNodeGpuGpuPingpong": [{"time": 3e-6, "iid": True}],
+           "interNodeCpuCpuPingpong": [], "interNodeGpuGpuPingpong": [],
+           "d2h": [{"time": 4e-6, "iid": True}], "h2d": [{"time": 5e-6, "iid": True}],
+           "packDevice": [[{"time": 1e-5, "iid": True}, {"time": 2e-5, "iid": False}]],
+           "unpackDevice": [[{"time": 1e-5, "iid": True}]], "packHost": [], "unpackHost": []}
+    out = ctypes.create_string_buffer(1 << 16)
+    assert L.tempi_perf_roundtrip(json.dumps(doc).encode(), out, 1 << 16) == 0
+    back = json.loads(out.value.decode())
+    for k, v in doc.items():
+        assert back[k] == v, k
+
+
+def test_perf_json_rejects_missing_keys():
+    out = ctypes.create_string_buffer(1024)
+    assert L.tempi_perf_roundtrip(b'{"d2h": []}', out, 1024) != 0
+
+
+L.tempi_sp800_90b_iid.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.c_int, ctypes.c_int, ctypes.c_uint64]
+
+
+def iid(v, perms=10000, seed=1):
+    return bool(L.tempi_sp800_90b_iid((ctypes.c_double * len(v))(*v), len(v), perms, seed))
+
+
+def test_iid_rejects_monotone():
+    # /root/reference/test/iid.cpp:18-24
+    assert not iid([-1, 0, 1, 2, 3, 4, 5])
+    assert not iid(list(range(100)))
+
+
+def test_iid_accepts_random_eventually():
+    # /root/reference/test/iid.cpp:26-45: uniform samples of 10 pass eventually
+    import numpy as np
+
+    rng = np.random.default_rng(5)
+    passed = any(iid(list(rng.uniform(0, 10000, 10)), perms=2000, seed=k) for k in range(20))
+    assert passed
+
+
+def test_iid_rejects_periodic():
+    assert not iid([1.0, 2.0] * 50, perms=2000)
