@@ -26,6 +26,7 @@
   X(MPI_Wait)                                                                  \
   X(MPI_Waitall)                                                               \
   X(MPI_Test)                                                                  \
+  X(MPI_Testsome)                                                                  \
   X(MPI_Alltoallv)
 
 namespace tempi {

@@ -15,6 +15,7 @@
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <map>
 #include <tuple>
 #include <memory>
@@ -141,37 +142,60 @@ void send_ack(const IpcDesc &d) {
 }
 
 // ---------------------------------------------------------------- operations
+//
+// Every operation is a small state machine with at most one GPU event and at
+// most one library request outstanding. progress() polls GPU events in
+// creation order and stops at the first one that is not complete (all TEMPI
+// work of a device runs on one in-order stream, so later events cannot be
+// complete either), then tests every outstanding library request with a
+// single MPI_Testsome. A pass therefore costs O(newly completed) HIP queries
+// plus one library call, instead of one query and one MPI_Test per operation
+// (the reference's try_progress wakes every operation: async_operation.cpp:
+// 501-513).
 
-struct Op {
-  virtual ~Op() {}
-  virtual bool step() = 0; // true when complete
-  virtual void status(MPI_Status *s) const = 0;
-  bool done = false;
-};
+std::vector<void *> eventPool;
 
-void *make_event() {
+void *get_event() {
+  if (!eventPool.empty()) {
+    void *e = eventPool.back();
+    eventPool.pop_back();
+    return e;
+  }
   void *e = nullptr;
   gpu::check(tempi_hip_event_create(&e, 0), "event create");
   return e;
 }
 
+void put_event(void *e) {
+  if (e) eventPool.push_back(e);
+}
+
+struct Op {
+  virtual ~Op() { put_event(event); }
+  virtual void gpu_done() {}                   // event completed
+  virtual void lib_done(const MPI_Status &) {} // library request completed
+  virtual void status(MPI_Status *s) const = 0;
+  void *event = nullptr;                  // outstanding GPU work
+  int device = 0;
+  MPI_Request lib = MPI_REQUEST_NULL;     // outstanding library request
+  bool done = false;
+};
+
 struct IsendOp : Op {
   Packer packer;
   const char *origin; // GPU-visible
-  int count, dest, tag, device;
+  int count, dest, tag;
   MPI_Datatype dt;
   MPI_Comm comm;
   Method method;
   int64_t bytes;
   Slab *dslab = nullptr, *hslab = nullptr;
-  void *event = nullptr;
-  MPI_Request lib = MPI_REQUEST_NULL;
   IpcDesc desc{};
-  enum { PACKING, SENDING } st = PACKING;
 
   IsendOp(const TypeRecord &rec, const char *o, int c, MPI_Datatype d, int de, int t, MPI_Comm cm, int dev,
           Method m, int64_t b)
-      : packer(rec.desc), origin(o), count(c), dest(de), tag(t), device(dev), dt(d), comm(cm), method(m), bytes(b) {
+      : packer(rec.desc), origin(o), count(c), dest(de), tag(t), dt(d), comm(cm), method(m), bytes(b) {
+    device = dev;
     void *s = gpu::stream(device);
     int e = 0;
     if (method == Method::ONESHOT) {
@@ -186,14 +210,11 @@ struct IsendOp : Op {
       }
     }
     gpu::check(e, "isend pack");
-    event = make_event();
+    event = get_event();
     gpu::check(tempi_hip_event_record(event, s), "event record");
   }
-  ~IsendOp() override {
-    if (event) tempi_hip_event_destroy(event);
-  }
 
-  void start_send() {
+  void gpu_done() override { // packed: hand it to the library
     switch (method) {
     case Method::ONESHOT:
     case Method::STAGED:
@@ -213,13 +234,13 @@ struct IsendOp : Op {
       desc.ackTag = int32_t(dslab->id % uint32_t(tagUb));
       desc.rawPtr = reinterpret_cast<uint64_t>(dslab->dev);
       std::memcpy(desc.handle, slab_ipc_handle(dslab), sizeof desc.handle);
-      // the ack comes from the receiver on the private communicator
+      // the slab is reused once the receiver acknowledges (private comm)
       const int peer = topology::world_rank(comm, dest);
       PendingAck pa{MPI_REQUEST_NULL, dslab};
       static char sink;
       next.MPI_Irecv(&sink, 0, MPI_BYTE, peer, desc.ackTag, ctrlComm, &pa.req);
       pendingAcks.push_back(pa);
-      dslab = nullptr; // owned by the pending ack now
+      dslab = nullptr;
       next.MPI_Isend(&desc, int(sizeof desc), MPI_PACKED, dest, tag, comm, &lib);
       break;
     }
@@ -227,24 +248,11 @@ struct IsendOp : Op {
       break;
     }
   }
-
-  bool step() override {
-    if (done) return true;
-    if (st == PACKING) {
-      const int q = tempi_hip_event_query(event);
-      if (q == 1) return false;
-      gpu::check(q, "isend event");
-      start_send();
-      st = SENDING;
-    }
-    int flag = 0;
-    next.MPI_Test(&lib, &flag, MPI_STATUS_IGNORE);
-    if (!flag) return false;
+  void lib_done(const MPI_Status &) override {
     if (dslab) device_pool().put(dslab);
     if (hslab) pinned_pool().put(hslab);
     dslab = hslab = nullptr;
     done = true;
-    return true;
   }
   void status(MPI_Status *s) const override {
     if (s != MPI_STATUS_IGNORE) {
@@ -259,66 +267,53 @@ struct IsendOp : Op {
 struct IrecvOp : Op {
   Packer packer;
   char *origin; // GPU-visible
-  int count, device;
+  int count;
   MPI_Datatype dt;
   MPI_Comm comm;
   int64_t bytes;
   Slab *hslab = nullptr;
-  void *event = nullptr;
-  MPI_Request lib = MPI_REQUEST_NULL;
   MPI_Status libStatus{};
   IpcDesc desc{};
   bool ipc = false;
   int64_t elems = 0;
-  enum { RECEIVING, UNPACKING } st = RECEIVING;
 
   IrecvOp(const TypeRecord &rec, char *o, int c, MPI_Datatype d, int source, int tag, MPI_Comm cm, int dev,
           int64_t b)
-      : packer(rec.desc), origin(o), count(c), device(dev), dt(d), comm(cm), bytes(b) {
+      : packer(rec.desc), origin(o), count(c), dt(d), comm(cm), bytes(b) {
+    device = dev;
     const size_t cap = std::max<size_t>(size_t(bytes), sizeof(IpcDesc));
     hslab = pinned_pool().get(cap, device);
     next.MPI_Irecv(hslab->host, int(cap), MPI_PACKED, source, tag, comm, &lib);
   }
-  ~IrecvOp() override {
-    if (event) tempi_hip_event_destroy(event);
-  }
 
-  bool step() override {
-    if (done) return true;
-    if (st == RECEIVING) {
-      int flag = 0;
-      next.MPI_Test(&lib, &flag, &libStatus);
-      if (!flag) return false;
-      int n = 0;
-      MPI_Get_count(&libStatus, MPI_PACKED, &n);
-      void *s = gpu::stream(device);
-      const unsigned char *hb = static_cast<const unsigned char *>(hslab->host);
-      IpcDesc d;
-      std::memcpy(&d, hb, std::min<size_t>(sizeof d, size_t(n)));
-      if (size_t(n) == sizeof(IpcDesc) && d.magic[0] == kMagic0 && d.magic[1] == kMagic1) {
-        ipc = true;
-        desc = d;
-        const char *peer = static_cast<const char *>(peer_pointer(d)) + d.offset;
-        elems = packer.desc().size ? d.bytes / packer.desc().size : 0;
-        if (d.bytes > bytes) LOG_FATAL("message truncated: " << d.bytes << " B into " << bytes);
-        gpu::check(packer.unpack_async(origin, peer, elems, s), "irecv ipc unpack");
-      } else {
-        if (int64_t(n) > bytes) LOG_FATAL("message truncated: " << n << " B into " << bytes);
-        elems = packer.desc().size ? n / packer.desc().size : 0;
-        gpu::check(packer.unpack_async(origin, hslab->dev, elems, s), "irecv unpack");
-      }
-      event = make_event();
-      gpu::check(tempi_hip_event_record(event, s), "event record");
-      st = UNPACKING;
+  void lib_done(const MPI_Status &st) override { // arrived: unpack it
+    libStatus = st;
+    int n = 0;
+    MPI_Get_count(&libStatus, MPI_PACKED, &n);
+    void *s = gpu::stream(device);
+    IpcDesc d;
+    std::memcpy(&d, hslab->host, std::min<size_t>(sizeof d, size_t(n)));
+    const int64_t size = packer.desc().size;
+    if (size_t(n) == sizeof(IpcDesc) && d.magic[0] == kMagic0 && d.magic[1] == kMagic1) {
+      ipc = true;
+      desc = d;
+      if (d.bytes > bytes) LOG_FATAL("message truncated: " << d.bytes << " B into " << bytes);
+      const char *peer = static_cast<const char *>(peer_pointer(d)) + d.offset;
+      elems = size ? d.bytes / size : 0;
+      gpu::check(packer.unpack_async(origin, peer, elems, s), "irecv ipc unpack");
+    } else {
+      if (int64_t(n) > bytes) LOG_FATAL("message truncated: " << n << " B into " << bytes);
+      elems = size ? n / size : 0;
+      gpu::check(packer.unpack_async(origin, hslab->dev, elems, s), "irecv unpack");
     }
-    const int q = tempi_hip_event_query(event);
-    if (q == 1) return false;
-    gpu::check(q, "irecv event");
+    event = get_event();
+    gpu::check(tempi_hip_event_record(event, s), "event record");
+  }
+  void gpu_done() override {
     if (ipc) send_ack(desc);
     pinned_pool().put(hslab);
     hslab = nullptr;
     done = true;
-    return true;
   }
   void status(MPI_Status *s) const override {
     if (s != MPI_STATUS_IGNORE) {
@@ -330,23 +325,17 @@ struct IrecvOp : Op {
 };
 
 // library-packed transfer of a device buffer whose type TEMPI cannot pack
-// (the touched span is staged through host memory by MPI_Pack/MPI_Unpack)
+// (the touched span is staged through host memory by tempi::pack / unpack)
 struct LibIsendOp : Op {
   std::vector<char> buf;
-  MPI_Request lib = MPI_REQUEST_NULL;
   MPI_Datatype dt;
   LibIsendOp(const void *b, int c, MPI_Datatype d, int dest, int tag, MPI_Comm comm) : dt(d) {
     buf.resize(size_t(std::max<int64_t>(pack_size(c, d, comm), 1)));
     int pos = 0;
-    tempi::pack(b, c, d, buf.data(), int(buf.size()), &pos, comm); // stages device data
+    tempi::pack(b, c, d, buf.data(), int(buf.size()), &pos, comm);
     next.MPI_Isend(buf.data(), pos, MPI_PACKED, dest, tag, comm, &lib);
   }
-  bool step() override {
-    if (done) return true;
-    int flag = 0;
-    next.MPI_Test(&lib, &flag, MPI_STATUS_IGNORE);
-    return done = flag != 0;
-  }
+  void lib_done(const MPI_Status &) override { done = true; }
   void status(MPI_Status *s) const override {
     if (s != MPI_STATUS_IGNORE) {
       s->MPI_ERROR = MPI_SUCCESS;
@@ -361,25 +350,21 @@ struct LibIrecvOp : Op {
   int count;
   MPI_Datatype dt;
   MPI_Comm comm;
-  MPI_Request lib = MPI_REQUEST_NULL;
   MPI_Status libStatus{};
   int elems = 0;
   LibIrecvOp(void *b, int c, MPI_Datatype d, int source, int tag, MPI_Comm cm) : user(b), count(c), dt(d), comm(cm) {
     buf.resize(size_t(std::max<int64_t>(pack_size(c, d, cm), 1)));
     next.MPI_Irecv(buf.data(), int(buf.size()), MPI_PACKED, source, tag, comm, &lib);
   }
-  bool step() override {
-    if (done) return true;
-    int flag = 0;
-    next.MPI_Test(&lib, &flag, &libStatus);
-    if (!flag) return false;
+  void lib_done(const MPI_Status &st) override {
+    libStatus = st;
     int n = 0, size = 0;
     MPI_Get_count(&libStatus, MPI_PACKED, &n);
     MPI_Type_size(dt, &size);
     elems = size ? n / size : 0;
     int pos = 0;
-    tempi::unpack(buf.data(), n, &pos, user, elems, dt, comm); // stages device data
-    return done = true;
+    tempi::unpack(buf.data(), n, &pos, user, elems, dt, comm);
+    done = true;
   }
   void status(MPI_Status *s) const override {
     if (s != MPI_STATUS_IGNORE) {
@@ -407,6 +392,13 @@ MPI_Request add(std::unique_ptr<Op> op) {
   return MPI_Request(h);
 }
 
+// scratch for progress()
+std::vector<MPI_Request> pollReqs;
+std::vector<Op *> pollOps;   // nullptr: a pending ack
+std::vector<size_t> pollAck; // index into pendingAcks
+std::vector<int> pollIdx;
+std::vector<MPI_Status> pollSt;
+
 } // namespace
 
 void init() {
@@ -425,13 +417,18 @@ void finalize() {
   // complete everything the application left behind, then wait (bounded) for
   // the acks that let us release IPC slabs
   const auto t0 = std::chrono::steady_clock::now();
-  for (auto &kv : active)
-    while (!kv.second->step()) {
-      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(30)) {
-        LOG_WARN("request left incomplete at MPI_Finalize");
-        break;
-      }
+  auto all_done = [] {
+    for (auto &kv : active)
+      if (!kv.second->done) return false;
+    return true;
+  };
+  while (!all_done()) {
+    progress();
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(30)) {
+      LOG_WARN("request(s) left incomplete at MPI_Finalize");
+      break;
     }
+  }
   active.clear();
   while (!pendingAcks.empty()) {
     progress();
@@ -441,6 +438,8 @@ void finalize() {
       pendingAcks.clear();
     }
   }
+  for (void *e : eventPool) tempi_hip_event_destroy(e);
+  eventPool.clear();
   for (auto &kv : ipcOpen) tempi_hip_ipc_close_handle(kv.second);
   ipcOpen.clear();
   if (ctrlComm != MPI_COMM_NULL) MPI_Comm_free(&ctrlComm);
@@ -511,18 +510,63 @@ bool is_tempi_request(MPI_Request r) {
 
 bool progress() {
   bool moved = false;
-  for (auto &kv : active)
-    if (!kv.second->done) moved |= kv.second->step();
-  for (size_t i = 0; i < pendingAcks.size();) {
-    int flag = 0;
-    next.MPI_Test(&pendingAcks[i].req, &flag, MPI_STATUS_IGNORE);
-    if (flag) {
-      device_pool().put(pendingAcks[i].slab);
-      pendingAcks[i] = pendingAcks.back();
-      pendingAcks.pop_back();
+  // 1. GPU events, in stream order
+  int blockedDevice = -1;
+  for (auto &kv : active) {
+    Op *op = kv.second.get();
+    if (!op->event || op->device == blockedDevice) continue;
+    const int q = tempi_hip_event_query(op->event);
+    if (q == 1) {
+      blockedDevice = op->device; // later work of that stream cannot be done
+      continue;
+    }
+    gpu::check(q, "event query");
+    put_event(op->event);
+    op->event = nullptr;
+    op->gpu_done();
+    moved = true;
+  }
+  // 2. every outstanding library request in one MPI_Testsome
+  pollReqs.clear();
+  pollOps.clear();
+  pollAck.clear();
+  for (auto &kv : active) {
+    Op *op = kv.second.get();
+    if (op->lib != MPI_REQUEST_NULL && !op->done) {
+      pollReqs.push_back(op->lib);
+      pollOps.push_back(op);
+      pollAck.push_back(0);
+    }
+  }
+  for (size_t i = 0; i < pendingAcks.size(); ++i) {
+    pollReqs.push_back(pendingAcks[i].req);
+    pollOps.push_back(nullptr);
+    pollAck.push_back(i);
+  }
+  if (!pollReqs.empty()) {
+    const int n = int(pollReqs.size());
+    pollIdx.resize(size_t(n));
+    pollSt.resize(size_t(n));
+    int outcount = 0;
+    next.MPI_Testsome(n, pollReqs.data(), &outcount, pollIdx.data(), pollSt.data());
+    if (outcount == MPI_UNDEFINED) outcount = 0;
+    std::vector<size_t> ackedSlots;
+    for (int k = 0; k < outcount; ++k) {
+      const size_t i = size_t(pollIdx[size_t(k)]);
+      if (Op *op = pollOps[i]) {
+        op->lib = MPI_REQUEST_NULL;
+        op->lib_done(pollSt[size_t(k)]);
+      } else {
+        ackedSlots.push_back(pollAck[i]);
+      }
       moved = true;
-    } else {
-      ++i;
+    }
+    // release acknowledged slabs (highest index first keeps indices valid)
+    std::sort(ackedSlots.rbegin(), ackedSlots.rend());
+    for (size_t a : ackedSlots) {
+      device_pool().put(pendingAcks[a].slab);
+      pendingAcks[a] = pendingAcks.back();
+      pendingAcks.pop_back();
     }
   }
   return moved;
