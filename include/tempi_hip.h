@@ -54,6 +54,18 @@ int tempi_hip_pack(void *packed, const void *first, const tempi_hip_desc *d,
 /* scatter: strided object whose first byte is `first` <- packed[0 .. bytes) */
 int tempi_hip_unpack(void *first, const void *packed, const tempi_hip_desc *d,
                      void *stream);
+/* Many objects in as few launches as possible (one per word width x rank
+   group, up to a few dozen objects per launch): item i gathers (pack) or
+   scatters (unpack) between items[i].packed and the strided object whose
+   first byte is items[i].first. Used for bursts of MPI_Isend / MPI_Irecv. */
+typedef struct tempi_hip_batch_item {
+  void *packed;
+  void *first;
+  tempi_hip_desc desc;
+} tempi_hip_batch_item;
+int tempi_hip_pack_batch(const tempi_hip_batch_item *items, int n, void *stream);
+int tempi_hip_unpack_batch(const tempi_hip_batch_item *items, int n, void *stream);
+
 /* number of packed bytes a descriptor describes */
 int64_t tempi_hip_desc_bytes(const tempi_hip_desc *d);
 /* the word width (1,2,4,8,16) the kernels will use for these pointers */

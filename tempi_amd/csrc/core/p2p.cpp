@@ -16,6 +16,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <algorithm>
+#include <deque>
 #include <map>
 #include <tuple>
 #include <memory>
@@ -170,16 +171,76 @@ void put_event(void *e) {
   if (e) eventPool.push_back(e);
 }
 
+// one batched launch (+ its trailing copies) and the event that follows it
+struct GpuBatch {
+  void *event = nullptr;
+  int device = 0;
+  bool complete = false;
+};
+std::deque<std::shared_ptr<GpuBatch>> batches; // launch order
+
 struct Op {
-  virtual ~Op() { put_event(event); }
-  virtual void gpu_done() {}                   // event completed
+  virtual ~Op() {}
+  virtual void gpu_done() {}                   // its GPU work completed
   virtual void lib_done(const MPI_Status &) {} // library request completed
   virtual void status(MPI_Status *s) const = 0;
-  void *event = nullptr;                  // outstanding GPU work
+  bool queued = false;                         // GPU work not launched yet
+  std::shared_ptr<GpuBatch> batch;             // launched GPU work
   int device = 0;
-  MPI_Request lib = MPI_REQUEST_NULL;     // outstanding library request
+  MPI_Request lib = MPI_REQUEST_NULL;          // outstanding library request
   bool done = false;
 };
+
+// GPU work waiting for the next flush: gathers of Isends, scatters of Irecvs
+struct Pending {
+  Op *op;
+  std::vector<tempi_hip_batch_item> items;
+  void *copyDst = nullptr, *copySrc = nullptr; // STAGED: D2H copy after the pack
+  size_t copyBytes = 0;
+};
+std::vector<Pending> pendingPack, pendingUnpack;
+constexpr size_t kMaxPending = 512;
+
+void flush_list(std::vector<Pending> &list, bool pack) {
+  if (list.empty()) return;
+  // group by device (almost always one)
+  std::vector<int> devices;
+  for (const Pending &p : list)
+    if (std::find(devices.begin(), devices.end(), p.op->device) == devices.end()) devices.push_back(p.op->device);
+  for (int dev : devices) {
+    std::vector<tempi_hip_batch_item> items;
+    for (const Pending &p : list)
+      if (p.op->device == dev) items.insert(items.end(), p.items.begin(), p.items.end());
+    void *s = gpu::stream(dev);
+    int cur = 0;
+    tempi_hip_get_device(&cur);
+    if (cur != dev) tempi_hip_set_device(dev);
+    counters.launches++;
+    gpu::check(pack ? tempi_hip_pack_batch(items.data(), int(items.size()), s)
+                    : tempi_hip_unpack_batch(items.data(), int(items.size()), s),
+               pack ? "batched pack" : "batched unpack");
+    for (const Pending &p : list)
+      if (p.op->device == dev && p.copyBytes)
+        gpu::check(tempi_hip_memcpy_async(p.copyDst, p.copySrc, p.copyBytes, s), "staged D2H");
+    auto b = std::make_shared<GpuBatch>();
+    b->device = dev;
+    b->event = get_event();
+    gpu::check(tempi_hip_event_record(b->event, s), "event record");
+    if (cur != dev) tempi_hip_set_device(cur);
+    for (const Pending &p : list)
+      if (p.op->device == dev) {
+        p.op->queued = false;
+        p.op->batch = b;
+      }
+    batches.push_back(b);
+  }
+  list.clear();
+}
+
+void flush() {
+  flush_list(pendingPack, true);
+  flush_list(pendingUnpack, false);
+}
 
 struct IsendOp : Op {
   Packer packer;
@@ -196,22 +257,23 @@ struct IsendOp : Op {
           Method m, int64_t b)
       : packer(rec.desc), origin(o), count(c), dest(de), tag(t), dt(d), comm(cm), method(m), bytes(b) {
     device = dev;
-    void *s = gpu::stream(device);
-    int e = 0;
+    Pending p;
+    p.op = this;
     if (method == Method::ONESHOT) {
       hslab = pinned_pool().get(size_t(bytes), device);
-      e = packer.pack_async(hslab->dev, origin, count, s);
+      packer.items(hslab->dev, origin, count, p.items);
     } else {
       dslab = device_pool().get(size_t(bytes), device);
-      e = packer.pack_async(dslab->dev, origin, count, s);
-      if (!e && method == Method::STAGED) {
+      packer.items(dslab->dev, origin, count, p.items);
+      if (method == Method::STAGED) {
         hslab = pinned_pool().get(size_t(bytes), device);
-        e = tempi_hip_memcpy_async(hslab->host, dslab->dev, size_t(bytes), s);
+        p.copyDst = hslab->host;
+        p.copySrc = dslab->dev;
+        p.copyBytes = size_t(bytes);
       }
     }
-    gpu::check(e, "isend pack");
-    event = get_event();
-    gpu::check(tempi_hip_event_record(event, s), "event record");
+    queued = true;
+    pendingPack.push_back(std::move(p));
   }
 
   void gpu_done() override { // packed: hand it to the library
@@ -286,28 +348,29 @@ struct IrecvOp : Op {
     next.MPI_Irecv(hslab->host, int(cap), MPI_PACKED, source, tag, comm, &lib);
   }
 
-  void lib_done(const MPI_Status &st) override { // arrived: unpack it
+  void lib_done(const MPI_Status &st) override { // arrived: queue its unpack
     libStatus = st;
     int n = 0;
     MPI_Get_count(&libStatus, MPI_PACKED, &n);
-    void *s = gpu::stream(device);
     IpcDesc d;
     std::memcpy(&d, hslab->host, std::min<size_t>(sizeof d, size_t(n)));
     const int64_t size = packer.desc().size;
+    Pending p;
+    p.op = this;
     if (size_t(n) == sizeof(IpcDesc) && d.magic[0] == kMagic0 && d.magic[1] == kMagic1) {
       ipc = true;
       desc = d;
       if (d.bytes > bytes) LOG_FATAL("message truncated: " << d.bytes << " B into " << bytes);
       const char *peer = static_cast<const char *>(peer_pointer(d)) + d.offset;
       elems = size ? d.bytes / size : 0;
-      gpu::check(packer.unpack_async(origin, peer, elems, s), "irecv ipc unpack");
+      packer.items(const_cast<char *>(peer), origin, elems, p.items);
     } else {
       if (int64_t(n) > bytes) LOG_FATAL("message truncated: " << n << " B into " << bytes);
       elems = size ? n / size : 0;
-      gpu::check(packer.unpack_async(origin, hslab->dev, elems, s), "irecv unpack");
+      packer.items(hslab->dev, origin, elems, p.items);
     }
-    event = get_event();
-    gpu::check(tempi_hip_event_record(event, s), "event record");
+    queued = true;
+    pendingUnpack.push_back(std::move(p));
   }
   void gpu_done() override {
     if (ipc) send_ack(desc);
@@ -458,7 +521,7 @@ bool handles(const void *buf, int count, MPI_Datatype dt, int peer) {
 int isend(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Comm comm, MPI_Request *req,
           int force) {
   const TypeRecord *rec = type_lookup(dt);
-  progress();
+  if (pendingPack.size() >= kMaxPending) flush(); // (no progress(): consecutive Isends share a launch)
   counters.isends++;
   if (!rec->packer) {
     *req = add(std::make_unique<LibIsendOp>(buf, count, dt, dest, tag, comm));
@@ -510,21 +573,34 @@ bool is_tempi_request(MPI_Request r) {
 
 bool progress() {
   bool moved = false;
-  // 1. GPU events, in stream order
+  // 0. launch whatever GPU work is queued (one launch per batch group)
+  if (!pendingPack.empty() || !pendingUnpack.empty()) {
+    flush();
+    moved = true;
+  }
+  // 1. GPU events, in launch order (one stream per device: a later event of
+  //    the same device cannot complete before an earlier one)
   int blockedDevice = -1;
-  for (auto &kv : active) {
-    Op *op = kv.second.get();
-    if (!op->event || op->device == blockedDevice) continue;
-    const int q = tempi_hip_event_query(op->event);
+  for (auto &b : batches) {
+    if (b->complete || b->device == blockedDevice) continue;
+    const int q = tempi_hip_event_query(b->event);
     if (q == 1) {
-      blockedDevice = op->device; // later work of that stream cannot be done
+      blockedDevice = b->device;
       continue;
     }
     gpu::check(q, "event query");
-    put_event(op->event);
-    op->event = nullptr;
-    op->gpu_done();
-    moved = true;
+    put_event(b->event);
+    b->event = nullptr;
+    b->complete = true;
+  }
+  while (!batches.empty() && batches.front()->complete) batches.pop_front();
+  for (auto &kv : active) {
+    Op *op = kv.second.get();
+    if (op->batch && op->batch->complete) {
+      op->batch.reset();
+      op->gpu_done();
+      moved = true;
+    }
   }
   // 2. every outstanding library request in one MPI_Testsome
   pollReqs.clear();
@@ -569,6 +645,8 @@ bool progress() {
       pendingAcks.pop_back();
     }
   }
+  // 3. unpacks of messages that just arrived start now, in one launch
+  if (!pendingUnpack.empty()) flush_list(pendingUnpack, false);
   return moved;
 }
 

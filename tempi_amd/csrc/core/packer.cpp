@@ -33,7 +33,39 @@ int issue(bool pack, char *packed, char *first, int64_t block, const Dim *dims, 
   return 0;
 }
 
+void collect(char *packed, char *first, int64_t block, const Dim *dims, int nd,
+             std::vector<tempi_hip_batch_item> &out) {
+  if (nd <= TEMPI_HIP_MAX_DIMS) {
+    tempi_hip_batch_item it{};
+    it.packed = packed;
+    it.first = first;
+    it.desc.block = block;
+    it.desc.ndims = nd;
+    for (int k = 0; k < nd; ++k) {
+      it.desc.counts[k] = dims[k].count;
+      it.desc.strides[k] = dims[k].stride;
+    }
+    out.push_back(it);
+    return;
+  }
+  int64_t inner = block;
+  for (int k = 1; k < nd; ++k) inner *= dims[k].count;
+  for (int64_t i = 0; i < dims[0].count; ++i)
+    collect(packed + i * inner, first + i * dims[0].stride, block, dims + 1, nd - 1, out);
+}
+
 } // namespace
+
+void Packer::items(void *packed, const void *origin, int64_t count, std::vector<tempi_hip_batch_item> &out) const {
+  if (count <= 0 || sb_.size == 0) return;
+  StridedBlock tmp;
+  tmp.block = sb_.block;
+  if (count > 1) tmp.dims.push_back(Dim{count, sb_.extent});
+  tmp.dims.insert(tmp.dims.end(), sb_.dims.begin(), sb_.dims.end());
+  simplify(tmp);
+  collect(static_cast<char *>(packed), const_cast<char *>(static_cast<const char *>(origin)) + sb_.start, tmp.block,
+          tmp.dims.data(), int(tmp.dims.size()), out);
+}
 
 int Packer::launch(bool pack, char *packed, char *origin, int64_t count, void *stream) const {
   if (count <= 0 || sb_.size == 0) return 0;

@@ -10,7 +10,10 @@
 
 #include "types.hpp"
 
+#include "tempi_hip.h"
+
 #include <cstdint>
+#include <vector>
 
 namespace tempi {
 
@@ -26,6 +29,10 @@ public:
   // addresses). Returns 0 or a tempi_hip status.
   int pack_async(void *packed, const void *origin, int64_t count, void *stream) const;
   int unpack_async(void *origin, const void *packed, int64_t count, void *stream) const;
+
+  // the same work as launch items, appended to `out` (nothing is launched):
+  // the transport batches many messages into one kernel launch
+  void items(void *packed, const void *origin, int64_t count, std::vector<tempi_hip_batch_item> &out) const;
 
   const StridedBlock &desc() const { return sb_; }
 

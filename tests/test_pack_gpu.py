@@ -276,3 +276,73 @@ def test_device_to_pageable_host(mpi, gpu):
         assert np.array_equal(out, to_np(src.view(1000, 40)[:, :12]).reshape(-1))
     finally:
         mpi.Type_free(t)
+
+
+class HipDesc(ctypes.Structure):
+    _fields_ = [("block", ctypes.c_int64), ("ndims", ctypes.c_int32), ("pad_", ctypes.c_int32),
+                ("counts", ctypes.c_int64 * 5), ("strides", ctypes.c_int64 * 5)]
+
+
+class HipItem(ctypes.Structure):
+    _fields_ = [("packed", ctypes.c_void_p), ("first", ctypes.c_void_p), ("desc", HipDesc)]
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_batched_kernel_c_abi(mpi, gpu, seed):
+    """tempi_hip_pack_batch / tempi_hip_unpack_batch (include/tempi_hip.h):
+    up to 100 objects of mixed word width / rank / alignment in one call,
+    against oracle/typemap.c, and the scatter back restores every type map."""
+    torch = _torch()
+    import tempi_amd
+
+    H = ctypes.CDLL(tempi_amd.LIBTEMPI_HIP)
+    H.tempi_hip_pack_batch.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+    H.tempi_hip_unpack_batch.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+    rng = random.Random(seed)
+    n = rng.choice([1, 7, 40, 100])
+    cases = []
+    off = 0
+    for i in range(n):
+        recipe = _random_recipe(rng)
+        count = rng.choice([1, 2])
+        t, temps, basic = typezoo.build(mpi, recipe)
+        d = mpi.describe(t)
+        typezoo.free(mpi, t, temps, basic)
+        dims = ([(count, d["extent"])] if count > 1 else []) + list(zip(d["counts"], d["strides"]))
+        if len(dims) > 5:
+            continue
+        tm = pyoracle.TypeMap(recipe)
+        origin, buflen = tm.geometry(count)
+        shift = rng.choice([0, 0, 1, 4, 8])
+        host = np.random.default_rng(seed * 1000 + i).integers(0, 256, buflen + shift, dtype=np.uint8)
+        off += rng.choice([0, 3])
+        size = tm.size * count
+        cases.append(dict(tm=tm, origin=origin + shift, count=count, host=host, off=off, size=size, d=d,
+                          dims=dims, src=torch.from_numpy(host).to(gpu)))
+        off += size
+    packed = torch.zeros(off + 64, dtype=torch.uint8, device=gpu)
+    items = (HipItem * len(cases))()
+    for k, c in enumerate(cases):
+        it = items[k]
+        it.packed = packed.data_ptr() + c["off"]
+        it.first = c["src"].data_ptr() + c["origin"] + c["d"]["start"]
+        it.desc.block = c["d"]["block"]
+        it.desc.ndims = len(c["dims"])
+        for j, (cn, st) in enumerate(c["dims"]):
+            it.desc.counts[j] = cn
+            it.desc.strides[j] = st
+    torch.cuda.synchronize()
+    assert H.tempi_hip_pack_batch(items, len(cases), None) == 0
+    torch.cuda.synchronize()
+    got = packed.cpu().numpy()
+    for c in cases:
+        assert np.array_equal(got[c["off"]:c["off"] + c["size"]], c["tm"].pack(c["host"], c["origin"], c["count"]))
+    for c in cases:
+        c["src"].zero_()
+    torch.cuda.synchronize()
+    assert H.tempi_hip_unpack_batch(items, len(cases), None) == 0
+    torch.cuda.synchronize()
+    for c in cases:
+        exp = np.zeros_like(c["host"])
+        c["tm"].unpack(c["tm"].pack(c["host"], c["origin"], c["count"]), exp, c["origin"], c["count"])
+        assert np.array_equal(c["src"].cpu().numpy(), exp)
