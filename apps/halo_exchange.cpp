@@ -81,6 +81,10 @@ __global__ void fill_kernel(uint64_t *buf, size_t pitchWords, int ysize, I3 lcr,
   }
 }
 
+// TEMPI's own entry points, when the interposer is linked (weak: the app runs
+// unchanged on a plain MPI)
+extern "C" __attribute__((weak)) void tempi_reset_counters(void);
+
 static double trimean(std::vector<double> v) {
   if (v.empty()) return 0;
   std::sort(v.begin(), v.end());
@@ -212,7 +216,12 @@ int main(int argc, char **argv) {
   std::vector<double> times;
   std::vector<MPI_Request> reqs(dirs.size() * 2 * size_t(nQuants));
   const int warm = 1;
+  double tIsend = 0, tIrecv = 0, tWait = 0;
   for (int it = 0; it < nIters + warm; ++it) {
+    if (it == warm) {
+      if (tempi_reset_counters) tempi_reset_counters();
+      tIsend = tIrecv = tWait = 0;
+    }
     double exch = 0;
     for (int sub = 0; sub < 3; ++sub) {
       MPI_Barrier(MPI_COMM_WORLD);
@@ -222,12 +231,18 @@ int main(int argc, char **argv) {
         for (const Dir &D : dirs)
           MPI_Isend(bufs[size_t(qi)], 1, D.interior, D.nbr, dir_code(D.dx, D.dy, D.dz) + 27 * qi, MPI_COMM_WORLD,
                     &reqs[ri++]);
+      const double t1 = MPI_Wtime();
       for (int qi = 0; qi < nQuants; ++qi)
         for (const Dir &D : dirs)
           MPI_Irecv(bufs[size_t(qi)], 1, D.exterior, D.nbr, dir_code(-D.dx, -D.dy, -D.dz) + 27 * qi,
                     MPI_COMM_WORLD, &reqs[ri++]);
+      const double t2 = MPI_Wtime();
       for (MPI_Request &r : reqs) MPI_Wait(&r, MPI_STATUS_IGNORE);
-      exch += MPI_Wtime() - t0;
+      const double t3 = MPI_Wtime();
+      tIsend += t1 - t0;
+      tIrecv += t2 - t1;
+      tWait += t3 - t2;
+      exch += t3 - t0;
     }
     MPI_Allreduce(MPI_IN_PLACE, &exch, 1, MPI_DOUBLE, MPI_MAX, MPI_COMM_WORLD);
     if (it >= warm) times.push_back(exch);
@@ -268,10 +283,12 @@ int main(int argc, char **argv) {
                 "\"quants\": %d, \"radius\": %d, \"iters\": %d, \"us_per_iter\": %.2f, \"us_min\": %.2f, "
                 "\"payload_bytes_per_iter_per_rank0\": %.0f, \"total_bytes_per_iter\": %.0f, "
                 "\"max_peer_bytes_per_iter\": %.0f, \"aggregate_GBps\": %.2f, \"busiest_link_GBps\": %.2f, "
-                "\"checked\": %s, \"errors\": %lld}\n",
+                "\"checked\": %s, \"errors\": %lld, \"rank0_us_per_iter\": {\"isend\": %.1f, \"irecv\": %.1f, "
+                "\"wait\": %.1f}}\n",
                 size, global.x, global.y, global.z, dims.x, dims.y, dims.z, lcr.x, lcr.y, lcr.z, nQuants, radius,
                 nIters, tIter * 1e6, *std::min_element(times.begin(), times.end()) * 1e6, bytesPerIter, totalBytes,
-                maxLinkAll, totalBytes / tIter / 1e9, maxLinkAll / tIter / 1e9, check ? "true" : "false", errors);
+                maxLinkAll, totalBytes / tIter / 1e9, maxLinkAll / tIter / 1e9, check ? "true" : "false", errors,
+                tIsend / nIters * 1e6, tIrecv / nIters * 1e6, tWait / nIters * 1e6);
     std::fflush(stdout);
   }
   for (Dir &D : dirs) {

@@ -20,6 +20,17 @@ struct Counters {
   // kernel time of synchronous MPI_Pack / MPI_Unpack while profiling is on
   double pack_kernel_ms = 0, unpack_kernel_ms = 0;
   uint64_t pack_timed = 0, unpack_timed = 0;
+  // host time (ns) inside the transport, for TEMPI_PRINT_COUNTERS
+  uint64_t ns_isend = 0, ns_irecv = 0, ns_flush = 0, ns_events = 0, ns_testsome = 0, ns_wait = 0;
+  uint64_t progress_passes = 0, batches = 0, batched_items = 0;
+};
+
+uint64_t now_ns();
+struct ScopedNs {
+  uint64_t &acc;
+  uint64_t t0;
+  explicit ScopedNs(uint64_t &a) : acc(a), t0(now_ns()) {}
+  ~ScopedNs() { acc += now_ns() - t0; }
 };
 
 extern Counters counters;

@@ -54,7 +54,7 @@ TEMPI_EXPORT int MPI_Isend(const void *buf, int count, MPI_Datatype datatype, in
   resolve_next();
   if (p2p::handles(buf, count, datatype, dest))
     return p2p::isend(buf, count, datatype, dest, tag, comm, request);
-  if (state.active) p2p::progress();
+  if (state.active) p2p::progress(false);
   counters.lib_sends++;
   return next.MPI_Isend(buf, count, datatype, dest, tag, comm, request);
 }
@@ -64,7 +64,7 @@ TEMPI_EXPORT int MPI_Irecv(void *buf, int count, MPI_Datatype datatype, int sour
   resolve_next();
   if (p2p::handles(buf, count, datatype, source))
     return p2p::irecv(buf, count, datatype, source, tag, comm, request);
-  if (state.active) p2p::progress();
+  if (state.active) p2p::progress(false);
   counters.lib_recvs++;
   return next.MPI_Irecv(buf, count, datatype, source, tag, comm, request);
 }

@@ -50,7 +50,7 @@ static_assert(sizeof(IpcDesc) == 128, "descriptor size");
 MPI_Comm ctrlComm = MPI_COMM_NULL; // private duplicate of MPI_COMM_WORLD for acks
 int tagUb = 32767;
 bool gpuAwareLibrary = false;
-int64_t ipcMinBytes = 64 * 1024;
+int64_t ipcMinBytes = 4 * 1024;
 
 // acks the sender is waiting for before reusing a device slab
 struct PendingAck {
@@ -203,6 +203,7 @@ constexpr size_t kMaxPending = 512;
 
 void flush_list(std::vector<Pending> &list, bool pack) {
   if (list.empty()) return;
+  ScopedNs timer(counters.ns_flush);
   // group by device (almost always one)
   std::vector<int> devices;
   for (const Pending &p : list)
@@ -215,7 +216,8 @@ void flush_list(std::vector<Pending> &list, bool pack) {
     int cur = 0;
     tempi_hip_get_device(&cur);
     if (cur != dev) tempi_hip_set_device(dev);
-    counters.launches++;
+    counters.batches++;
+    counters.batched_items += items.size();
     gpu::check(pack ? tempi_hip_pack_batch(items.data(), int(items.size()), s)
                     : tempi_hip_unpack_batch(items.data(), int(items.size()), s),
                pack ? "batched pack" : "batched unpack");
@@ -521,6 +523,7 @@ bool handles(const void *buf, int count, MPI_Datatype dt, int peer) {
 int isend(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Comm comm, MPI_Request *req,
           int force) {
   const TypeRecord *rec = type_lookup(dt);
+  ScopedNs timer(counters.ns_isend);
   if (pendingPack.size() >= kMaxPending) flush(); // (no progress(): consecutive Isends share a launch)
   counters.isends++;
   if (!rec->packer) {
@@ -553,7 +556,10 @@ int isend(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Co
 
 int irecv(void *buf, int count, MPI_Datatype dt, int source, int tag, MPI_Comm comm, MPI_Request *req) {
   const TypeRecord *rec = type_lookup(dt);
-  progress();
+  // start queued gathers (a burst of Isends shares this launch); the rest of
+  // progress is left to the waits, so a burst of Irecvs stays O(1) each
+  if (!pendingPack.empty()) flush_list(pendingPack, true);
+  uint64_t t0 = now_ns();
   counters.irecvs++;
   if (!rec->packer) {
     *req = add(std::make_unique<LibIrecvOp>(buf, count, dt, source, tag, comm));
@@ -563,6 +569,7 @@ int irecv(void *buf, int count, MPI_Datatype dt, int source, int tag, MPI_Comm c
   const int64_t bytes = pack_size(count, dt, comm);
   char *origin = static_cast<char *>(p.dptr) - rec->desc.start;
   *req = add(std::make_unique<IrecvOp>(*rec, origin, count, dt, source, tag, comm, p.device, bytes));
+  counters.ns_irecv += now_ns() - t0;
   return MPI_SUCCESS;
 }
 
@@ -571,15 +578,22 @@ bool is_tempi_request(MPI_Request r) {
   return h != 0 && h < kHandleSpace && active.count(h);
 }
 
-bool progress() {
+bool progress(bool full) {
   bool moved = false;
-  // 0. launch whatever GPU work is queued (one launch per batch group)
-  if (!pendingPack.empty() || !pendingUnpack.empty()) {
-    flush();
+  counters.progress_passes++;
+  // 0. launch queued gathers (one launch per batch group); scatters too when
+  //    the caller is about to wait
+  if (!pendingPack.empty()) {
+    flush_list(pendingPack, true);
+    moved = true;
+  }
+  if (full && !pendingUnpack.empty()) {
+    flush_list(pendingUnpack, false);
     moved = true;
   }
   // 1. GPU events, in launch order (one stream per device: a later event of
   //    the same device cannot complete before an earlier one)
+  uint64_t t0 = now_ns();
   int blockedDevice = -1;
   for (auto &b : batches) {
     if (b->complete || b->device == blockedDevice) continue;
@@ -602,6 +616,8 @@ bool progress() {
       moved = true;
     }
   }
+  counters.ns_events += now_ns() - t0;
+  t0 = now_ns();
   // 2. every outstanding library request in one MPI_Testsome
   pollReqs.clear();
   pollOps.clear();
@@ -645,8 +661,11 @@ bool progress() {
       pendingAcks.pop_back();
     }
   }
-  // 3. unpacks of messages that just arrived start now, in one launch
-  if (!pendingUnpack.empty()) flush_list(pendingUnpack, false);
+  counters.ns_testsome += now_ns() - t0;
+  // 3. unpacks of messages that arrived: launched together when the caller
+  //    is about to wait for them (light passes from MPI_Isend / MPI_Irecv
+  //    only queue them, so a burst of receives shares one launch)
+  if (!pendingUnpack.empty() && (full || pendingUnpack.size() >= kMaxPending)) flush_list(pendingUnpack, false);
   return moved;
 }
 
@@ -656,6 +675,7 @@ int wait(MPI_Request *req, MPI_Status *status) {
   const uint32_t h = uint32_t(*req);
   auto it = active.find(h);
   if (it == active.end()) return next.MPI_Wait(req, status);
+  ScopedNs timer(counters.ns_wait);
   while (!it->second->done) progress();
   it->second->status(status);
   active.erase(it);

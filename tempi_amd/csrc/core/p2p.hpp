@@ -22,7 +22,7 @@
 //            the receiver maps the sender's slab and its unpack kernel reads
 //            the packed bytes over xGMI, then acknowledges so the sender can
 //            reuse the slab
-//   AUTO     IPC for co-located peers at >= TEMPI_IPC_MIN_BYTES (64 KiB),
+//   AUTO     IPC for co-located peers at >= TEMPI_IPC_MIN_BYTES (4 KiB),
 //            ONESHOT otherwise (with no perf.json the reference would stop
 //            here with LOG_FATAL: SURVEY F10)
 // Receives are adaptive: a TEMPI device receive lands in pinned host memory
@@ -49,8 +49,10 @@ int isend(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Co
 int irecv(void *buf, int count, MPI_Datatype dt, int source, int tag, MPI_Comm comm, MPI_Request *req);
 
 bool is_tempi_request(MPI_Request r);
-// drive every TEMPI operation one step; returns true if anything moved
-bool progress();
+// drive every TEMPI operation one step; returns true if anything moved.
+// full = false (from MPI_Isend / MPI_Irecv) leaves arrived messages' unpacks
+// queued so that a burst shares one launch; waits use full = true
+bool progress(bool full = true);
 bool busy(); // active operations or unacknowledged IPC slabs exist
 
 // complete a TEMPI request (blocking); fills status, sets *req to NULL
