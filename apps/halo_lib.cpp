@@ -15,8 +15,11 @@
 // by list position, which guarantees only equal sizes. (2) --check verifies
 // every halo byte against the value the owning rank wrote.
 //
-// usage: halo_exchange ITERS X [Y Z] [--quants N] [--radius R] [--check]
-// prints one JSON line (rank 0)
+// Library form: tempi_bench_halo() (libtempi_apps.so), called by bench.py
+// inside the driver's torch.distributed launch; the CLI wrapper is
+// apps/halo_exchange_main.cpp:
+//   halo_exchange ITERS X [Y Z] [--quants N] [--radius R] [--check]
+// Result: one JSON object (rank 0).
 #include <hip/hip_runtime.h>
 #include <mpi.h>
 
@@ -96,37 +99,18 @@ static double trimean(std::vector<double> v) {
   return (pct(0.25) + 2 * pct(0.5) + pct(0.75)) / 4;
 }
 
-int main(int argc, char **argv) {
-  MPI_Init(&argc, &argv);
+extern "C" __attribute__((visibility("default"))) int
+tempi_bench_halo(int nIters, int gx, int gy, int gz, int nQuants, int radius, int check, int setDevice, char *json,
+                 int jsonCap) {
   int rank, size;
   MPI_Comm_rank(MPI_COMM_WORLD, &rank);
   MPI_Comm_size(MPI_COMM_WORLD, &size);
-
-  int nIters = 5, nQuants = 8, radius = 3;
-  bool check = false;
-  std::vector<int> pos;
-  for (int i = 1; i < argc; ++i) {
-    std::string a = argv[i];
-    if (a == "--check")
-      check = true;
-    else if (a == "--quants")
-      nQuants = std::atoi(argv[++i]);
-    else if (a == "--radius")
-      radius = std::atoi(argv[++i]);
-    else
-      pos.push_back(std::atoi(argv[i]));
-  }
-  if (pos.size() != 2 && pos.size() != 4) {
-    if (!rank) std::fprintf(stderr, "usage: %s ITERS X [Y Z] [--quants N] [--radius R] [--check]\n", argv[0]);
-    MPI_Abort(MPI_COMM_WORLD, 1);
-  }
-  nIters = pos[0];
-  I3 global{pos[1], pos.size() == 4 ? pos[2] : pos[1], pos.size() == 4 ? pos[3] : pos[1]};
+  I3 global{gx, gy, gz};
 
   // one GPU per rank on the node (ranks beyond the GPU count share)
   int ndev = 0;
   HIPCHECK(hipGetDeviceCount(&ndev));
-  {
+  if (setDevice) {
     MPI_Comm node;
     MPI_Comm_split_type(MPI_COMM_WORLD, MPI_COMM_TYPE_SHARED, rank, MPI_INFO_NULL, &node);
     int lr;
@@ -278,8 +262,8 @@ int main(int argc, char **argv) {
   double totalBytes = bytesPerIter;
   MPI_Allreduce(MPI_IN_PLACE, &totalBytes, 1, MPI_DOUBLE, MPI_SUM, MPI_COMM_WORLD);
   const double tIter = trimean(times);
-  if (rank == 0) {
-    std::printf("{\"ranks\": %d, \"global\": [%d, %d, %d], \"dims\": [%d, %d, %d], \"lcr\": [%d, %d, %d], "
+  if (rank == 0 && json && jsonCap > 0) {
+    std::snprintf(json, size_t(jsonCap), "{\"ranks\": %d, \"global\": [%d, %d, %d], \"dims\": [%d, %d, %d], \"lcr\": [%d, %d, %d], "
                 "\"quants\": %d, \"radius\": %d, \"iters\": %d, \"us_per_iter\": %.2f, \"us_min\": %.2f, "
                 "\"payload_bytes_per_iter_per_rank0\": %.0f, \"total_bytes_per_iter\": %.0f, "
                 "\"max_peer_bytes_per_iter\": %.0f, \"aggregate_GBps\": %.2f, \"busiest_link_GBps\": %.2f, "
@@ -289,13 +273,11 @@ int main(int argc, char **argv) {
                 nIters, tIter * 1e6, *std::min_element(times.begin(), times.end()) * 1e6, bytesPerIter, totalBytes,
                 maxLinkAll, totalBytes / tIter / 1e9, maxLinkAll / tIter / 1e9, check ? "true" : "false", errors,
                 tIsend / nIters * 1e6, tIrecv / nIters * 1e6, tWait / nIters * 1e6);
-    std::fflush(stdout);
   }
   for (Dir &D : dirs) {
     MPI_Type_free(&D.interior);
     MPI_Type_free(&D.exterior);
   }
   for (char *b : bufs) HIPCHECK(hipFree(b));
-  MPI_Finalize();
   return errors ? 3 : 0;
 }

@@ -14,6 +14,12 @@ one pack or unpack of P payload bytes moves 2P (read P + write P; SURVEY
 8(d)). N > 1 (torchrun): every rank packs its own object on its own GPU, no
 collective on the data path (weak scaling, replicas).
 
+The same line carries "halo": the 3D halo exchange of config 4 (512^3 grid,
+8 quantities of 8 B, radius 3, 26 neighbours, periodic, 3 substeps per
+iteration) run through MPI_Isend/MPI_Irecv/MPI_Wait on the same ranks
+(strong scaling of the fixed grid), with its xGMI roofline. Under torchrun
+the ranks are wired into one MPI job by tempi_amd.pmi.
+
 Other modes (not the driver's line):
   --sweep FILE   the config-2 sweep (block 1 B - 4 KiB, 2D and 3D, 1 MiB -
                  1 GiB), one JSON record per point, written to FILE
@@ -42,8 +48,11 @@ def parse():
     p.add_argument("--block", type=int, default=512)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=8.0)
-    p.add_argument("--traffic", action="store_true",
-                   help="run rocprofv3 FETCH_SIZE / WRITE_SIZE passes (child processes) for roofline.traffic")
+    p.add_argument("--no-traffic", action="store_true",
+                   help="skip the rocprofv3 FETCH_SIZE / WRITE_SIZE passes (child processes) for roofline.traffic")
+    p.add_argument("--no-halo", action="store_true")
+    p.add_argument("--halo-grid", type=int, default=512)
+    p.add_argument("--halo-iters", type=int, default=10)
     p.add_argument("--sweep", default=None, help="run the config-2 sweep and write JSON records here")
     p.add_argument("--inner", action="store_true", help=argparse.SUPPRESS)  # child for --traffic
     return p.parse_args()
@@ -54,12 +63,16 @@ def dist_setup(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     pg = None
+    keep = None
     if world > 1:
         import torch.distributed as dist
 
+        from tempi_amd import pmi
+
         dist.init_process_group("gloo", rank=rank, world_size=world)
         pg = dist
-    return rank, world, local, pg
+        keep = pmi.wire_torch_ranks(rank, world, dist)  # one MPI job over the torch ranks
+    return rank, world, local, pg, keep
 
 
 def barrier(pg):
@@ -152,10 +165,10 @@ def run_traffic_passes(args, kernel_substr):
     for counter in ("FETCH_SIZE", "WRITE_SIZE"):
         d = tempfile.mkdtemp(prefix="tempi_pmc_", dir=os.path.join(ROOT, "gpurun_out") if os.path.isdir(
             os.path.join(ROOT, "gpurun_out")) else None)
-        cmd = ["timeout", "-s", "KILL", "120", "rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", d,
+        cmd = ["timeout", "-s", "KILL", "150", "rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", d,
                "-o", "pmc", "--", sys.executable, os.path.abspath(__file__), "--inner", "--steps", "3",
                "--warmup", "1", "--rows", str(args.rows), "--pitch", str(args.pitch), "--block", str(args.block),
-               "--no-cpu-baseline"]
+               "--no-cpu-baseline", "--no-halo", "--no-traffic"]
         r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
         if r.returncode != 0:
             return None
@@ -256,6 +269,45 @@ def headline(args, mpi, torch, rank, world, pg, dev):
     return rec
 
 
+XGMI_LINK_GBS = 153.0  # per direction, per link
+
+
+def halo(args, mpi, world):
+    """Config 4 through libtempi_apps.so's tempi_bench_halo (every rank)."""
+    import ctypes
+
+    import tempi_amd
+
+    L = ctypes.CDLL(os.path.join(tempi_amd.LIBDIR, "libtempi_apps.so"), mode=ctypes.RTLD_GLOBAL)
+    L.tempi_bench_halo.argtypes = [ctypes.c_int] * 8 + [ctypes.c_char_p, ctypes.c_int]
+    buf = ctypes.create_string_buffer(4096)
+    g = args.halo_grid
+    rc = L.tempi_bench_halo(args.halo_iters, g, g, g, 8, 3, 0, 0, buf, 4096)
+    if rc != 0:
+        raise SystemExit(f"halo exchange failed rc={rc}")
+    if not buf.value:
+        return None
+    r = json.loads(buf.value.decode())
+    t = r["us_per_iter"] * 1e-6
+    out = {
+        "workload": (f"{g}^3 grid, 8 quantities x 8 B, radius 3, 26 neighbours, periodic, 3 substeps/iter, "
+                     f"{world} rank(s) {r['dims']} (recursive bisection), MPI_Isend/Irecv/Wait of subarray types"),
+        "us_per_iter": r["us_per_iter"],
+        "us_min": r["us_min"],
+        "bytes_per_iter_all_ranks": r["total_bytes_per_iter"],
+        "busiest_peer_bytes_per_iter": r["max_peer_bytes_per_iter"],
+        "rank0_phase_us": r.get("rank0_us_per_iter"),
+    }
+    if world > 1:
+        # xGMI: the busiest point-to-point link carries max_peer bytes per iteration
+        out["xgmi"] = {"busiest_link_GBps": round(r["busiest_link_GBps"], 2), "link_peak_GBps": XGMI_LINK_GBS,
+                       "frac": round(r["busiest_link_GBps"] / XGMI_LINK_GBS, 4),
+                       "lower_bound_us": round(r["max_peer_bytes_per_iter"] / (XGMI_LINK_GBS * 1e9) * 1e6, 1)}
+    # HBM: pack + unpack of every byte = 4 x payload per iteration per rank
+    out["hbm_equiv_GBps_per_rank"] = round(4 * r["total_bytes_per_iter"] / world / t / 1e9, 1)
+    return out
+
+
 def sweep(args, mpi, torch, dev, path):
     """Config-2 sweep: 2D subarray and 3D subarray, block 1 B - 4 KiB."""
     recs = []
@@ -318,12 +370,12 @@ def sweep(args, mpi, torch, dev, path):
 
 def main():
     args = parse()
-    rank, world, local, pg = dist_setup(args)
+    rank, world, local, pg, keep = dist_setup(args)
     import torch
 
     import tempi_amd
 
-    dev = torch.device("cuda", local)
+    dev = torch.device("cuda", local % max(torch.cuda.device_count(), 1))  # ranks may share a GPU when testing
     torch.cuda.set_device(dev)
     mpi = tempi_amd.get_mpi()
     mpi.Init()
@@ -335,13 +387,21 @@ def main():
         rec = headline(args, mpi, torch, rank, world, pg, dev)
         if args.inner:
             return
+        torch.cuda.empty_cache()
+        if not args.no_halo:
+            h = halo(args, mpi, world)
+            if rank == 0:
+                rec["halo"] = h
         if rank == 0 and world == 1:
-            if args.traffic:
+            if not args.no_traffic:
                 tr = run_traffic_passes(args, "pack_kernel")
                 if tr:
                     rec["roofline"]["traffic"] = int(tr[0] + tr[1])
                     rec["roofline"]["traffic_read"] = int(tr[0])
                     rec["roofline"]["traffic_write"] = int(tr[1])
+                    rec["roofline"]["traffic_source"] = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, "
+                                                         "per launch of pack_kernel/unpack_kernel, FETCH_SIZE x2 "
+                                                         "(gfx950)")
             if not args.no_cpu_baseline:
                 rec["cpu_baseline"] = cpu_baseline(mpi, args.pitch, args.block, args.cpu_seconds)
         if rank == 0:

@@ -56,8 +56,12 @@ int64_t ipcMinBytes = 4 * 1024;
 struct PendingAck {
   MPI_Request req;
   Slab *slab;
+  int peer;     // world rank of the receiver
+  int tag;      // ack tag
+  int64_t bytes;
+  int code;     // received ack payload
 };
-std::vector<PendingAck> pendingAcks;
+std::vector<std::unique_ptr<PendingAck>> pendingAcks; // stable addresses: Irecv targets
 
 // peer slabs mapped into this process: (world rank, slab id) -> base
 std::map<std::pair<int, uint64_t>, void *> ipcOpen;
@@ -124,21 +128,44 @@ Method choose(int64_t bytes, bool colocated) {
   }
 }
 
+// peers whose memory could not be mapped: no more IPC to or from them
+std::vector<char> ipcBroken;
+
+bool ipc_broken(int world) { return world >= 0 && size_t(world) < ipcBroken.size() && ipcBroken[size_t(world)]; }
+
+void mark_ipc_broken(int world) {
+  if (world < 0) return;
+  if (ipcBroken.size() <= size_t(world)) ipcBroken.resize(size_t(world) + 1, 0);
+  if (!ipcBroken[size_t(world)]) LOG_WARN("IPC with rank " << world << " unavailable; using host-staged transfers");
+  ipcBroken[size_t(world)] = 1;
+}
+
+// the sender's slab mapped into this process, or nullptr when it cannot be
 void *peer_pointer(const IpcDesc &d) {
   if (d.senderPid == int32_t(getpid())) return reinterpret_cast<void *>(d.rawPtr);
   auto key = std::make_pair(int(d.senderWorld), d.slabId);
   auto it = ipcOpen.find(key);
   if (it != ipcOpen.end()) return it->second;
   void *p = nullptr;
-  gpu::check(tempi_hip_ipc_open_handle(&p, d.handle), "ipc open handle");
+  // fault injection (tests): TEMPI_FAULT_IPC_OPEN makes every mapping fail
+  static const bool injectFault = std::getenv("TEMPI_FAULT_IPC_OPEN") != nullptr;
+  const int e = injectFault ? 1 : tempi_hip_ipc_open_handle(&p, d.handle);
+  if (e != 0) {
+    LOG_WARN("cannot map rank " << d.senderWorld << "'s slab: " << tempi_hip_error_string(e));
+    mark_ipc_broken(d.senderWorld);
+    return nullptr;
+  }
   ipcOpen[key] = p;
   return p;
 }
 
-void send_ack(const IpcDesc &d) {
-  static char dummy = 0;
+// ack payload: 0 = pulled, release the slab; 1 = could not map it, send the
+// bytes through the host on (ctrlComm, ackTag)
+int ackCodes[2] = {0, 1};
+
+void send_ack(const IpcDesc &d, int code = 0) {
   MPI_Request r;
-  next.MPI_Isend(&dummy, 0, MPI_BYTE, d.senderWorld, d.ackTag, ctrlComm, &r);
+  next.MPI_Isend(&ackCodes[code], 1, MPI_INT, d.senderWorld, d.ackTag, ctrlComm, &r);
   MPI_Request_free(&r);
 }
 
@@ -300,10 +327,9 @@ struct IsendOp : Op {
       std::memcpy(desc.handle, slab_ipc_handle(dslab), sizeof desc.handle);
       // the slab is reused once the receiver acknowledges (private comm)
       const int peer = topology::world_rank(comm, dest);
-      PendingAck pa{MPI_REQUEST_NULL, dslab};
-      static char sink;
-      next.MPI_Irecv(&sink, 0, MPI_BYTE, peer, desc.ackTag, ctrlComm, &pa.req);
-      pendingAcks.push_back(pa);
+      pendingAcks.push_back(std::unique_ptr<PendingAck>(new PendingAck{MPI_REQUEST_NULL, dslab, peer, desc.ackTag, bytes, -1}));
+      PendingAck &pa = *pendingAcks.back();
+      next.MPI_Irecv(&pa.code, 1, MPI_INT, peer, desc.ackTag, ctrlComm, &pa.req);
       dslab = nullptr;
       next.MPI_Isend(&desc, int(sizeof desc), MPI_PACKED, dest, tag, comm, &lib);
       break;
@@ -339,6 +365,7 @@ struct IrecvOp : Op {
   MPI_Status libStatus{};
   IpcDesc desc{};
   bool ipc = false;
+  bool fallback = false; // waiting for the bytes the peer re-sends through the host
   int64_t elems = 0;
 
   IrecvOp(const TypeRecord &rec, char *o, int c, MPI_Datatype d, int source, int tag, MPI_Comm cm, int dev,
@@ -351,6 +378,15 @@ struct IrecvOp : Op {
   }
 
   void lib_done(const MPI_Status &st) override { // arrived: queue its unpack
+    if (fallback) { // the host copy of an IPC message we could not map
+      Pending p;
+      p.op = this;
+      elems = packer.desc().size ? desc.bytes / packer.desc().size : 0;
+      packer.items(hslab->dev, origin, elems, p.items);
+      queued = true;
+      pendingUnpack.push_back(std::move(p));
+      return;
+    }
     libStatus = st;
     int n = 0;
     MPI_Get_count(&libStatus, MPI_PACKED, &n);
@@ -363,7 +399,15 @@ struct IrecvOp : Op {
       ipc = true;
       desc = d;
       if (d.bytes > bytes) LOG_FATAL("message truncated: " << d.bytes << " B into " << bytes);
-      const char *peer = static_cast<const char *>(peer_pointer(d)) + d.offset;
+      void *base = peer_pointer(d);
+      if (!base) { // cannot map the sender's slab: ask for the bytes via the host
+        ipc = false;
+        fallback = true;
+        next.MPI_Irecv(hslab->host, int(d.bytes), MPI_PACKED, d.senderWorld, d.ackTag, ctrlComm, &lib);
+        send_ack(d, 1);
+        return;
+      }
+      const char *peer = static_cast<const char *>(base) + d.offset;
       elems = size ? d.bytes / size : 0;
       packer.items(const_cast<char *>(peer), origin, elems, p.items);
     } else {
@@ -499,7 +543,7 @@ void finalize() {
     progress();
     if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(30)) {
       LOG_WARN(pendingAcks.size() << " IPC slab(s) never acknowledged; abandoning");
-      for (auto &pa : pendingAcks) MPI_Cancel(&pa.req);
+      for (auto &pa : pendingAcks) MPI_Cancel(&pa->req);
       pendingAcks.clear();
     }
   }
@@ -536,7 +580,7 @@ int isend(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Co
   modelBlock = std::min<int64_t>(std::max<int64_t>(1, rec->desc.block), 512);
   Method m = choose(bytes, colocated);
   if (force >= 0) m = Method(force);
-  if (m == Method::IPC && !colocated) m = Method::ONESHOT;
+  if (m == Method::IPC && (!colocated || ipc_broken(topology::world_rank(comm, dest)))) m = Method::ONESHOT;
   if (m == Method::DEVICE && !gpuAwareLibrary) m = colocated ? Method::IPC : Method::STAGED;
   switch (m) {
   case Method::ONESHOT: counters.send_oneshot++; break;
@@ -631,7 +675,7 @@ bool progress(bool full) {
     }
   }
   for (size_t i = 0; i < pendingAcks.size(); ++i) {
-    pollReqs.push_back(pendingAcks[i].req);
+    pollReqs.push_back(pendingAcks[i]->req);
     pollOps.push_back(nullptr);
     pollAck.push_back(i);
   }
@@ -656,8 +700,17 @@ bool progress(bool full) {
     // release acknowledged slabs (highest index first keeps indices valid)
     std::sort(ackedSlots.rbegin(), ackedSlots.rend());
     for (size_t a : ackedSlots) {
-      device_pool().put(pendingAcks[a].slab);
-      pendingAcks[a] = pendingAcks.back();
+      PendingAck &pa = *pendingAcks[a];
+      pa.req = MPI_REQUEST_NULL;
+      if (pa.code == 1) { // the receiver could not map the slab: send the bytes through the host
+        mark_ipc_broken(pa.peer);
+        Slab *h = pinned_pool().get(size_t(pa.bytes), pa.slab->device);
+        gpu::check(tempi_hip_memcpy(h->host, pa.slab->dev, size_t(pa.bytes)), "ipc fallback D2H");
+        next.MPI_Send(h->host, int(pa.bytes), MPI_PACKED, pa.peer, pa.tag, ctrlComm); // receive already posted
+        pinned_pool().put(h);
+      }
+      device_pool().put(pa.slab);
+      pendingAcks[a] = std::move(pendingAcks.back());
       pendingAcks.pop_back();
     }
   }
@@ -723,10 +776,22 @@ int recv_host_ipc_aware(void *buf, int count, MPI_Datatype dt, int source, int t
   const char *src = reinterpret_cast<const char *>(&d);
   if (d.magic[0] == kMagic0 && d.magic[1] == kMagic1) { // pull over IPC
     packed.resize(size_t(std::max<int64_t>(d.bytes, 1)));
-    gpu::check(tempi_hip_memcpy(packed.data(), static_cast<const char *>(peer_pointer(d)) + d.offset,
-                                size_t(d.bytes)),
-               "ipc pull");
-    send_ack(d);
+    void *base = peer_pointer(d);
+    if (base) {
+      gpu::check(tempi_hip_memcpy(packed.data(), static_cast<const char *>(base) + d.offset, size_t(d.bytes)),
+                 "ipc pull");
+      send_ack(d);
+    } else {
+      MPI_Request r;
+      next.MPI_Irecv(packed.data(), int(d.bytes), MPI_PACKED, d.senderWorld, d.ackTag, ctrlComm, &r);
+      send_ack(d, 1);
+      while (true) {
+        int flag = 0;
+        next.MPI_Test(&r, &flag, MPI_STATUS_IGNORE);
+        if (flag) break;
+        progress();
+      }
+    }
     src = packed.data();
     nbytes = int(d.bytes);
   }

@@ -16,3 +16,27 @@ def test_two_ranks_host_buffers():
 def test_alltoallv_host(ranks, nnz):
     rc, out = mpi_launch.run(ranks, mpi_launch.py("alltoallv.py", "--nnz", str(nnz), "--scale", "100"), timeout=180)
     assert rc == 0 and "RESULT errors=0" in out, out[-3000:]
+
+
+def test_mpi_under_torchrun():
+    """bench.py's multi-GPU launch is torch.distributed.run, not mpiexec: the
+    ranks are wired into one MPI job by tempi_amd.pmi (PMI-1 server)."""
+    import os
+    import socket
+    import subprocess
+    import sys
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.join(mpi_launch.ROOT, "tests", "mpi_progs", "torchrun_mpi.py")]
+    env = dict(os.environ)
+    for k in list(env):
+        if k.startswith("PMI_"):
+            env.pop(k)
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=240, env=env,
+                       start_new_session=True)
+    assert r.returncode == 0 and r.stdout.count("RESULT ok") == 2, r.stdout[-3000:]

@@ -18,6 +18,8 @@ METHODS = {
     "STAGED": {"TEMPI_DATATYPE_STAGED": "1"},
     "IPC": {"TEMPI_DATATYPE_IPC": "1"},
     "DEVICE": {"TEMPI_DATATYPE_DEVICE": "1"},  # no GPU-aware MPI here: IPC intra-node
+    # IPC whose peer mapping fails (fault injection): NACK -> host re-send
+    "IPC_FAULT": {"TEMPI_DATATYPE_IPC": "1", "TEMPI_FAULT_IPC_OPEN": "1"},
 }
 
 
@@ -44,10 +46,12 @@ def test_pingpong_nd(gpu, method, total, block):
     assert rc == 0 and r["errors"] == 0, out[-3000:]
 
 
-@pytest.mark.parametrize("ranks,grid", [(1, "48"), (2, "48"), (4, "40"), (3, "30"), (1, "128")])
-def test_halo_exchange_content(gpu, ranks, grid):
+@pytest.mark.parametrize("ranks,grid,env", [(1, "48", {}), (2, "48", {}), (4, "40", {}), (3, "30", {}),
+                                           (1, "128", {}), (2, "40", {"TEMPI_FAULT_IPC_OPEN": "1"}),
+                                           (4, "32", {"TEMPI_DATATYPE_ONESHOT": "1"})])
+def test_halo_exchange_content(gpu, ranks, grid, env):
     rc, out = mpi_launch.run(ranks, [os.path.join(LIB, "halo_exchange"), "2", grid, "--quants", "2", "--check"],
-                             timeout=300)
+                             env=env, timeout=300)
     r = _json_line(out)
     assert rc == 0 and r["checked"] and r["errors"] == 0, out[-3000:]
 
