@@ -15,10 +15,15 @@
 // by list position, which guarantees only equal sizes. (2) --check verifies
 // every halo byte against the value the owning rank wrote.
 //
+// --neighbor: the same exchange as one MPI_Neighbor_alltoallw per quantity
+// on an MPI_Dist_graph_create_adjacent communicator (26 out-edges toward each
+// direction d, 26 in-edges from the neighbour at -d; repeated edges between
+// the same pair match in edge order, which this ordering makes exact).
+//
 // Library form: tempi_bench_halo() (libtempi_apps.so), called by bench.py
 // inside the driver's torch.distributed launch; the CLI wrapper is
 // apps/halo_exchange_main.cpp:
-//   halo_exchange ITERS X [Y Z] [--quants N] [--radius R] [--check]
+//   halo_exchange ITERS X [Y Z] [--quants N] [--radius R] [--check] [--neighbor]
 // Result: one JSON object (rank 0).
 #include <hip/hip_runtime.h>
 #include <mpi.h>
@@ -100,8 +105,8 @@ static double trimean(std::vector<double> v) {
 }
 
 extern "C" __attribute__((visibility("default"))) int
-tempi_bench_halo(int nIters, int gx, int gy, int gz, int nQuants, int radius, int check, int setDevice, char *json,
-                 int jsonCap) {
+tempi_bench_halo(int nIters, int gx, int gy, int gz, int nQuants, int radius, int check, int neighbor,
+                 int setDevice, char *json, int jsonCap) {
   int rank, size;
   MPI_Comm_rank(MPI_COMM_WORLD, &rank);
   MPI_Comm_size(MPI_COMM_WORLD, &size);
@@ -197,6 +202,26 @@ tempi_bench_halo(int nIters, int gx, int gy, int gz, int nQuants, int radius, in
   }
   const double maxLink = *std::max_element(peerBytes.begin(), peerBytes.end());
 
+  // neighbourhood form: out-edge i toward dirs[i], in-edge i from the
+  // neighbour at -dirs[i] (whose send toward dirs[i] fills exterior(-dirs[i]))
+  MPI_Comm graph = MPI_COMM_NULL;
+  std::vector<int> nbrIn, nbrOut, ncount(dirs.size(), 1);
+  std::vector<MPI_Aint> ndispl(dirs.size(), 0);
+  std::vector<MPI_Datatype> nsend, nrecv;
+  if (neighbor) {
+    for (const Dir &D : dirs) {
+      nbrOut.push_back(D.nbr);
+      nsend.push_back(D.interior);
+      for (const Dir &E : dirs)
+        if (E.dx == -D.dx && E.dy == -D.dy && E.dz == -D.dz) {
+          nbrIn.push_back(E.nbr);
+          nrecv.push_back(E.exterior);
+        }
+    }
+    MPI_Dist_graph_create_adjacent(MPI_COMM_WORLD, int(nbrIn.size()), nbrIn.data(), MPI_UNWEIGHTED,
+                                   int(nbrOut.size()), nbrOut.data(), MPI_UNWEIGHTED, MPI_INFO_NULL, 0, &graph);
+  }
+
   std::vector<double> times;
   std::vector<MPI_Request> reqs(dirs.size() * 2 * size_t(nQuants));
   const int warm = 1;
@@ -210,6 +235,15 @@ tempi_bench_halo(int nIters, int gx, int gy, int gz, int nQuants, int radius, in
     for (int sub = 0; sub < 3; ++sub) {
       MPI_Barrier(MPI_COMM_WORLD);
       const double t0 = MPI_Wtime();
+      if (neighbor) {
+        for (int qi = 0; qi < nQuants; ++qi)
+          MPI_Neighbor_alltoallw(bufs[size_t(qi)], ncount.data(), ndispl.data(), nsend.data(), bufs[size_t(qi)],
+                                 ncount.data(), ndispl.data(), nrecv.data(), graph);
+        const double t3 = MPI_Wtime();
+        tWait += t3 - t0;
+        exch += t3 - t0;
+        continue;
+      }
       size_t ri = 0;
       for (int qi = 0; qi < nQuants; ++qi)
         for (const Dir &D : dirs)
@@ -267,13 +301,15 @@ tempi_bench_halo(int nIters, int gx, int gy, int gz, int nQuants, int radius, in
                 "\"quants\": %d, \"radius\": %d, \"iters\": %d, \"us_per_iter\": %.2f, \"us_min\": %.2f, "
                 "\"payload_bytes_per_iter_per_rank0\": %.0f, \"total_bytes_per_iter\": %.0f, "
                 "\"max_peer_bytes_per_iter\": %.0f, \"aggregate_GBps\": %.2f, \"busiest_link_GBps\": %.2f, "
-                "\"checked\": %s, \"errors\": %lld, \"rank0_us_per_iter\": {\"isend\": %.1f, \"irecv\": %.1f, "
-                "\"wait\": %.1f}}\n",
+                "\"checked\": %s, \"errors\": %lld, \"api\": \"%s\", \"rank0_us_per_iter\": {\"isend\": %.1f, "
+                "\"irecv\": %.1f, \"wait\": %.1f}}\n",
                 size, global.x, global.y, global.z, dims.x, dims.y, dims.z, lcr.x, lcr.y, lcr.z, nQuants, radius,
                 nIters, tIter * 1e6, *std::min_element(times.begin(), times.end()) * 1e6, bytesPerIter, totalBytes,
                 maxLinkAll, totalBytes / tIter / 1e9, maxLinkAll / tIter / 1e9, check ? "true" : "false", errors,
+                neighbor ? "MPI_Neighbor_alltoallw" : "MPI_Isend/MPI_Irecv/MPI_Wait",
                 tIsend / nIters * 1e6, tIrecv / nIters * 1e6, tWait / nIters * 1e6);
   }
+  if (graph != MPI_COMM_NULL) MPI_Comm_free(&graph);
   for (Dir &D : dirs) {
     MPI_Type_free(&D.interior);
     MPI_Type_free(&D.exterior);

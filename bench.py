@@ -279,10 +279,10 @@ def halo(args, mpi, world):
     import tempi_amd
 
     L = ctypes.CDLL(os.path.join(tempi_amd.LIBDIR, "libtempi_apps.so"), mode=ctypes.RTLD_GLOBAL)
-    L.tempi_bench_halo.argtypes = [ctypes.c_int] * 8 + [ctypes.c_char_p, ctypes.c_int]
+    L.tempi_bench_halo.argtypes = [ctypes.c_int] * 9 + [ctypes.c_char_p, ctypes.c_int]
     buf = ctypes.create_string_buffer(4096)
     g = args.halo_grid
-    rc = L.tempi_bench_halo(args.halo_iters, g, g, g, 8, 3, 0, 0, buf, 4096)
+    rc = L.tempi_bench_halo(args.halo_iters, g, g, g, 8, 3, 0, 0, 0, buf, 4096)
     if rc != 0:
         raise SystemExit(f"halo exchange failed rc={rc}")
     if not buf.value:

@@ -38,6 +38,8 @@ typedef struct tempi_counters_t {
   uint64_t sends, recvs, isends, irecvs;
   uint64_t send_device, send_oneshot, send_staged, send_ipc;
   uint64_t lib_sends, lib_recvs;
+  uint64_t send_direct, direct_fallbacks; /* sends to the same process */
+  uint64_t neighbor_colls; /* MPI_Neighbor_alltoall{v,w} taken by TEMPI */
 } tempi_counters_t;
 void tempi_get_counters(tempi_counters_t *out);
 void tempi_reset_counters(void);

@@ -66,6 +66,24 @@ typedef struct tempi_hip_batch_item {
 int tempi_hip_pack_batch(const tempi_hip_batch_item *items, int n, void *stream);
 int tempi_hip_unpack_batch(const tempi_hip_batch_item *items, int n, void *stream);
 
+/* Strided -> strided copy with no packed intermediate: the object at
+   dst_first (shape dst) <- the object at src_first (shape src), in type-map
+   order; both shapes must describe the same number of bytes. This is what a
+   message between two buffers of one process (a send to self) reduces to.
+   tempi_hip_copy_supported() says whether one item can run as a copy kernel
+   (at most 3 strided dimensions a side after normalisation, < 2 GiB);
+   tempi_hip_copy_batch() fails with hipErrorInvalidValue on an item that
+   cannot, so callers route those through pack + unpack. */
+typedef struct tempi_hip_copy_item {
+  void *dst_first;
+  const void *src_first;
+  tempi_hip_desc dst;
+  tempi_hip_desc src;
+} tempi_hip_copy_item;
+int tempi_hip_copy_supported(void *dst_first, const void *src_first,
+                             const tempi_hip_desc *dst, const tempi_hip_desc *src);
+int tempi_hip_copy_batch(const tempi_hip_copy_item *items, int n, void *stream);
+
 /* number of packed bytes a descriptor describes */
 int64_t tempi_hip_desc_bytes(const tempi_hip_desc *d);
 /* the word width (1,2,4,8,16) the kernels will use for these pointers */

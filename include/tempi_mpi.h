@@ -28,12 +28,17 @@
  *   MPI_Waitall      (not interposed: F8)            progress TEMPI requests
  *   MPI_Test         (not interposed: F8)            progress TEMPI requests
  *   MPI_Alltoallv    src/alltoallv.cpp:14-68         device-buffer alltoallv
- *
- * Not exported (out of scope): MPI_Neighbor_alltoallv (a
- * pure passthrough in the reference), MPI_Neighbor_alltoallw,
- * MPI_Dist_graph_create_adjacent / _neighbors, MPI_Comm_rank / _free (rank
- * placement, a no-op on one node: SURVEY F12). Calls to them reach the MPI
- * library unchanged.
+ *   MPI_Neighbor_alltoallw  src/neighbor_alltoallw.cpp:11-18 (-> internal/
+ *                    neighbor_alltoallw.cpp:19-77)   per-edge Isend/Irecv when
+ *                                                    any block is on the GPU
+ *   MPI_Neighbor_alltoallv  src/neighbor_alltoallv.cpp:12-24 (passthrough
+ *                    there)                          same route as alltoallw
+ *   MPI_Dist_graph_create_adjacent  src/dist_graph_create_adjacent.cpp:55-470
+ *   MPI_Dist_graph_neighbors        src/dist_graph_neighbors.cpp:13-49
+ *   MPI_Comm_rank    src/comm_rank.cpp:13-27         these three forward
+ *                    unchanged: they exist for KaHIP/METIS rank placement,
+ *                    which is out of scope (a no-op on one node: SURVEY F12)
+ *   MPI_Comm_free    src/comm_free.cpp:13-19         drop per-handle caches
  *
  * Error behaviour: return codes of the library pass through unchanged. Where
  * TEMPI itself detects an error (a pack that does not fit in outsize) it
@@ -72,6 +77,20 @@ int MPI_Test(MPI_Request *request, int *flag, MPI_Status *status);
 int MPI_Alltoallv(const void *sendbuf, const int sendcounts[], const int sdispls[],
                   MPI_Datatype sendtype, void *recvbuf, const int recvcounts[], const int rdispls[],
                   MPI_Datatype recvtype, MPI_Comm comm);
+int MPI_Neighbor_alltoallw(const void *sendbuf, const int sendcounts[], const MPI_Aint sdispls[],
+                           const MPI_Datatype sendtypes[], void *recvbuf, const int recvcounts[],
+                           const MPI_Aint rdispls[], const MPI_Datatype recvtypes[], MPI_Comm comm);
+int MPI_Neighbor_alltoallv(const void *sendbuf, const int sendcounts[], const int sdispls[],
+                           MPI_Datatype sendtype, void *recvbuf, const int recvcounts[],
+                           const int rdispls[], MPI_Datatype recvtype, MPI_Comm comm);
+int MPI_Dist_graph_create_adjacent(MPI_Comm comm_old, int indegree, const int sources[],
+                                   const int sourceweights[], int outdegree,
+                                   const int destinations[], const int destweights[],
+                                   MPI_Info info, int reorder, MPI_Comm *comm_dist_graph);
+int MPI_Dist_graph_neighbors(MPI_Comm comm, int maxindegree, int sources[], int sourceweights[],
+                             int maxoutdegree, int destinations[], int destweights[]);
+int MPI_Comm_rank(MPI_Comm comm, int *rank);
+int MPI_Comm_free(MPI_Comm *comm);
 
 #ifdef __cplusplus
 }

@@ -17,6 +17,10 @@ struct Counters {
   uint64_t sends = 0, recvs = 0, isends = 0, irecvs = 0;
   uint64_t send_device = 0, send_oneshot = 0, send_staged = 0, send_ipc = 0;
   uint64_t lib_sends = 0, lib_recvs = 0;
+  // sends to this same process: strided->strided copies, and those that
+  // had to be packed because their wait came before the matching receive
+  uint64_t send_direct = 0, direct_fallbacks = 0;
+  uint64_t neighbor_colls = 0; // neighbourhood collectives on device buffers
   // kernel time of synchronous MPI_Pack / MPI_Unpack while profiling is on
   double pack_kernel_ms = 0, unpack_kernel_ms = 0;
   uint64_t pack_timed = 0, unpack_timed = 0;

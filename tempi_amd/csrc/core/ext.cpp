@@ -59,6 +59,9 @@ TEMPI_EXPORT void tempi_get_counters(tempi_counters_t *o) {
   o->send_ipc = c.send_ipc;
   o->lib_sends = c.lib_sends;
   o->lib_recvs = c.lib_recvs;
+  o->send_direct = c.send_direct;
+  o->direct_fallbacks = c.direct_fallbacks;
+  o->neighbor_colls = c.neighbor_colls;
 }
 
 TEMPI_EXPORT void tempi_reset_counters(void) { counters = Counters(); }
@@ -95,7 +98,7 @@ TEMPI_EXPORT int64_t tempi_mpi_constant(const char *name, int *found) {
       H(MPI_PROC_NULL), H(MPI_SUM), H(MPI_MAX), H(MPI_MIN), H(MPI_THREAD_SINGLE),
       H(MPI_THREAD_FUNNELED), H(MPI_THREAD_SERIALIZED), H(MPI_THREAD_MULTIPLE),
       H(MPI_MAX_PROCESSOR_NAME), H(MPI_UNDEFINED),
-      P(MPI_STATUS_IGNORE), P(MPI_STATUSES_IGNORE), P(MPI_IN_PLACE),
+      P(MPI_STATUS_IGNORE), P(MPI_STATUSES_IGNORE), P(MPI_IN_PLACE), P(MPI_UNWEIGHTED), H(MPI_INFO_NULL),
       H(MPI_ERRORS_RETURN), H(MPI_ERRORS_ARE_FATAL),
       {"sizeof(MPI_Status)", int64_t(sizeof(MPI_Status))},
       {"sizeof(MPI_Aint)", int64_t(sizeof(MPI_Aint))},

@@ -32,6 +32,7 @@
 #include "tempi_mpi.h"
 
 #include <algorithm>
+#include <map>
 #include <vector>
 
 #define TEMPI_EXPORT extern "C" __attribute__((visibility("default")))
@@ -131,13 +132,37 @@ int isir(const void *sendbuf, const int *scounts, const int *sdispls, MPI_Dataty
   return err;
 }
 
-MPI_Comm worldDup = MPI_COMM_NULL;
+// private duplicates of application communicators, one per communicator,
+// made on first use and freed with it (MPI_Comm_free below) -- the
+// reference instead reserves tags on the application's communicator
+// (/root/reference/src/internal/tags.cpp)
+std::map<MPI_Comm, MPI_Comm> privateComms;
 
 } // namespace
 
-void coll_init() { MPI_Comm_dup(MPI_COMM_WORLD, &worldDup); }
+MPI_Comm private_comm(MPI_Comm comm) {
+  auto it = privateComms.find(comm);
+  if (it != privateComms.end()) return it->second;
+  MPI_Comm d;
+  MPI_Comm_dup(comm, &d);
+  privateComms[comm] = d;
+  return d;
+}
+
+void coll_init() { private_comm(MPI_COMM_WORLD); }
 void coll_finalize() {
-  if (worldDup != MPI_COMM_NULL) MPI_Comm_free(&worldDup);
+  for (auto &kv : privateComms) next.MPI_Comm_free(&kv.second);
+  privateComms.clear();
+}
+
+// the application frees `comm`: drop what TEMPI cached for the handle
+void comm_release(MPI_Comm comm) {
+  topology::uncache(comm);
+  auto it = privateComms.find(comm);
+  if (it != privateComms.end()) {
+    next.MPI_Comm_free(&it->second);
+    privateComms.erase(it);
+  }
 }
 
 } // namespace tempi
@@ -167,11 +192,7 @@ TEMPI_EXPORT int MPI_Alltoallv(const void *sendbuf, const int sendcounts[], cons
                     gpu::classify(static_cast<char *>(recvbuf) + lo).device_accessible;
   if (!sdev && !rdev) return lib();
   if (!type_lookup(sendtype) || !type_lookup(recvtype)) return lib(); // uncommitted: let MPI complain
-  MPI_Comm c = comm;
-  if (comm == MPI_COMM_WORLD)
-    c = worldDup;
-  else
-    MPI_Comm_dup(comm, &c);
+  const MPI_Comm c = private_comm(comm);
   int rc;
   switch (env.alltoallv) {
   case AlltoallvMethod::STAGED:
@@ -189,6 +210,5 @@ TEMPI_EXPORT int MPI_Alltoallv(const void *sendbuf, const int sendcounts[], cons
     rc = isir(sendbuf, sendcounts, sdispls, sendtype, recvbuf, recvcounts, rdispls, recvtype, c, n, rank, -1, -1);
     break;
   }
-  if (c != worldDup) MPI_Comm_free(&c);
   return rc;
 }

@@ -1,0 +1,203 @@
+// tempi_amd/csrc/core/interpose_neighbor.cpp -- neighbourhood collectives on
+// device buffers, and the communicator entry points of the reference's
+// exported set.
+//
+//   MPI_Neighbor_alltoallw  reference: /root/reference/src/neighbor_alltoallw.cpp:11-18
+//                           -> neighbor_alltoallw::isir
+//                           (/root/reference/src/internal/neighbor_alltoallw.cpp:19-77):
+//                           one MPI_Isend / MPI_Irecv per edge, so device
+//                           buffers go through TEMPI's packers.
+//   MPI_Neighbor_alltoallv  reference: /root/reference/src/neighbor_alltoallv.cpp:12-24
+//                           (a pure passthrough there: a non-GPU-aware MPI then
+//                           reads device memory from the host). Here it takes
+//                           the same per-edge route as alltoallw when any block
+//                           is on the GPU.
+//   MPI_Dist_graph_create_adjacent, MPI_Dist_graph_neighbors, MPI_Comm_rank
+//                           reference: src/dist_graph_create_adjacent.cpp:55-470,
+//                           src/dist_graph_neighbors.cpp:13-49, src/comm_rank.cpp:13-27.
+//                           They exist there for KaHIP/METIS rank placement,
+//                           out of scope here (a no-op on one node: SURVEY F12),
+//                           so the application and library ranks coincide and
+//                           these forward unchanged.
+//   MPI_Comm_free           reference: src/comm_free.cpp:13-19 -- drop the
+//                           handle's cached state (world-rank map, private
+//                           duplicate) before the library may reuse it.
+//
+// Differences from the reference's isir: receives are posted before sends
+// (the transport then launches arrived messages' copies while sends are still
+// being queued), completion goes through one MPI_Waitall, messages travel on
+// a private duplicate of the communicator instead of a reserved tag, and
+// Cartesian and (non-distributed) graph topologies are handled too, with
+// MPI_PROC_NULL neighbours skipped. Edges between the same pair of ranks are
+// matched in edge order, as the library's own implementation does.
+#include "counters.hpp"
+#include "gpu.hpp"
+#include "next_mpi.hpp"
+#include "state.hpp"
+#include "type_cache.hpp"
+
+#include "tempi_mpi.h"
+
+#include <vector>
+
+#define TEMPI_EXPORT extern "C" __attribute__((visibility("default")))
+
+namespace tempi {
+
+MPI_Comm private_comm(MPI_Comm comm); // interpose_coll.cpp
+void comm_release(MPI_Comm comm);
+
+namespace {
+
+// incoming / outgoing neighbours in MPI's canonical order; false when the
+// communicator has no topology (the library then raises the error)
+bool neighbours(MPI_Comm comm, std::vector<int> &in, std::vector<int> &out) {
+  int topo = MPI_UNDEFINED;
+  MPI_Topo_test(comm, &topo);
+  in.clear();
+  out.clear();
+  if (topo == MPI_DIST_GRAPH) {
+    int indeg = 0, outdeg = 0, weighted = 0;
+    MPI_Dist_graph_neighbors_count(comm, &indeg, &outdeg, &weighted);
+    in.resize(size_t(indeg));
+    out.resize(size_t(outdeg));
+    std::vector<int> iw(size_t(indeg) + 1), ow(size_t(outdeg) + 1);
+    next.MPI_Dist_graph_neighbors(comm, indeg, in.data(), weighted ? iw.data() : MPI_UNWEIGHTED, outdeg, out.data(),
+                                  weighted ? ow.data() : MPI_UNWEIGHTED);
+    return true;
+  }
+  if (topo == MPI_CART) {
+    int nd = 0;
+    MPI_Cartdim_get(comm, &nd);
+    for (int d = 0; d < nd; ++d) {
+      int lo = MPI_PROC_NULL, hi = MPI_PROC_NULL;
+      MPI_Cart_shift(comm, d, 1, &lo, &hi);
+      in.push_back(lo);
+      in.push_back(hi);
+    }
+    out = in;
+    return true;
+  }
+  if (topo == MPI_GRAPH) {
+    int rank = 0, n = 0;
+    next.MPI_Comm_rank(comm, &rank);
+    MPI_Graph_neighbors_count(comm, rank, &n);
+    in.resize(size_t(n));
+    MPI_Graph_neighbors(comm, rank, n, in.data());
+    out = in;
+    return true;
+  }
+  return false;
+}
+
+// true when some non-empty block lives in GPU-accessible memory
+bool any_device(const void *buf, const int *counts, const MPI_Aint *displs, const MPI_Datatype *types, size_t n) {
+  for (size_t i = 0; i < n; ++i) {
+    if (counts[i] <= 0) continue;
+    MPI_Aint tlb = 0, text = 0;
+    MPI_Type_get_true_extent(types[i], &tlb, &text);
+    if (gpu::classify(static_cast<const char *>(buf) + displs[i] + tlb).device_accessible) return true;
+  }
+  return false;
+}
+
+// one Isend / Irecv per edge through the interposed entry points (device
+// blocks -> TEMPI transport, host blocks -> library), receives first
+int isir(const void *sendbuf, const int *scounts, const MPI_Aint *sdispls, const MPI_Datatype *stypes,
+         void *recvbuf, const int *rcounts, const MPI_Aint *rdispls, const MPI_Datatype *rtypes, MPI_Comm comm,
+         const std::vector<int> &in, const std::vector<int> &out) {
+  const MPI_Comm c = private_comm(comm);
+  const int tag = 0x4E41; // "NA": alone on the private communicator
+  std::vector<MPI_Request> reqs;
+  reqs.reserve(in.size() + out.size());
+  for (size_t i = 0; i < in.size(); ++i) {
+    if (in[i] == MPI_PROC_NULL) continue;
+    MPI_Request r;
+    const int rc = MPI_Irecv(static_cast<char *>(recvbuf) + rdispls[i], rcounts[i], rtypes[i], in[i], tag, c, &r);
+    if (rc != MPI_SUCCESS) return rc;
+    reqs.push_back(r);
+  }
+  for (size_t i = 0; i < out.size(); ++i) {
+    if (out[i] == MPI_PROC_NULL) continue;
+    MPI_Request r;
+    const int rc =
+        MPI_Isend(static_cast<const char *>(sendbuf) + sdispls[i], scounts[i], stypes[i], out[i], tag, c, &r);
+    if (rc != MPI_SUCCESS) return rc;
+    reqs.push_back(r);
+  }
+  return MPI_Waitall(int(reqs.size()), reqs.data(), MPI_STATUSES_IGNORE);
+}
+
+} // namespace
+} // namespace tempi
+
+using namespace tempi;
+
+TEMPI_EXPORT int MPI_Neighbor_alltoallw(const void *sendbuf, const int sendcounts[], const MPI_Aint sdispls[],
+                                        const MPI_Datatype sendtypes[], void *recvbuf, const int recvcounts[],
+                                        const MPI_Aint rdispls[], const MPI_Datatype recvtypes[], MPI_Comm comm) {
+  resolve_next();
+  auto lib = [&] {
+    return next.MPI_Neighbor_alltoallw(sendbuf, sendcounts, sdispls, sendtypes, recvbuf, recvcounts, rdispls,
+                                       recvtypes, comm);
+  };
+  std::vector<int> in, out;
+  if (!state.active || !gpu::available() || !neighbours(comm, in, out)) return lib();
+  if (!any_device(sendbuf, sendcounts, sdispls, sendtypes, out.size()) &&
+      !any_device(recvbuf, recvcounts, rdispls, recvtypes, in.size()))
+    return lib(); // host memory only: the library's own algorithm
+  counters.neighbor_colls++;
+  return isir(sendbuf, sendcounts, sdispls, sendtypes, recvbuf, recvcounts, rdispls, recvtypes, comm, in, out);
+}
+
+TEMPI_EXPORT int MPI_Neighbor_alltoallv(const void *sendbuf, const int sendcounts[], const int sdispls[],
+                                        MPI_Datatype sendtype, void *recvbuf, const int recvcounts[],
+                                        const int rdispls[], MPI_Datatype recvtype, MPI_Comm comm) {
+  resolve_next();
+  auto lib = [&] {
+    return next.MPI_Neighbor_alltoallv(sendbuf, sendcounts, sdispls, sendtype, recvbuf, recvcounts, rdispls,
+                                       recvtype, comm);
+  };
+  std::vector<int> in, out;
+  if (!state.active || !gpu::available() || !neighbours(comm, in, out)) return lib();
+  // displacements are in extents of the one type: make the alltoallw form
+  MPI_Aint lb, sext, rext;
+  MPI_Type_get_extent(sendtype, &lb, &sext);
+  MPI_Type_get_extent(recvtype, &lb, &rext);
+  std::vector<MPI_Aint> sd(out.size()), rd(in.size());
+  for (size_t i = 0; i < out.size(); ++i) sd[i] = MPI_Aint(sdispls[i]) * sext;
+  for (size_t i = 0; i < in.size(); ++i) rd[i] = MPI_Aint(rdispls[i]) * rext;
+  std::vector<MPI_Datatype> st(out.size(), sendtype), rt(in.size(), recvtype);
+  if (!any_device(sendbuf, sendcounts, sd.data(), st.data(), out.size()) &&
+      !any_device(recvbuf, recvcounts, rd.data(), rt.data(), in.size()))
+    return lib();
+  counters.neighbor_colls++;
+  return isir(sendbuf, sendcounts, sd.data(), st.data(), recvbuf, recvcounts, rd.data(), rt.data(), comm, in, out);
+}
+
+TEMPI_EXPORT int MPI_Dist_graph_create_adjacent(MPI_Comm comm_old, int indegree, const int sources[],
+                                                const int sourceweights[], int outdegree, const int destinations[],
+                                                const int destweights[], MPI_Info info, int reorder,
+                                                MPI_Comm *comm_dist_graph) {
+  resolve_next();
+  return next.MPI_Dist_graph_create_adjacent(comm_old, indegree, sources, sourceweights, outdegree, destinations,
+                                             destweights, info, reorder, comm_dist_graph);
+}
+
+TEMPI_EXPORT int MPI_Dist_graph_neighbors(MPI_Comm comm, int maxindegree, int sources[], int sourceweights[],
+                                          int maxoutdegree, int destinations[], int destweights[]) {
+  resolve_next();
+  return next.MPI_Dist_graph_neighbors(comm, maxindegree, sources, sourceweights, maxoutdegree, destinations,
+                                       destweights);
+}
+
+TEMPI_EXPORT int MPI_Comm_rank(MPI_Comm comm, int *rank) {
+  resolve_next();
+  return next.MPI_Comm_rank(comm, rank);
+}
+
+TEMPI_EXPORT int MPI_Comm_free(MPI_Comm *comm) {
+  resolve_next();
+  if (state.active && comm && *comm != MPI_COMM_NULL) comm_release(*comm);
+  return next.MPI_Comm_free(comm);
+}

@@ -27,7 +27,7 @@ TEMPI_EXPORT int MPI_Send(const void *buf, int count, MPI_Datatype datatype, int
   }
   counters.sends++;
   MPI_Request r;
-  int rc = p2p::isend(buf, count, datatype, dest, tag, comm, &r);
+  int rc = p2p::isend(buf, count, datatype, dest, tag, comm, &r, -1, /*blocking=*/true);
   if (rc != MPI_SUCCESS) return rc;
   return p2p::wait(&r, MPI_STATUS_IGNORE);
 }

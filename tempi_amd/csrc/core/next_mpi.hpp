@@ -26,8 +26,14 @@
   X(MPI_Wait)                                                                  \
   X(MPI_Waitall)                                                               \
   X(MPI_Test)                                                                  \
-  X(MPI_Testsome)                                                                  \
-  X(MPI_Alltoallv)
+  X(MPI_Testsome)                                                              \
+  X(MPI_Alltoallv)                                                             \
+  X(MPI_Neighbor_alltoallv)                                                    \
+  X(MPI_Neighbor_alltoallw)                                                    \
+  X(MPI_Dist_graph_create_adjacent)                                            \
+  X(MPI_Dist_graph_neighbors)                                                  \
+  X(MPI_Comm_rank)                                                             \
+  X(MPI_Comm_free)
 
 namespace tempi {
 

@@ -47,6 +47,41 @@ struct IpcDesc {
 };
 static_assert(sizeof(IpcDesc) == 128, "descriptor size");
 
+// DIRECT (a send to this same process): the descriptor names the sender's
+// object itself, and the receiver copies it strided -> strided into its own
+// object with one kernel (tempi_hip_copy_batch): no packed intermediate, half
+// the HBM traffic of pack + unpack. The sender completes once the receiver's
+// copy has run. If the sender is waited on before the matching receive has
+// been posted, it falls back to gathering into a slab (so a wait on a send
+// never depends on a later receive), and the receiver unpacks that slab.
+constexpr uint64_t kMagicDirect = 0x54454d5049445254ull; // "TEMPIDRT"
+
+struct DirectDesc {
+  uint64_t magic[2];
+  uint64_t token; // key of the DirectShared below
+  int64_t bytes;
+  int32_t senderWorld;
+  int32_t senderPid;
+  int32_t device; // the sender object's GPU
+  int32_t pad;
+  uint64_t first;      // the sender object's first byte
+  tempi_hip_desc desc; // its shape, element count folded in
+  uint64_t reserved;
+};
+static_assert(sizeof(DirectDesc) == 160 && sizeof(DirectDesc) != sizeof(IpcDesc), "descriptor size");
+
+struct Op;
+struct DirectShared {
+  DirectDesc desc{}; // the library's send buffer: alive until the receiver claims it
+  enum State { PENDING, CLAIMED, PACKED, DONE } state = PENDING;
+  Slab *slab = nullptr; // PACKED: the sender's gather (released by the receiver)
+  int device = 0;
+  Op *sender = nullptr; // while the send is incomplete
+};
+std::map<uint64_t, std::shared_ptr<DirectShared>> directShared; // sent, not yet matched
+uint64_t nextDirectToken = 1;
+bool directEnabled = true;
+
 MPI_Comm ctrlComm = MPI_COMM_NULL; // private duplicate of MPI_COMM_WORLD for acks
 int tagUb = 32767;
 bool gpuAwareLibrary = false;
@@ -199,10 +234,12 @@ void put_event(void *e) {
 }
 
 // one batched launch (+ its trailing copies) and the event that follows it
+struct Op;
 struct GpuBatch {
   void *event = nullptr;
   int device = 0;
   bool complete = false;
+  std::vector<Op *> ops; // whose GPU work this batch carries (alive until gpu_done)
 };
 std::deque<std::shared_ptr<GpuBatch>> batches; // launch order
 
@@ -211,22 +248,36 @@ struct Op {
   virtual void gpu_done() {}                   // its GPU work completed
   virtual void lib_done(const MPI_Status &) {} // library request completed
   virtual void status(MPI_Status *s) const = 0;
+  virtual void stalled() {}                    // waited on and still incomplete after a pass
+  virtual void peer_done() {}                  // (direct sends) the receiver's copy ran
   bool queued = false;                         // GPU work not launched yet
-  std::shared_ptr<GpuBatch> batch;             // launched GPU work
   int device = 0;
   MPI_Request lib = MPI_REQUEST_NULL;          // outstanding library request
+  bool watched = false;                        // in libWatch
   bool done = false;
 };
+
+// ops with a library request outstanding (tested together by progress()).
+// Every post of Op::lib is followed by watch(op).
+std::vector<Op *> libWatch;
+void watch(Op *op) {
+  if (!op->watched && op->lib != MPI_REQUEST_NULL) {
+    op->watched = true;
+    libWatch.push_back(op);
+  }
+}
 
 // GPU work waiting for the next flush: gathers of Isends, scatters of Irecvs
 struct Pending {
   Op *op;
   std::vector<tempi_hip_batch_item> items;
+  std::vector<tempi_hip_copy_item> copies; // direct: strided -> strided (unpack list only)
   void *copyDst = nullptr, *copySrc = nullptr; // STAGED: D2H copy after the pack
   size_t copyBytes = 0;
 };
 std::vector<Pending> pendingPack, pendingUnpack;
 constexpr size_t kMaxPending = 512;
+constexpr size_t kEarlyFlush = 16;
 
 void flush_list(std::vector<Pending> &list, bool pack) {
   if (list.empty()) return;
@@ -248,6 +299,15 @@ void flush_list(std::vector<Pending> &list, bool pack) {
     gpu::check(pack ? tempi_hip_pack_batch(items.data(), int(items.size()), s)
                     : tempi_hip_unpack_batch(items.data(), int(items.size()), s),
                pack ? "batched pack" : "batched unpack");
+    if (!pack) {
+      std::vector<tempi_hip_copy_item> copies;
+      for (const Pending &p : list)
+        if (p.op->device == dev) copies.insert(copies.end(), p.copies.begin(), p.copies.end());
+      if (!copies.empty()) {
+        counters.batched_items += copies.size();
+        gpu::check(tempi_hip_copy_batch(copies.data(), int(copies.size()), s), "batched direct copy");
+      }
+    }
     for (const Pending &p : list)
       if (p.op->device == dev && p.copyBytes)
         gpu::check(tempi_hip_memcpy_async(p.copyDst, p.copySrc, p.copyBytes, s), "staged D2H");
@@ -259,7 +319,7 @@ void flush_list(std::vector<Pending> &list, bool pack) {
     for (const Pending &p : list)
       if (p.op->device == dev) {
         p.op->queued = false;
-        p.op->batch = b;
+        b->ops.push_back(p.op);
       }
     batches.push_back(b);
   }
@@ -310,9 +370,11 @@ struct IsendOp : Op {
     case Method::ONESHOT:
     case Method::STAGED:
       next.MPI_Isend(hslab->host, int(bytes), MPI_PACKED, dest, tag, comm, &lib);
+      watch(this);
       break;
     case Method::DEVICE:
       next.MPI_Isend(dslab->dev, int(bytes), MPI_PACKED, dest, tag, comm, &lib);
+      watch(this);
       break;
     case Method::IPC: {
       desc.magic[0] = kMagic0;
@@ -332,6 +394,7 @@ struct IsendOp : Op {
       next.MPI_Irecv(&pa.code, 1, MPI_INT, peer, desc.ackTag, ctrlComm, &pa.req);
       dslab = nullptr;
       next.MPI_Isend(&desc, int(sizeof desc), MPI_PACKED, dest, tag, comm, &lib);
+      watch(this);
       break;
     }
     default:
@@ -354,6 +417,164 @@ struct IsendOp : Op {
   }
 };
 
+struct IsendDirectOp : Op {
+  Packer packer;
+  const char *origin;
+  int count;
+  MPI_Datatype dt;
+  int64_t bytes;
+  std::shared_ptr<DirectShared> sh;
+  bool packDone = false;
+
+  IsendDirectOp(const TypeRecord &rec, const char *o, int c, MPI_Datatype d, int dest, int tag, MPI_Comm comm,
+                int dev, int64_t b, const tempi_hip_desc &flat)
+      : packer(rec.desc), origin(o), count(c), dt(d), bytes(b) {
+    device = dev;
+    sh = std::make_shared<DirectShared>();
+    sh->device = dev;
+    sh->sender = this;
+    const uint64_t token = nextDirectToken++;
+    directShared[token] = sh;
+    DirectDesc &desc = sh->desc;
+    desc.magic[0] = kMagicDirect;
+    desc.magic[1] = kMagic1;
+    desc.token = token;
+    desc.bytes = b;
+    desc.senderWorld = state.worldRank;
+    desc.senderPid = int32_t(getpid());
+    desc.device = dev;
+    desc.first = reinterpret_cast<uint64_t>(o + rec.desc.start);
+    desc.desc = flat;
+    // the library may hold a send to this same process open until its
+    // receive is posted (MPICH does), so the send's completion cannot wait for
+    // it: the request is released now and the descriptor outlives it in `sh`
+    MPI_Request r;
+    next.MPI_Isend(&desc, int(sizeof desc), MPI_PACKED, dest, tag, comm, &r);
+    MPI_Request_free(&r);
+  }
+  ~IsendDirectOp() override {
+    if (sh) sh->sender = nullptr;
+  }
+  void maybe_done() {
+    done = sh->state == DirectShared::DONE || (sh->state == DirectShared::PACKED && packDone);
+  }
+  void gpu_done() override {
+    packDone = true;
+    maybe_done();
+  }
+  void peer_done() override { maybe_done(); }
+  void stalled() override {
+    if (sh->state != DirectShared::PENDING) return;
+    // waited on before its receive exists: gather into a slab the receiver
+    // will unpack, so the send can complete on its own
+    counters.direct_fallbacks++;
+    sh->state = DirectShared::PACKED;
+    sh->slab = device_pool().get(size_t(bytes), device);
+    Pending p;
+    p.op = this;
+    packer.items(sh->slab->dev, origin, count, p.items);
+    queued = true;
+    pendingPack.push_back(std::move(p));
+  }
+  void status(MPI_Status *s) const override {
+    if (s != MPI_STATUS_IGNORE) {
+      s->MPI_SOURCE = MPI_ANY_SOURCE;
+      s->MPI_TAG = MPI_ANY_TAG;
+      s->MPI_ERROR = MPI_SUCCESS;
+      MPI_Status_set_elements(s, dt, 0);
+    }
+  }
+};
+
+// the receiver side is done with a direct send's bytes
+void direct_finish(std::shared_ptr<DirectShared> &sh) {
+  if (!sh) return;
+  if (sh->slab) {
+    device_pool().put(sh->slab);
+    sh->slab = nullptr;
+  }
+  sh->state = DirectShared::DONE;
+  if (sh->sender) sh->sender->peer_done();
+  sh.reset();
+}
+
+// the matched descriptor's shared state (unmatched until now)
+std::shared_ptr<DirectShared> claim_direct(const DirectDesc &d) {
+  auto it = directShared.find(d.token);
+  if (d.senderPid != int32_t(getpid()) || it == directShared.end())
+    LOG_FATAL("direct-send descriptor from another process (rank " << d.senderWorld << ")");
+  std::shared_ptr<DirectShared> sh = it->second;
+  directShared.erase(it);
+  return sh;
+}
+
+// a direct send's packed bytes into pinned host memory `dst`, synchronously
+// (receivers that are not a same-device TEMPI receive), then finish it
+void materialise_direct(std::shared_ptr<DirectShared> &sh, const DirectDesc &d, Slab *dst) {
+  void *s = gpu::stream(sh->device);
+  int cur = 0;
+  tempi_hip_get_device(&cur);
+  if (cur != sh->device) tempi_hip_set_device(sh->device);
+  if (sh->state == DirectShared::PACKED) {
+    gpu::check(tempi_hip_stream_synchronize(s), "direct fallback sync");
+    gpu::check(tempi_hip_memcpy(dst->host, sh->slab->dev, size_t(d.bytes)), "direct fallback copy");
+  } else {
+    gpu::check(tempi_hip_pack(dst->dev, reinterpret_cast<const void *>(d.first), &d.desc, s), "direct gather");
+    gpu::check(tempi_hip_stream_synchronize(s), "direct gather sync");
+  }
+  if (cur != sh->device) tempi_hip_set_device(cur);
+  direct_finish(sh);
+}
+
+bool is_direct(const void *msg, int n) {
+  if (size_t(n) != sizeof(DirectDesc)) return false;
+  uint64_t m[2];
+  std::memcpy(m, msg, sizeof m);
+  return m[0] == kMagicDirect && m[1] == kMagic1;
+}
+bool is_ipc(const void *msg, int n) {
+  if (size_t(n) != sizeof(IpcDesc)) return false;
+  uint64_t m[2];
+  std::memcpy(m, msg, sizeof m);
+  return m[0] == kMagic0 && m[1] == kMagic1;
+}
+
+// A descriptor landed in a host buffer of a receive that cannot use it
+// in place (library receives): fetch the bytes it names into `out` (the IPC
+// pull or the direct gather, blocking) and release the sender.
+void land_descriptor(const void *msg, int n, std::vector<char> &out) {
+  if (is_direct(msg, n)) {
+    DirectDesc d;
+    std::memcpy(&d, msg, sizeof d);
+    std::shared_ptr<DirectShared> sh = claim_direct(d);
+    Slab *h = pinned_pool().get(size_t(std::max<int64_t>(d.bytes, 1)), sh->device);
+    materialise_direct(sh, d, h);
+    out.assign(static_cast<char *>(h->host), static_cast<char *>(h->host) + d.bytes);
+    pinned_pool().put(h);
+    return;
+  }
+  IpcDesc d;
+  std::memcpy(&d, msg, sizeof d);
+  out.resize(size_t(std::max<int64_t>(d.bytes, 1)));
+  if (void *base = peer_pointer(d)) {
+    gpu::check(tempi_hip_memcpy(out.data(), static_cast<const char *>(base) + d.offset, size_t(d.bytes)), "ipc pull");
+    send_ack(d);
+  } else { // the sender re-sends through the host
+    MPI_Request r;
+    next.MPI_Irecv(out.data(), int(d.bytes), MPI_PACKED, d.senderWorld, d.ackTag, ctrlComm, &r);
+    send_ack(d, 1);
+    for (;;) {
+      int flag = 0;
+      next.MPI_Test(&r, &flag, MPI_STATUS_IGNORE);
+      if (flag) break;
+      progress();
+    }
+  }
+  out.resize(size_t(d.bytes));
+}
+
+constexpr size_t kDescCap = sizeof(DirectDesc) > sizeof(IpcDesc) ? sizeof(DirectDesc) : sizeof(IpcDesc);
+
 struct IrecvOp : Op {
   Packer packer;
   char *origin; // GPU-visible
@@ -367,14 +588,27 @@ struct IrecvOp : Op {
   bool ipc = false;
   bool fallback = false; // waiting for the bytes the peer re-sends through the host
   int64_t elems = 0;
+  std::shared_ptr<DirectShared> direct; // a same-process send being copied / unpacked
 
   IrecvOp(const TypeRecord &rec, char *o, int c, MPI_Datatype d, int source, int tag, MPI_Comm cm, int dev,
           int64_t b)
       : packer(rec.desc), origin(o), count(c), dt(d), comm(cm), bytes(b) {
     device = dev;
-    const size_t cap = std::max<size_t>(size_t(bytes), sizeof(IpcDesc));
+    const size_t cap = std::max<size_t>(size_t(bytes), kDescCap);
     hslab = pinned_pool().get(cap, device);
     next.MPI_Irecv(hslab->host, int(cap), MPI_PACKED, source, tag, comm, &lib);
+    // a message from this same process is matched as the receive is posted:
+    // take it now, so its copy can start while the caller posts more
+    if (source >= 0 && topology::world_rank(comm, source) == state.worldRank) {
+      int flag = 0;
+      MPI_Status st;
+      next.MPI_Test(&lib, &flag, &st);
+      if (flag) {
+        lib = MPI_REQUEST_NULL;
+        lib_done(st);
+      }
+    }
+    watch(this);
   }
 
   void lib_done(const MPI_Status &st) override { // arrived: queue its unpack
@@ -395,6 +629,35 @@ struct IrecvOp : Op {
     const int64_t size = packer.desc().size;
     Pending p;
     p.op = this;
+    if (is_direct(hslab->host, n)) {
+      DirectDesc dd;
+      std::memcpy(&dd, hslab->host, sizeof dd);
+      direct = claim_direct(dd);
+      if (dd.bytes > bytes) LOG_FATAL("message truncated: " << dd.bytes << " B into " << bytes);
+      elems = size ? dd.bytes / size : 0;
+      const bool sameDevice = direct->device == device;
+      tempi_hip_desc mine;
+      char *first = origin + packer.desc().start;
+      if (direct->state == DirectShared::PENDING && sameDevice && elems * size == dd.bytes &&
+          packer.flat(elems, &mine) &&
+          tempi_hip_copy_supported(first, reinterpret_cast<const void *>(dd.first), &mine, &dd.desc) == 1) {
+        direct->state = DirectShared::CLAIMED;
+        tempi_hip_copy_item c;
+        c.dst_first = first;
+        c.src_first = reinterpret_cast<const void *>(dd.first);
+        c.dst = mine;
+        c.src = dd.desc;
+        p.copies.push_back(c);
+      } else if (direct->state == DirectShared::PACKED && sameDevice) {
+        packer.items(direct->slab->dev, origin, elems, p.items);
+      } else { // another device, or a shape the copy kernel does not take
+        materialise_direct(direct, dd, hslab);
+        packer.items(hslab->dev, origin, elems, p.items);
+      }
+      queued = true;
+      pendingUnpack.push_back(std::move(p));
+      return;
+    }
     if (size_t(n) == sizeof(IpcDesc) && d.magic[0] == kMagic0 && d.magic[1] == kMagic1) {
       ipc = true;
       desc = d;
@@ -404,6 +667,7 @@ struct IrecvOp : Op {
         ipc = false;
         fallback = true;
         next.MPI_Irecv(hslab->host, int(d.bytes), MPI_PACKED, d.senderWorld, d.ackTag, ctrlComm, &lib);
+        watch(this);
         send_ack(d, 1);
         return;
       }
@@ -420,6 +684,7 @@ struct IrecvOp : Op {
   }
   void gpu_done() override {
     if (ipc) send_ack(desc);
+    direct_finish(direct);
     pinned_pool().put(hslab);
     hslab = nullptr;
     done = true;
@@ -443,6 +708,7 @@ struct LibIsendOp : Op {
     int pos = 0;
     tempi::pack(b, c, d, buf.data(), int(buf.size()), &pos, comm);
     next.MPI_Isend(buf.data(), pos, MPI_PACKED, dest, tag, comm, &lib);
+    watch(this);
   }
   void lib_done(const MPI_Status &) override { done = true; }
   void status(MPI_Status *s) const override {
@@ -462,13 +728,20 @@ struct LibIrecvOp : Op {
   MPI_Status libStatus{};
   int elems = 0;
   LibIrecvOp(void *b, int c, MPI_Datatype d, int source, int tag, MPI_Comm cm) : user(b), count(c), dt(d), comm(cm) {
-    buf.resize(size_t(std::max<int64_t>(pack_size(c, d, cm), 1)));
+    buf.resize(std::max<size_t>(size_t(std::max<int64_t>(pack_size(c, d, cm), 1)), kDescCap));
     next.MPI_Irecv(buf.data(), int(buf.size()), MPI_PACKED, source, tag, comm, &lib);
+    watch(this);
   }
   void lib_done(const MPI_Status &st) override {
     libStatus = st;
     int n = 0, size = 0;
     MPI_Get_count(&libStatus, MPI_PACKED, &n);
+    if (is_direct(buf.data(), n) || is_ipc(buf.data(), n)) { // a TEMPI sender's descriptor
+      std::vector<char> bytes;
+      land_descriptor(buf.data(), n, bytes);
+      buf.swap(bytes);
+      n = int(buf.size());
+    }
     MPI_Type_size(dt, &size);
     elems = size ? n / size : 0;
     int pos = 0;
@@ -512,6 +785,8 @@ std::vector<MPI_Status> pollSt;
 
 void init() {
   gpuAwareLibrary = std::getenv("TEMPI_MPI_GPU_AWARE") != nullptr;
+  directEnabled = std::getenv("TEMPI_NO_DIRECT") == nullptr;
+  directShared.clear();
   systemPerformanceLoaded = import_system_performance(&systemPerformance);
   modelCache.clear();
   if (const char *s = std::getenv("TEMPI_IPC_MIN_BYTES")) ipcMinBytes = std::atoll(s);
@@ -539,6 +814,10 @@ void finalize() {
     }
   }
   active.clear();
+  libWatch.clear();
+  for (auto &b : batches)
+    if (b->event) tempi_hip_event_destroy(b->event);
+  batches.clear();
   while (!pendingAcks.empty()) {
     progress();
     if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(30)) {
@@ -565,7 +844,7 @@ bool handles(const void *buf, int count, MPI_Datatype dt, int peer) {
 }
 
 int isend(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Comm comm, MPI_Request *req,
-          int force) {
+          int force, bool blocking) {
   const TypeRecord *rec = type_lookup(dt);
   ScopedNs timer(counters.ns_isend);
   if (pendingPack.size() >= kMaxPending) flush(); // (no progress(): consecutive Isends share a launch)
@@ -590,6 +869,14 @@ int isend(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Co
   default: break;
   }
   const char *origin = static_cast<const char *>(p.dptr) - rec->desc.start;
+  // a non-blocking send to this same process: the receiver copies directly
+  tempi_hip_desc flat;
+  if (directEnabled && !blocking && force < 0 && topology::world_rank(comm, dest) == state.worldRank &&
+      Packer(rec->desc).flat(count, &flat)) {
+    counters.send_direct++;
+    *req = add(std::make_unique<IsendDirectOp>(*rec, origin, count, dt, dest, tag, comm, p.device, bytes, flat));
+    return MPI_SUCCESS;
+  }
   int cur = 0;
   tempi_hip_get_device(&cur);
   if (cur != p.device) tempi_hip_set_device(p.device);
@@ -613,6 +900,9 @@ int irecv(void *buf, int count, MPI_Datatype dt, int source, int tag, MPI_Comm c
   const int64_t bytes = pack_size(count, dt, comm);
   char *origin = static_cast<char *>(p.dptr) - rec->desc.start;
   *req = add(std::make_unique<IrecvOp>(*rec, origin, count, dt, source, tag, comm, p.device, bytes));
+  // keep the GPU busy while the caller is still posting: launch arrived
+  // messages' copies / unpacks once a launch's worth has queued up
+  if (pendingUnpack.size() >= kEarlyFlush) flush_list(pendingUnpack, false);
   counters.ns_irecv += now_ns() - t0;
   return MPI_SUCCESS;
 }
@@ -638,41 +928,35 @@ bool progress(bool full) {
   // 1. GPU events, in launch order (one stream per device: a later event of
   //    the same device cannot complete before an earlier one)
   uint64_t t0 = now_ns();
-  int blockedDevice = -1;
+  uint64_t blocked = 0; // devices (bit per device < 64) with an incomplete batch
   for (auto &b : batches) {
-    if (b->complete || b->device == blockedDevice) continue;
+    const uint64_t bit = uint64_t(1) << (b->device & 63);
+    if (b->complete || (blocked & bit)) continue;
     const int q = tempi_hip_event_query(b->event);
     if (q == 1) {
-      blockedDevice = b->device;
+      blocked |= bit;
       continue;
     }
     gpu::check(q, "event query");
     put_event(b->event);
     b->event = nullptr;
     b->complete = true;
+    std::vector<Op *> ops;
+    ops.swap(b->ops);
+    for (Op *op : ops) op->gpu_done();
+    moved = true;
   }
   while (!batches.empty() && batches.front()->complete) batches.pop_front();
-  for (auto &kv : active) {
-    Op *op = kv.second.get();
-    if (op->batch && op->batch->complete) {
-      op->batch.reset();
-      op->gpu_done();
-      moved = true;
-    }
-  }
   counters.ns_events += now_ns() - t0;
   t0 = now_ns();
   // 2. every outstanding library request in one MPI_Testsome
   pollReqs.clear();
   pollOps.clear();
   pollAck.clear();
-  for (auto &kv : active) {
-    Op *op = kv.second.get();
-    if (op->lib != MPI_REQUEST_NULL && !op->done) {
-      pollReqs.push_back(op->lib);
-      pollOps.push_back(op);
-      pollAck.push_back(0);
-    }
+  for (Op *op : libWatch) {
+    pollReqs.push_back(op->lib);
+    pollOps.push_back(op);
+    pollAck.push_back(0);
   }
   for (size_t i = 0; i < pendingAcks.size(); ++i) {
     pollReqs.push_back(pendingAcks[i]->req);
@@ -696,6 +980,16 @@ bool progress(bool full) {
         ackedSlots.push_back(pollAck[i]);
       }
       moved = true;
+    }
+    if (outcount) { // drop completed requests from the watch list (re-posted ones stay)
+      size_t w = 0;
+      for (Op *op : libWatch) {
+        if (op->lib != MPI_REQUEST_NULL)
+          libWatch[w++] = op;
+        else
+          op->watched = false;
+      }
+      libWatch.resize(w);
     }
     // release acknowledged slabs (highest index first keeps indices valid)
     std::sort(ackedSlots.rbegin(), ackedSlots.rend());
@@ -729,7 +1023,11 @@ int wait(MPI_Request *req, MPI_Status *status) {
   auto it = active.find(h);
   if (it == active.end()) return next.MPI_Wait(req, status);
   ScopedNs timer(counters.ns_wait);
-  while (!it->second->done) progress();
+  Op *op = it->second.get();
+  while (!op->done) {
+    progress();
+    if (!op->done) op->stalled();
+  }
   it->second->status(status);
   active.erase(it);
   *req = MPI_REQUEST_NULL;
@@ -741,6 +1039,7 @@ int test(MPI_Request *req, int *flag, MPI_Status *status) {
   auto it = active.find(h);
   if (it == active.end()) return next.MPI_Test(req, flag, status);
   progress();
+  if (!it->second->done) it->second->stalled();
   *flag = it->second->done ? 1 : 0;
   if (*flag) {
     it->second->status(status);
@@ -766,34 +1065,18 @@ int recv_host_ipc_aware(void *buf, int count, MPI_Datatype dt, int source, int t
   *handled = true;
   int n = 0;
   MPI_Get_count(&st, MPI_BYTE, &n);
-  if (size_t(n) != sizeof(IpcDesc)) return MPI_Mrecv(buf, count, dt, &msg, status);
-  IpcDesc d;
-  MPI_Mrecv(&d, n, MPI_BYTE, &msg, &st);
+  if (size_t(n) != sizeof(IpcDesc) && size_t(n) != sizeof(DirectDesc)) return MPI_Mrecv(buf, count, dt, &msg, status);
+  alignas(16) char raw[kDescCap];
+  MPI_Mrecv(raw, n, MPI_BYTE, &msg, &st);
   int size = 0;
   MPI_Type_size(dt, &size);
   std::vector<char> packed;
   int nbytes = n;
-  const char *src = reinterpret_cast<const char *>(&d);
-  if (d.magic[0] == kMagic0 && d.magic[1] == kMagic1) { // pull over IPC
-    packed.resize(size_t(std::max<int64_t>(d.bytes, 1)));
-    void *base = peer_pointer(d);
-    if (base) {
-      gpu::check(tempi_hip_memcpy(packed.data(), static_cast<const char *>(base) + d.offset, size_t(d.bytes)),
-                 "ipc pull");
-      send_ack(d);
-    } else {
-      MPI_Request r;
-      next.MPI_Irecv(packed.data(), int(d.bytes), MPI_PACKED, d.senderWorld, d.ackTag, ctrlComm, &r);
-      send_ack(d, 1);
-      while (true) {
-        int flag = 0;
-        next.MPI_Test(&r, &flag, MPI_STATUS_IGNORE);
-        if (flag) break;
-        progress();
-      }
-    }
+  const char *src = raw;
+  if (is_direct(raw, n) || is_ipc(raw, n)) { // a TEMPI sender's descriptor: fetch what it names
+    land_descriptor(raw, n, packed);
     src = packed.data();
-    nbytes = int(d.bytes);
+    nbytes = int(packed.size());
   }
   const int elems = size ? nbytes / size : 0;
   int pos = 0;

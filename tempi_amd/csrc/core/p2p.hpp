@@ -22,6 +22,11 @@
 //            the receiver maps the sender's slab and its unpack kernel reads
 //            the packed bytes over xGMI, then acknowledges so the sender can
 //            reuse the slab
+//   DIRECT   (sends to the same process, non-blocking only) the descriptor
+//            names the sender's object; the receiver copies it strided ->
+//            strided with one kernel (no packed intermediate); a send waited
+//            on before its receive is posted falls back to a gathered slab.
+//            TEMPI_NO_DIRECT disables it
 //   AUTO     IPC for co-located peers at >= TEMPI_IPC_MIN_BYTES (4 KiB),
 //            ONESHOT otherwise (with no perf.json the reference would stop
 //            here with LOG_FATAL: SURVEY F10)
@@ -44,8 +49,10 @@ bool handles(const void *buf, int count, MPI_Datatype dt, int peer);
 
 // force: -1 = choose by TEMPI_DATATYPE_* / AUTO; else a forced method
 // (0 ONESHOT, 1 STAGED, 2 DEVICE, 3 IPC)
+// blocking = true (MPI_Send) never takes the DIRECT route, whose completion
+// needs the matching receive
 int isend(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Comm comm, MPI_Request *req,
-          int force = -1);
+          int force = -1, bool blocking = false);
 int irecv(void *buf, int count, MPI_Datatype dt, int source, int tag, MPI_Comm comm, MPI_Request *req);
 
 bool is_tempi_request(MPI_Request r);

@@ -67,6 +67,23 @@ void Packer::items(void *packed, const void *origin, int64_t count, std::vector<
           tmp.dims.data(), int(tmp.dims.size()), out);
 }
 
+bool Packer::flat(int64_t count, tempi_hip_desc *out) const {
+  StridedBlock tmp;
+  tmp.block = sb_.block;
+  if (count > 1) tmp.dims.push_back(Dim{count, sb_.extent});
+  tmp.dims.insert(tmp.dims.end(), sb_.dims.begin(), sb_.dims.end());
+  simplify(tmp);
+  if (tmp.dims.size() > size_t(TEMPI_HIP_MAX_DIMS)) return false;
+  *out = tempi_hip_desc{};
+  out->block = count > 0 ? tmp.block : 0;
+  out->ndims = int32_t(tmp.dims.size());
+  for (size_t k = 0; k < tmp.dims.size(); ++k) {
+    out->counts[k] = tmp.dims[k].count;
+    out->strides[k] = tmp.dims[k].stride;
+  }
+  return true;
+}
+
 int Packer::launch(bool pack, char *packed, char *origin, int64_t count, void *stream) const {
   if (count <= 0 || sb_.size == 0) return 0;
   std::vector<Dim> dims;

@@ -34,6 +34,10 @@ public:
   // the transport batches many messages into one kernel launch
   void items(void *packed, const void *origin, int64_t count, std::vector<tempi_hip_batch_item> &out) const;
 
+  // `count` elements as ONE descriptor whose first byte is origin + start
+  // (false when it needs more than TEMPI_HIP_MAX_DIMS dimensions)
+  bool flat(int64_t count, tempi_hip_desc *out) const;
+
   const StridedBlock &desc() const { return sb_; }
 
 private:

@@ -6,6 +6,7 @@
 
 #include <cstring>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 namespace tempi {
@@ -14,6 +15,9 @@ namespace topology {
 namespace {
 std::vector<int> nodeOf; // world rank -> node index
 int myNode = 0, localRank = 0, nodeRanks = 1;
+// communicator -> world rank of each of its ranks (remote group for an
+// intercommunicator); dropped by MPI_Comm_free (uncache)
+std::unordered_map<MPI_Comm, std::vector<int>> worldOf;
 } // namespace
 
 void init() {
@@ -44,25 +48,37 @@ void init() {
   LOG_DEBUG("topology: " << uniq.size() << " node(s), " << nodeRanks << " rank(s) on mine");
 }
 
-void finalize() { nodeOf.clear(); }
+void finalize() {
+  nodeOf.clear();
+  worldOf.clear();
+}
 
 int world_rank(MPI_Comm comm, int rank) {
   if (comm == MPI_COMM_WORLD) return rank;
   if (rank < 0) return MPI_UNDEFINED;
-  MPI_Group g, wg;
-  int inter = 0;
-  MPI_Comm_test_inter(comm, &inter);
-  if (inter)
-    MPI_Comm_remote_group(comm, &g);
-  else
-    MPI_Comm_group(comm, &g);
-  MPI_Comm_group(MPI_COMM_WORLD, &wg);
-  int out = MPI_UNDEFINED;
-  MPI_Group_translate_ranks(g, 1, &rank, wg, &out);
-  MPI_Group_free(&g);
-  MPI_Group_free(&wg);
-  return out;
+  auto it = worldOf.find(comm);
+  if (it == worldOf.end()) {
+    MPI_Group g, wg;
+    int inter = 0;
+    MPI_Comm_test_inter(comm, &inter);
+    if (inter)
+      MPI_Comm_remote_group(comm, &g);
+    else
+      MPI_Comm_group(comm, &g);
+    MPI_Comm_group(MPI_COMM_WORLD, &wg);
+    int n = 0;
+    MPI_Group_size(g, &n);
+    std::vector<int> mine(static_cast<size_t>(n)), world(static_cast<size_t>(n), MPI_UNDEFINED);
+    for (int i = 0; i < n; ++i) mine[size_t(i)] = i;
+    MPI_Group_translate_ranks(g, n, mine.data(), wg, world.data());
+    MPI_Group_free(&g);
+    MPI_Group_free(&wg);
+    it = worldOf.emplace(comm, std::move(world)).first;
+  }
+  return size_t(rank) < it->second.size() ? it->second[size_t(rank)] : MPI_UNDEFINED;
 }
+
+void uncache(MPI_Comm comm) { worldOf.erase(comm); }
 
 bool colocated_world(int w) {
   if (w < 0 || size_t(w) >= nodeOf.size()) return false;

@@ -4,7 +4,9 @@
 // communicator (/root/reference/src/internal/topology.cpp:34-90) and answers
 // is_colocated (:191-196). Here: one allgather of host names over
 // MPI_COMM_WORLD at MPI_Init; other communicators are mapped to world ranks
-// with MPI_Group_translate_ranks on demand (no stale per-handle cache). The
+// with MPI_Group_translate_ranks once, cached per handle and dropped by the
+// interposed MPI_Comm_free before the library frees (and may reuse) the
+// handle (/root/reference/src/comm_free.cpp:13-19 does the same). The
 // reference's app/library rank permutation exists only for KaHIP/METIS
 // placement, which is out of scope (identity here: SURVEY F12).
 #pragma once
@@ -17,6 +19,7 @@ namespace topology {
 void init();
 void finalize();
 int world_rank(MPI_Comm comm, int rank); // MPI_UNDEFINED if not in world
+void uncache(MPI_Comm comm);              // the handle is about to be freed
 bool colocated(MPI_Comm comm, int rank);
 bool colocated_world(int worldRank);
 int node_local_rank(); // this rank's index among the ranks on its node

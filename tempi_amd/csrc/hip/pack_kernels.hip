@@ -608,9 +608,213 @@ int run_batch(bool pack, const tempi_hip_batch_item *items, int n, hipStream_t s
   return 0;
 }
 
+// ------------------------------------------------------ strided -> strided copy
+//
+// dst object <- src object, both describing the same bytes in type-map order
+// (e.g. a halo face sent to the same process: the interior face of one buffer
+// into the exterior face of another). No packed intermediate, so HBM sees the
+// payload once each way instead of twice. Each side keeps its own shape: the
+// virtual packed word q is decoded independently into a src and a dst offset.
+//
+// A workgroup owns kBlock * 16/W consecutive words; word j of a lane is
+// tileBase + j * kBlock + lane, so every load/store instruction of a wave
+// touches 64 consecutive words (coalesced whenever rows are longer than a few
+// words). Each side has at most kCopyND dimensions after normalisation (the
+// unbounded outermost one lives in the last slot; the unused slots in between
+// have count 1, stride 0); anything deeper is reported unsupported and the
+// caller packs + unpacks through a slab instead.
+constexpr int kCopyND = 3;
+
+struct CSide {
+  char *first;
+  uint32_t wpr;
+  Magic mwpr;
+  uint32_t cnt[kCopyND - 1]; // the outermost slot is unbounded
+  Magic mcnt[kCopyND - 1];
+  int64_t stride[kCopyND];
+};
+
+struct CArgs {
+  CSide s, d;
+  uint32_t nwords;
+};
+
+template <int W> __device__ __forceinline__ int64_t side_offset(uint32_t q, const CSide &c) {
+  uint32_t row = mdiv(q, c.mwpr);
+  int64_t off = int64_t(q - row * c.wpr) * W;
+#pragma unroll
+  for (int k = 0; k < kCopyND - 1; ++k) {
+    const uint32_t r2 = mdiv(row, c.mcnt[k]);
+    off += int64_t(row - r2 * c.cnt[k]) * c.stride[k];
+    row = r2;
+  }
+  return off + int64_t(row) * c.stride[kCopyND - 1];
+}
+
+#ifndef TEMPI_COPY_U
+#define TEMPI_COPY_U 1
+#endif
+template <int W> __device__ __forceinline__ void copy_body(const CArgs &a, uint32_t blk, uint32_t nblk) {
+  typedef typename Word<W>::T WT;
+  constexpr int CW = 16 / W * TEMPI_COPY_U;
+  constexpr bool nt = W == 16;
+  const uint32_t tile = uint32_t(kBlock) * CW;
+  for (uint32_t base = blk * tile; base < a.nwords; base += nblk * tile) {
+    WT v[CW];
+#pragma unroll
+    for (int j = 0; j < CW; ++j) {
+      const uint32_t q = base + uint32_t(j) * kBlock + threadIdx.x;
+      if (q < a.nwords) v[j] = ld(reinterpret_cast<const WT *>(a.s.first + side_offset<W>(q, a.s)), nt);
+    }
+#pragma unroll
+    for (int j = 0; j < CW; ++j) {
+      const uint32_t q = base + uint32_t(j) * kBlock + threadIdx.x;
+      if (q < a.nwords) st(reinterpret_cast<WT *>(a.d.first + side_offset<W>(q, a.d)), v[j], nt);
+    }
+  }
+}
+
+template <int W> __global__ __launch_bounds__(kBlock) void copy_kernel(const CArgs a) {
+  copy_body<W>(a, blockIdx.x, gridDim.x);
+}
+
+constexpr int kCopyMax = int((kBatchBytes - 8) / (sizeof(CArgs) + 4));
+struct CBatchArgs {
+  uint32_t nitems;
+  uint32_t first[kCopyMax + 1];
+  CArgs item[kCopyMax];
+};
+
+template <int W> __global__ __launch_bounds__(kBlock) void copy_batch_kernel(const CBatchArgs b) {
+  uint32_t lo = 0, hi = b.nitems;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (blockIdx.x >= b.first[mid])
+      lo = mid;
+    else
+      hi = mid;
+  }
+  copy_body<W>(b.item[lo], blockIdx.x - b.first[lo], b.first[lo + 1] - b.first[lo]);
+}
+
+bool make_side(char *first, const Norm &n, int W, CSide *c) {
+  if (n.nd > kCopyND) return false;
+  *c = CSide{};
+  c->first = first;
+  c->wpr = uint32_t(n.block / W);
+  c->mwpr = make_magic(c->wpr);
+  for (int k = 0; k < kCopyND - 1; ++k) {
+    c->cnt[k] = 1;
+    c->mcnt[k] = make_magic(1);
+  }
+  // innermost first into slots 0 .. nd-2; the outermost into the last slot
+  for (int k = 0; k < n.nd; ++k) {
+    const int src = n.nd - 1 - k;
+    if (src == 0) {
+      c->stride[kCopyND - 1] = n.str[0];
+    } else {
+      if (n.cnt[src] >= (int64_t(1) << 32)) return false;
+      c->cnt[k] = uint32_t(n.cnt[src]);
+      c->mcnt[k] = make_magic(c->cnt[k]);
+      c->stride[k] = n.str[src];
+    }
+  }
+  return true;
+}
+
+struct CopyJob {
+  CArgs a;
+  int w;
+};
+
+// the copy as one kernel item, or false when it needs the pack + unpack route
+bool plan_copy(void *dst, const void *src, const tempi_hip_desc *dd, const tempi_hip_desc *sd, CopyJob *job) {
+  Norm nd, ns;
+  if (!normalise(dd, &nd) || !normalise(sd, &ns)) return false;
+  const int64_t bytes = norm_bytes(ns);
+  if (bytes != norm_bytes(nd) || bytes >= kMaxLaunchBytes) return false;
+  int w = word_width(reinterpret_cast<uintptr_t>(dst), reinterpret_cast<uintptr_t>(src), ns);
+  const int wd = word_width(reinterpret_cast<uintptr_t>(dst), reinterpret_cast<uintptr_t>(src), nd);
+  if (wd < w) w = wd;
+  if (!make_side(const_cast<char *>(static_cast<const char *>(src)), ns, w, &job->a.s)) return false;
+  if (!make_side(static_cast<char *>(dst), nd, w, &job->a.d)) return false;
+  job->a.nwords = uint32_t(bytes / w);
+  job->w = w;
+  return true;
+}
+
+uint32_t copy_blocks(const CopyJob &j) {
+  const uint64_t tile = uint64_t(kBlock) * (16 / j.w) * TEMPI_COPY_U;
+  uint64_t b = (uint64_t(j.a.nwords) + tile - 1) / tile;
+  if (b > TEMPI_MAX_BLOCKS) b = TEMPI_MAX_BLOCKS;
+  return uint32_t(b);
+}
+
+template <int W> int launch_copy_group(const std::vector<CopyJob> &jobs, hipStream_t s) {
+  CBatchArgs b;
+  b.nitems = 0;
+  uint32_t total = 0;
+  auto flush = [&]() -> int {
+    if (!b.nitems) return 0;
+    b.first[b.nitems] = total;
+    if (b.nitems == 1)
+      hipLaunchKernelGGL(copy_kernel<W>, dim3(total), dim3(kBlock), 0, s, b.item[0]);
+    else
+      hipLaunchKernelGGL(copy_batch_kernel<W>, dim3(total), dim3(kBlock), 0, s, b);
+    b.nitems = 0;
+    total = 0;
+    return int(hipGetLastError());
+  };
+  for (const CopyJob &j : jobs) {
+    const uint32_t blocks = copy_blocks(j);
+    if (!blocks) continue;
+    if (uint64_t(total) + blocks >= (uint64_t(1) << 31))
+      if (int e = flush()) return e;
+    b.first[b.nitems] = total;
+    b.item[b.nitems] = j.a;
+    b.nitems++;
+    total += blocks;
+    if (b.nitems == uint32_t(kCopyMax))
+      if (int e = flush()) return e;
+  }
+  return flush();
+}
+
 } // namespace
 
 extern "C" {
+
+int tempi_hip_copy_supported(void *dst_first, const void *src_first, const tempi_hip_desc *dst,
+                             const tempi_hip_desc *src) {
+  CopyJob j;
+  return plan_copy(dst_first, src_first, dst, src, &j) ? 1 : 0;
+}
+
+int tempi_hip_copy_batch(const tempi_hip_copy_item *items, int n, void *stream) {
+  std::vector<CopyJob> groups[5];
+  for (int i = 0; i < n; ++i) {
+    CopyJob j;
+    if (!plan_copy(items[i].dst_first, items[i].src_first, &items[i].dst, &items[i].src, &j))
+      return int(hipErrorInvalidValue);
+    if (j.a.nwords == 0) continue;
+    const int wi = j.w == 1 ? 0 : j.w == 2 ? 1 : j.w == 4 ? 2 : j.w == 8 ? 3 : 4;
+    groups[wi].push_back(j);
+  }
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  for (int wi = 0; wi < 5; ++wi) {
+    if (groups[wi].empty()) continue;
+    int e = 0;
+    switch (wi) {
+    case 0: e = launch_copy_group<1>(groups[wi], s); break;
+    case 1: e = launch_copy_group<2>(groups[wi], s); break;
+    case 2: e = launch_copy_group<4>(groups[wi], s); break;
+    case 3: e = launch_copy_group<8>(groups[wi], s); break;
+    default: e = launch_copy_group<16>(groups[wi], s); break;
+    }
+    if (e) return e;
+  }
+  return 0;
+}
 
 int tempi_hip_pack(void *packed, const void *first, const tempi_hip_desc *d, void *stream) {
   Norm n;

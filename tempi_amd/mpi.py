@@ -39,7 +39,8 @@ class TypeInfo(ctypes.Structure):
 _COUNTER_FIELDS = [
     "packs", "unpacks", "pack_bytes", "unpack_bytes", "launches", "lib_packs", "lib_unpacks",
     "sends", "recvs", "isends", "irecvs", "send_device", "send_oneshot", "send_staged",
-    "send_ipc", "lib_sends", "lib_recvs",
+    "send_ipc", "lib_sends", "lib_recvs", "send_direct", "direct_fallbacks",
+    "neighbor_colls",
 ]
 
 
@@ -285,6 +286,62 @@ class MPI:
         self._call("MPI_Alltoallv", ctypes.c_void_p(sbuf), A(*scounts), A(*sdispls), self.h(stype),
                    ctypes.c_void_p(rbuf), A(*rcounts), A(*rdispls), self.h(rtype),
                    self.h(self.COMM_WORLD if comm is None else comm))
+
+    # ------------------------------------------------ topologies / neighbours
+    def Dist_graph_create_adjacent(self, sources, destinations, reorder=False, comm=None):
+        A = ctypes.c_int * max(len(sources), 1)
+        B = ctypes.c_int * max(len(destinations), 1)
+        out = self.Handle()
+        unweighted = ctypes.c_void_p(self.const("MPI_UNWEIGHTED"))
+        self._call("MPI_Dist_graph_create_adjacent", self.h(self.COMM_WORLD if comm is None else comm),
+                   len(sources), A(*sources), unweighted, len(destinations), B(*destinations), unweighted,
+                   self.h(self.const("MPI_INFO_NULL")), int(reorder), ctypes.byref(out))
+        return out.value
+
+    def Dist_graph_neighbors(self, comm, indeg, outdeg):
+        A = ctypes.c_int * max(indeg, 1)
+        B = ctypes.c_int * max(outdeg, 1)
+        s, d = A(), B()
+        unweighted = ctypes.c_void_p(self.const("MPI_UNWEIGHTED"))
+        self._call("MPI_Dist_graph_neighbors", self.h(comm), indeg, s, unweighted, outdeg, d, unweighted)
+        return list(s)[:indeg], list(d)[:outdeg]
+
+    def Cart_create(self, dims, periods, reorder=False, comm=None):
+        n = len(dims)
+        out = self.Handle()
+        self._call("MPI_Cart_create", self.h(self.COMM_WORLD if comm is None else comm), n,
+                   (ctypes.c_int * n)(*dims), (ctypes.c_int * n)(*[int(p) for p in periods]), int(reorder),
+                   ctypes.byref(out))
+        return out.value
+
+    def Cart_shift(self, comm, direction, disp=1):
+        lo, hi = ctypes.c_int(), ctypes.c_int()
+        self._call("MPI_Cart_shift", self.h(comm), direction, disp, ctypes.byref(lo), ctypes.byref(hi))
+        return lo.value, hi.value
+
+    def Comm_free(self, comm):
+        c = self.Handle(comm)
+        self._call("MPI_Comm_free", ctypes.byref(c))
+        return c.value
+
+    def Comm_dup(self, comm=None):
+        out = self.Handle()
+        self._call("MPI_Comm_dup", self.h(self.COMM_WORLD if comm is None else comm), ctypes.byref(out))
+        return out.value
+
+    def Neighbor_alltoallw(self, sbuf, scounts, sdispls, stypes, rbuf, rcounts, rdispls, rtypes, comm):
+        ns, nr = max(len(scounts), 1), max(len(rcounts), 1)
+        I, J = ctypes.c_int * ns, ctypes.c_int * nr
+        AS, AR = self.Aint * ns, self.Aint * nr
+        HS, HR = self.Handle * ns, self.Handle * nr
+        self._call("MPI_Neighbor_alltoallw", ctypes.c_void_p(sbuf), I(*scounts), AS(*sdispls), HS(*stypes),
+                   ctypes.c_void_p(rbuf), J(*rcounts), AR(*rdispls), HR(*rtypes), self.h(comm))
+
+    def Neighbor_alltoallv(self, sbuf, scounts, sdispls, stype, rbuf, rcounts, rdispls, rtype, comm):
+        ns, nr = max(len(scounts), 1), max(len(rcounts), 1)
+        I, J = ctypes.c_int * ns, ctypes.c_int * nr
+        self._call("MPI_Neighbor_alltoallv", ctypes.c_void_p(sbuf), I(*scounts), I(*sdispls), self.h(stype),
+                   ctypes.c_void_p(rbuf), J(*rcounts), J(*rdispls), self.h(rtype), self.h(comm))
 
     # --------------------------------------------------------------- TEMPI
     def describe(self, t):

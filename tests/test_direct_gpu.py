@@ -1,0 +1,285 @@
+"""Sends to the same process (DIRECT): the strided -> strided copy kernel
+(tempi_hip_copy_batch, include/tempi_hip.h) and the transport route built on
+it (p2p.cpp IsendDirectOp / IrecvOp), on the GPU.
+
+Oracle: oracle/typemap.c through pyoracle -- the destination must equal
+unpack(dst type, pack(src type, src)) over an untouched canvas, the MPI
+semantics of a message between two type maps of equal size
+(/root/reference/test/pack_unpack.cpp:61-97 checks the same identity against
+the library). Bit-exact.
+"""
+import ctypes
+import random
+
+import numpy as np
+import pytest
+
+from oracle import pyoracle
+from tests import typezoo
+from tests.test_pack_gpu import HipDesc, _random_recipe
+
+pytestmark = pytest.mark.gpu
+
+
+class CopyItem(ctypes.Structure):
+    _fields_ = [("dst_first", ctypes.c_void_p), ("src_first", ctypes.c_void_p), ("dst", HipDesc),
+                ("src", HipDesc)]
+
+
+def _hip():
+    import tempi_amd
+
+    H = ctypes.CDLL(tempi_amd.LIBTEMPI_HIP)
+    H.tempi_hip_copy_batch.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+    H.tempi_hip_copy_supported.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(HipDesc),
+                                           ctypes.POINTER(HipDesc)]
+    return H
+
+
+def _flat(mpi, recipe, count):
+    t, temps, basic = typezoo.build(mpi, recipe)
+    d = mpi.describe(t)
+    typezoo.free(mpi, t, temps, basic)
+    dims = ([(count, d["extent"])] if count > 1 else []) + list(zip(d["counts"], d["strides"]))
+    desc = HipDesc()
+    desc.block = d["block"]
+    desc.ndims = len(dims)
+    for j, (cn, st) in enumerate(dims):
+        desc.counts[j] = cn
+        desc.strides[j] = st
+    return d, desc, len(dims) <= 5
+
+
+def _reshape(rng, size):
+    """a byte layout of exactly `size` bytes with another shape"""
+    divs = [b for b in (1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 64, 128, 512, 4096) if size % b == 0 and size // b < 200000]
+    bl = rng.choice(divs or [size])
+    nb = size // bl
+    if rng.random() < 0.5 or nb < 4:
+        return f"vector({nb},{bl},{bl + rng.choice([0, 1, 8, 16, bl])},byte)", 1
+    for z in (2, 3, 4, 5, 7):
+        if nb % z == 0:
+            y = nb // z
+            return f"subarray(C,[{z + 1},{y + 2},{bl + 24}],[{z},{y},{bl}],[1,{rng.randrange(3)},{rng.choice([0, 3, 8, 24])}],byte)", 1
+    return f"vector({nb},{bl},{2 * bl},byte)", 1
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_copy_kernel_c_abi(mpi, gpu, seed):
+    """tempi_hip_copy_batch: 1-60 (src, dst) pairs of equal size -- same shape
+    at other offsets (the halo case), or a different shape entirely -- mixed
+    word widths and ranks in one call; the canvas outside each dst type map
+    stays untouched."""
+    import torch
+
+    H = _hip()
+    rng = random.Random(seed)
+    n = rng.choice([1, 5, 24, 60])
+    cases = []
+    for i in range(n):
+        srecipe, scount = _random_recipe(rng), rng.choice([1, 1, 2])
+        stm = pyoracle.TypeMap(srecipe)
+        size = stm.size * scount
+        if size == 0:
+            continue
+        if rng.random() < 0.4:
+            drecipe, dcount = srecipe, scount
+        else:
+            drecipe, dcount = _reshape(rng, size)
+        dtm = pyoracle.TypeMap(drecipe)
+        if dtm.size * dcount != size:
+            continue
+        sd, sdesc, sok = _flat(mpi, srecipe, scount)
+        dd, ddesc, dok = _flat(mpi, drecipe, dcount)
+        if not (sok and dok):
+            continue
+        so, slen = stm.geometry(scount)
+        do, dlen = dtm.geometry(dcount)
+        sshift, dshift = rng.choice([0, 0, 8, 3]), rng.choice([0, 0, 8, 5])
+        sh = np.random.default_rng(seed * 977 + i).integers(0, 256, slen + sshift, dtype=np.uint8)
+        canvas = np.random.default_rng(seed * 1931 + i).integers(0, 256, dlen + dshift, dtype=np.uint8)
+        src = torch.from_numpy(sh).to(gpu)
+        dst = torch.from_numpy(canvas).to(gpu)
+        it = CopyItem()
+        it.src_first = src.data_ptr() + so + sshift + sd["start"]
+        it.dst_first = dst.data_ptr() + do + dshift + dd["start"]
+        it.src, it.dst = sdesc, ddesc
+        ok = H.tempi_hip_copy_supported(it.dst_first, it.src_first, ctypes.byref(it.dst), ctypes.byref(it.src))
+        if not ok:
+            continue
+        exp = canvas.copy()
+        dtm.unpack(stm.pack(sh, so + sshift, scount), exp, do + dshift, dcount)
+        cases.append((it, src, dst, exp, srecipe, drecipe))
+    if not cases:
+        pytest.skip("no supported pair drawn")
+    items = (CopyItem * len(cases))(*[c[0] for c in cases])
+    torch.cuda.synchronize()
+    assert H.tempi_hip_copy_batch(items, len(cases), None) == 0
+    torch.cuda.synchronize()
+    for it, src, dst, exp, sr, dr in cases:
+        assert np.array_equal(dst.cpu().numpy(), exp), f"{sr} -> {dr}"
+
+
+def test_copy_unsupported_and_size_mismatch(mpi, gpu):
+    """> 3 dims a side after normalisation, or unequal byte counts: refused
+    (the transport then packs + unpacks instead)."""
+    import torch
+
+    H = _hip()
+    buf = torch.zeros(1 << 16, dtype=torch.uint8, device=gpu)
+    deep = HipDesc()
+    deep.block, deep.ndims = 1, 4
+    for k, (c, s) in enumerate([(2, 4096), (2, 1024), (2, 256), (2, 16)]):
+        deep.counts[k], deep.strides[k] = c, s
+    flat = HipDesc()
+    flat.block, flat.ndims = 16, 0
+    p = buf.data_ptr()
+    assert H.tempi_hip_copy_supported(p, p + 8192, ctypes.byref(flat), ctypes.byref(deep)) == 0
+    three = HipDesc()
+    three.block, three.ndims = 2, 3
+    for k, (c, s) in enumerate([(2, 1024), (2, 256), (2, 16)]):
+        three.counts[k], three.strides[k] = c, s
+    assert H.tempi_hip_copy_supported(p, p + 8192, ctypes.byref(flat), ctypes.byref(three)) == 1
+    flat.block = 15
+    assert H.tempi_hip_copy_supported(p, p + 8192, ctypes.byref(flat), ctypes.byref(three)) == 0
+    it = CopyItem(p, p + 8192, flat, three)
+    assert H.tempi_hip_copy_batch(ctypes.byref(it), 1, None) != 0
+
+
+SELF_RECIPES = [
+    ("subarray(C,[40,38,512],[30,3,24],[5,3,24],byte)", 2),  # halo x-face shape
+    ("subarray(C,[20,30,600],[3,24,512],[2,3,24],byte)", 1),  # y-face, 8-byte aligned rows
+    ("vector(1024,512,1024,byte)", 1),
+    ("vector(300,3,7,byte)", 2),
+    ("hvector(5,1,53,hvector(3,1,16,contig(13,byte)))", 3),
+]
+
+
+def _setup(mpi, gpu, recipe, count, seed):
+    import torch
+
+    tm = pyoracle.TypeMap(recipe)
+    origin, buflen = tm.geometry(count)
+    t, temps, basic = typezoo.build(mpi, recipe)
+    sh = np.random.default_rng(seed).integers(0, 256, buflen, dtype=np.uint8)
+    canvas = np.random.default_rng(seed + 1).integers(0, 256, buflen, dtype=np.uint8)
+    exp = canvas.copy()
+    tm.unpack(tm.pack(sh, origin, count), exp, origin, count)
+    src = torch.from_numpy(sh).to(gpu)
+    dst = torch.from_numpy(canvas).to(gpu)
+    torch.cuda.synchronize()
+    return tm, origin, (t, temps, basic), src, dst, exp
+
+
+@pytest.mark.parametrize("recipe,count", SELF_RECIPES)
+def test_self_isend_irecv_direct(mpi, gpu, recipe, count):
+    """Irecv posted, Isend to self, Waitall: one strided -> strided copy, no
+    pack, no fallback."""
+    tm, origin, tt, src, dst, exp = _setup(mpi, gpu, recipe, count, 11)
+    t = tt[0]
+    try:
+        before = mpi.counters()
+        r = mpi.Irecv(dst.data_ptr() + origin, count, t, 0, 5)
+        s = mpi.Isend(src.data_ptr() + origin, count, t, 0, 5)
+        assert mpi.Waitall([s, r]) == [mpi.REQUEST_NULL] * 2
+        after = mpi.counters()
+        assert after["send_direct"] == before["send_direct"] + 1
+        assert after["direct_fallbacks"] == before["direct_fallbacks"]
+        assert np.array_equal(dst.cpu().numpy(), exp)
+    finally:
+        typezoo.free(mpi, *tt)
+
+
+@pytest.mark.parametrize("recipe,count", SELF_RECIPES[:3])
+def test_self_send_waited_before_receive(mpi, gpu, recipe, count):
+    """Isend to self and Wait on it before the Irecv exists: the send gathers
+    into a slab and completes; the later receive unpacks that slab."""
+    tm, origin, tt, src, dst, exp = _setup(mpi, gpu, recipe, count, 21)
+    t = tt[0]
+    try:
+        before = mpi.counters()
+        s = mpi.Isend(src.data_ptr() + origin, count, t, 0, 6)
+        assert mpi.Wait(s) == mpi.REQUEST_NULL
+        src.zero_()  # the send is complete: the buffer may be reused
+        import torch
+
+        torch.cuda.synchronize()
+        r = mpi.Irecv(dst.data_ptr() + origin, count, t, 0, 6)
+        assert mpi.Wait(r) == mpi.REQUEST_NULL
+        after = mpi.counters()
+        assert after["direct_fallbacks"] == before["direct_fallbacks"] + 1
+        assert np.array_equal(dst.cpu().numpy(), exp)
+    finally:
+        typezoo.free(mpi, *tt)
+
+
+def test_self_direct_other_shape_and_test_loop(mpi, gpu):
+    """The receive type differs from the send type (same size): the copy maps
+    one shape onto the other; completion is polled with MPI_Test."""
+    import torch
+
+    srecipe, drecipe = "subarray(C,[40,38,512],[30,3,24],[5,3,24],byte)", "vector(30,24,100,byte)"
+    stm, dtm = pyoracle.TypeMap(srecipe), pyoracle.TypeMap(drecipe)
+    dcount = stm.size // dtm.size
+    so, slen = stm.geometry(1)
+    do, dlen = dtm.geometry(dcount)
+    st_ = typezoo.build(mpi, srecipe)
+    dt_ = typezoo.build(mpi, drecipe)
+    try:
+        sh = np.random.default_rng(3).integers(0, 256, slen, dtype=np.uint8)
+        canvas = np.random.default_rng(4).integers(0, 256, dlen, dtype=np.uint8)
+        assert dcount == 3 and dcount * dtm.size == stm.size
+        exp = canvas.copy()
+        dtm.unpack(stm.pack(sh, so, 1), exp, do, dcount)
+        src, dst = torch.from_numpy(sh).to(gpu), torch.from_numpy(canvas).to(gpu)
+        torch.cuda.synchronize()
+        r = mpi.Irecv(dst.data_ptr() + do, dcount, dt_[0], 0, 7)
+        s = mpi.Isend(src.data_ptr() + so, 1, st_[0], 0, 7)
+        for req in (r, s):
+            done = False
+            while not done:
+                done, req = mpi.Test(req)
+        assert np.array_equal(dst.cpu().numpy(), exp)
+    finally:
+        typezoo.free(mpi, *st_)
+        typezoo.free(mpi, *dt_)
+
+
+def test_self_direct_into_library_receives(mpi, gpu):
+    """A direct descriptor landing in receives that cannot copy in place: a
+    blocking MPI_Recv into host memory, and a device receive of a type TEMPI
+    does not pack (library path) -- both fetch the sender's bytes."""
+    import torch
+
+    recipe, count = "vector(300,3,7,byte)", 2
+    tm, origin, tt, src, dst, exp = _setup(mpi, gpu, recipe, count, 31)
+    t = tt[0]
+    try:
+        host = np.random.default_rng(32).integers(0, 256, exp.size, dtype=np.uint8)
+        hexp = host.copy()
+        sh = src.cpu().numpy()
+        tm.unpack(tm.pack(sh, origin, count), hexp, origin, count)
+        s = mpi.Isend(src.data_ptr() + origin, count, t, 0, 8)
+        mpi.Recv(host.ctypes.data + origin, count, t, 0, 8)
+        assert mpi.Wait(s) == mpi.REQUEST_NULL
+        assert np.array_equal(host, hexp)
+        # irregular receive type (library-packed) of the same size: 1800 bytes
+        irr = "hindexed([700,1100],[0,1000],byte)"
+        itm = pyoracle.TypeMap(irr)
+        assert itm.size == tm.size * count
+        io, ilen = itm.geometry(1)
+        it_ = typezoo.build(mpi, irr)
+        try:
+            canvas = np.random.default_rng(33).integers(0, 256, ilen, dtype=np.uint8)
+            iexp = canvas.copy()
+            itm.unpack(tm.pack(sh, origin, count), iexp, io, 1)
+            idst = torch.from_numpy(canvas).to(gpu)
+            torch.cuda.synchronize()
+            r = mpi.Irecv(idst.data_ptr() + io, 1, it_[0], 0, 9)
+            s = mpi.Isend(src.data_ptr() + origin, count, t, 0, 9)
+            mpi.Waitall([r, s])
+            assert np.array_equal(idst.cpu().numpy(), iexp)
+        finally:
+            typezoo.free(mpi, *it_)
+    finally:
+        typezoo.free(mpi, *tt)

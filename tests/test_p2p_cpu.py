@@ -18,6 +18,15 @@ def test_alltoallv_host(ranks, nnz):
     assert rc == 0 and "RESULT errors=0" in out, out[-3000:]
 
 
+@pytest.mark.parametrize("ranks", [1, 2, 3, 4])
+def test_neighbor_collectives_host(ranks):
+    """MPI_Neighbor_alltoallw (dist graph with self / repeated edges) and
+    MPI_Neighbor_alltoallv (periodic Cartesian) through libtempi on host
+    buffers, against oracle/typemap.c."""
+    rc, out = mpi_launch.run(ranks, mpi_launch.py("neighbor.py"), timeout=180)
+    assert rc == 0 and "RESULT errors=0" in out, out[-3000:]
+
+
 def test_mpi_under_torchrun():
     """bench.py's multi-GPU launch is torch.distributed.run, not mpiexec: the
     ranks are wired into one MPI job by tempi_amd.pmi (PMI-1 server)."""

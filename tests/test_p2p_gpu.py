@@ -46,11 +46,14 @@ def test_pingpong_nd(gpu, method, total, block):
     assert rc == 0 and r["errors"] == 0, out[-3000:]
 
 
-@pytest.mark.parametrize("ranks,grid,env", [(1, "48", {}), (2, "48", {}), (4, "40", {}), (3, "30", {}),
-                                           (1, "128", {}), (2, "40", {"TEMPI_FAULT_IPC_OPEN": "1"}),
-                                           (4, "32", {"TEMPI_DATATYPE_ONESHOT": "1"})])
-def test_halo_exchange_content(gpu, ranks, grid, env):
-    rc, out = mpi_launch.run(ranks, [os.path.join(LIB, "halo_exchange"), "2", grid, "--quants", "2", "--check"],
+@pytest.mark.parametrize("ranks,grid,env,extra", [
+    (1, "48", {}, []), (2, "48", {}, []), (4, "40", {}, []), (3, "30", {}, []), (1, "128", {}, []),
+    (1, "48", {"TEMPI_NO_DIRECT": "1"}, []), (2, "40", {"TEMPI_FAULT_IPC_OPEN": "1"}, []),
+    (4, "32", {"TEMPI_DATATYPE_ONESHOT": "1"}, []),
+    (1, "48", {}, ["--neighbor"]), (2, "40", {}, ["--neighbor"]), (4, "32", {}, ["--neighbor"]),
+    (3, "30", {}, ["--neighbor"])])
+def test_halo_exchange_content(gpu, ranks, grid, env, extra):
+    rc, out = mpi_launch.run(ranks, [os.path.join(LIB, "halo_exchange"), "2", grid, "--quants", "2", "--check"] + extra,
                              env=env, timeout=300)
     r = _json_line(out)
     assert rc == 0 and r["checked"] and r["errors"] == 0, out[-3000:]
@@ -65,4 +68,14 @@ A2AV = {"AUTO": {}, "STAGED": {"TEMPI_ALLTOALLV_STAGED": "1"}, "ISIR_STAGED": {"
 def test_alltoallv_device(gpu, method, ranks, scale, nnz):
     rc, out = mpi_launch.run(ranks, mpi_launch.py("alltoallv.py", "--device", "--scale", str(scale), "--nnz",
                                                   str(nnz)), env=A2AV[method], timeout=240)
+    assert rc == 0 and "RESULT errors=0" in out, out[-3000:]
+
+
+@pytest.mark.parametrize("ranks,env", [(1, {}), (2, {}), (3, {}), (4, {}), (2, {"TEMPI_DATATYPE_ONESHOT": "1"}),
+                                       (3, {"TEMPI_NO_DIRECT": "1"})])
+def test_neighbor_collectives_device(gpu, ranks, env):
+    """MPI_Neighbor_alltoallw / _alltoallv on device buffers: TEMPI's per-edge
+    route, checked against the oracle and the library's own result on host
+    copies."""
+    rc, out = mpi_launch.run(ranks, mpi_launch.py("neighbor.py", "--device"), env=env, timeout=240)
     assert rc == 0 and "RESULT errors=0" in out, out[-3000:]

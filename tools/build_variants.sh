@@ -1,8 +1,10 @@
 #!/bin/bash
-# Build libtempi_hip.so tuning variants into tools/_variants/ and kbench.
+# Build libtempi_hip.so tuning variants into tools/_variants/ plus the kernel
+# benches (kbench: pack/unpack shapes, hbench: halo regions incl. the copy).
 set -e
 cd "$(dirname "$0")/.."
 mkdir -p tools/_variants
+rm -f tools/_variants/*.so
 build() { # name flags...
   local name=$1; shift
   hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Iinclude "$@" \
@@ -10,8 +12,9 @@ build() { # name flags...
     -Wl,-rpath,/opt/rocm/lib &
 }
 build cur
-build u8_1 -DTEMPI_UNROLL_WIDE=1
-build u16_2 -DTEMPI_UNROLL_16=2
+build cu2 -DTEMPI_COPY_U=2
+build cu4 -DTEMPI_COPY_U=4
 wait
 g++ -O2 -std=c++17 -Iinclude -o tools/_variants/kbench tools/kbench.cpp -ldl
+g++ -O2 -std=c++17 -Iinclude -o tools/_variants/hbench tools/hbench.cpp -ldl
 ls tools/_variants

@@ -1,0 +1,169 @@
+// tools/hbench.cpp -- halo-region kernel microbenchmark (config 4 shapes).
+//
+// usage: hbench LIB.so REPS [LCR] [QUANTS]
+// One rank's buffers of the 512^3 halo exchange (LCR^3 cells + radius 3, 8-byte
+// quantities, pitch rounded to 512 B, /root/reference/bin/bench_halo_exchange.cpp:
+// 727-733). For each class of region (x / y / z faces, edges, corners, all 26)
+// it times, with HIP events over REPS back-to-back batched launches:
+//   pack   interior(d) -> packed slab            (tempi_hip_pack_batch)
+//   unpack packed slab  -> exterior(-d)          (tempi_hip_unpack_batch)
+//   copy   interior(d)  -> exterior(-d) directly (tempi_hip_copy_batch)
+// over QUANTS buffers, and prints one JSON line per class with the kernel time
+// and the algorithmic GB/s (2 x payload per launch set).
+#include "tempi_hip.h"
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <dlfcn.h>
+#include <string>
+#include <vector>
+
+#define SYM(name)                                                                                  \
+  auto name = reinterpret_cast<decltype(&::name)>(dlsym(h, #name));                               \
+  if (!name) {                                                                                     \
+    std::fprintf(stderr, "missing %s\n", #name);                                                   \
+    return 2;                                                                                      \
+  }
+#define CK(x)                                                                                      \
+  do {                                                                                             \
+    int e_ = (x);                                                                                  \
+    if (e_) {                                                                                      \
+      std::fprintf(stderr, "%s: error %d\n", #x, e_);                                              \
+      return 3;                                                                                    \
+    }                                                                                              \
+  } while (0)
+
+struct Region {
+  int dx, dy, dz;
+  tempi_hip_desc desc;
+  long long srcOff, dstOff, bytes;
+};
+
+int main(int argc, char **argv) {
+  if (argc < 3) {
+    std::fprintf(stderr, "usage: %s LIB REPS [LCR] [QUANTS]\n", argv[0]);
+    return 1;
+  }
+  void *h = dlopen(argv[1], RTLD_NOW | RTLD_LOCAL);
+  if (!h) {
+    std::fprintf(stderr, "dlopen: %s\n", dlerror());
+    return 2;
+  }
+  SYM(tempi_hip_pack_batch) SYM(tempi_hip_unpack_batch) SYM(tempi_hip_copy_batch) SYM(tempi_hip_malloc)
+  SYM(tempi_hip_stream_create) SYM(tempi_hip_event_create) SYM(tempi_hip_event_record)
+  SYM(tempi_hip_event_synchronize) SYM(tempi_hip_event_elapsed_ms) SYM(tempi_hip_memset_async)
+  SYM(tempi_hip_stream_synchronize)
+  const int reps = std::atoi(argv[2]);
+  const int l = argc > 3 ? std::atoi(argv[3]) : 512;
+  const int nq = argc > 4 ? std::atoi(argv[4]) : 8;
+  const int r = 3, q = 8;
+  const long long width = (l + 2LL * r) * q, pitch = (width + 511) / 512 * 512;
+  const long long ysize = l + 2 * r, zsize = l + 2 * r;
+  const long long plane = pitch * ysize, bufBytes = plane * zsize;
+
+  std::vector<Region> regions;
+  for (int dz = -1; dz <= 1; ++dz)
+    for (int dy = -1; dy <= 1; ++dy)
+      for (int dx = -1; dx <= 1; ++dx) {
+        if (!dx && !dy && !dz) continue;
+        const int d[3] = {dx, dy, dz};
+        long long pin[3], pex[3], e[3];
+        for (int k = 0; k < 3; ++k) {
+          pin[k] = d[k] == -1 ? r : d[k] == 1 ? l : r;
+          // the exterior on the OPPOSITE side receives interior(d)
+          pex[k] = -d[k] == -1 ? 0 : -d[k] == 1 ? l + r : r;
+          e[k] = d[k] == 0 ? l : r;
+        }
+        Region R{dx, dy, dz, {}, 0, 0, 0};
+        R.desc.block = e[0] * q;
+        R.desc.ndims = 2;
+        R.desc.counts[0] = e[2];
+        R.desc.strides[0] = plane;
+        R.desc.counts[1] = e[1];
+        R.desc.strides[1] = pitch;
+        R.srcOff = pin[2] * plane + pin[1] * pitch + pin[0] * q;
+        R.dstOff = pex[2] * plane + pex[1] * pitch + pex[0] * q;
+        R.bytes = e[0] * e[1] * e[2] * q;
+        regions.push_back(R);
+      }
+
+  std::vector<char *> bufs(static_cast<size_t>(nq), nullptr);
+  void *s, *e0, *e1;
+  CK(tempi_hip_stream_create(&s));
+  CK(tempi_hip_event_create(&e0, 1));
+  CK(tempi_hip_event_create(&e1, 1));
+  for (auto &b : bufs) {
+    void *p;
+    CK(tempi_hip_malloc(&p, size_t(bufBytes)));
+    CK(tempi_hip_memset_async(p, 1, size_t(bufBytes), s));
+    b = static_cast<char *>(p);
+  }
+  long long slabBytes = 0;
+  for (const Region &R : regions) slabBytes += (R.bytes + 255) / 256 * 256;
+  void *slab;
+  CK(tempi_hip_malloc(&slab, size_t(slabBytes * nq)));
+  CK(tempi_hip_stream_synchronize(s));
+
+
+  struct Cls {
+    const char *name;
+    bool (*pick)(const Region &);
+  };
+  const Cls classes[] = {
+      {"x_faces", [](const Region &R) { return R.dx != 0 && !R.dy && !R.dz; }},
+      {"y_faces", [](const Region &R) { return !R.dx && R.dy != 0 && !R.dz; }},
+      {"z_faces", [](const Region &R) { return !R.dx && !R.dy && R.dz != 0; }},
+      {"edges", [](const Region &R) { return (R.dx != 0) + (R.dy != 0) + (R.dz != 0) == 2; }},
+      {"corners", [](const Region &R) { return R.dx != 0 && R.dy != 0 && R.dz != 0; }},
+      {"all26", [](const Region &) { return true; }},
+  };
+
+  for (const Cls &c : classes) {
+    std::vector<tempi_hip_batch_item> pk, up;
+    std::vector<tempi_hip_copy_item> cp;
+    long long payload = 0, off = 0;
+    for (int qi = 0; qi < nq; ++qi)
+      for (const Region &R : regions) {
+        if (!c.pick(R)) continue;
+        char *packed = static_cast<char *>(slab) + off;
+        off += (R.bytes + 255) / 256 * 256;
+        payload += R.bytes;
+        tempi_hip_batch_item a{}, b{};
+        tempi_hip_copy_item cc{};
+        a.packed = b.packed = packed;
+        a.first = bufs[size_t(qi)] + R.srcOff;
+        b.first = bufs[size_t(qi)] + R.dstOff;
+        a.desc = b.desc = cc.dst = cc.src = R.desc;
+        cc.dst_first = b.first;
+        cc.src_first = a.first;
+        pk.push_back(a);
+        up.push_back(b);
+        cp.push_back(cc);
+      }
+    float ms[3];
+    for (int mode = 0; mode < 3; ++mode) {
+      auto run = [&]() -> int {
+        if (mode == 0) return tempi_hip_pack_batch(pk.data(), int(pk.size()), s);
+        if (mode == 1) return tempi_hip_unpack_batch(up.data(), int(up.size()), s);
+        return tempi_hip_copy_batch(cp.data(), int(cp.size()), s);
+      };
+      CK(run());
+      CK(run());
+      CK(tempi_hip_event_record(e0, s));
+      for (int i = 0; i < reps; ++i) CK(run());
+      CK(tempi_hip_event_record(e1, s));
+      CK(tempi_hip_event_synchronize(e1));
+      CK(tempi_hip_event_elapsed_ms(&ms[mode], e0, e1));
+      ms[mode] /= float(reps);
+    }
+    auto gbs = [&](float m) { return 2.0 * double(payload) / (double(m) * 1e-3) / 1e9; };
+    std::printf("{\"lib\": \"%s\", \"class\": \"%s\", \"items\": %zu, \"payload\": %lld, \"pack_us\": %.1f, "
+                "\"unpack_us\": %.1f, \"copy_us\": %.1f, \"pack_gbs\": %.1f, \"unpack_gbs\": %.1f, "
+                "\"copy_gbs\": %.1f}\n",
+                argv[1], c.name, cp.size(), payload, ms[0] * 1e3, ms[1] * 1e3, ms[2] * 1e3, gbs(ms[0]), gbs(ms[1]),
+                gbs(ms[2]));
+    std::fflush(stdout);
+  }
+  return 0;
+}
