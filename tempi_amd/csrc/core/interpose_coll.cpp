@@ -100,8 +100,9 @@ int isir(const void *sendbuf, const int *scounts, const int *sdispls, MPI_Dataty
     if (rcounts[p] > 0) {
       MPI_Request r;
       char *b = static_cast<char *>(recvbuf) + int64_t(rdispls[p]) * rext;
-      if (p2p::handles(b, rcounts[p], rtype, p))
-        p2p::irecv(b, rcounts[p], rtype, p, tag, comm, &r);
+      p2p::Route route;
+      if (p2p::handles(b, rcounts[p], rtype, p, &route))
+        p2p::irecv(b, rcounts[p], rtype, p, tag, comm, &r, route);
       else
         next.MPI_Irecv(b, rcounts[p], rtype, p, tag, comm, &r);
       reqs.push_back(r);
@@ -111,8 +112,9 @@ int isir(const void *sendbuf, const int *scounts, const int *sdispls, MPI_Dataty
       MPI_Request r;
       const char *b = static_cast<const char *>(sendbuf) + int64_t(sdispls[p]) * sext;
       const int force = topology::colocated(comm, p) ? local : remote;
-      if (p2p::handles(b, scounts[p], stype, p))
-        p2p::isend(b, scounts[p], stype, p, tag, comm, &r, force);
+      p2p::Route route;
+      if (p2p::handles(b, scounts[p], stype, p, &route))
+        p2p::isend(b, scounts[p], stype, p, tag, comm, &r, route, force);
       else
         next.MPI_Isend(b, scounts[p], stype, p, tag, comm, &r);
       reqs.push_back(r);

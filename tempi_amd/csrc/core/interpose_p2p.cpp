@@ -21,13 +21,14 @@ using namespace tempi;
 TEMPI_EXPORT int MPI_Send(const void *buf, int count, MPI_Datatype datatype, int dest, int tag,
                           MPI_Comm comm) {
   resolve_next();
-  if (!p2p::handles(buf, count, datatype, dest)) {
+  p2p::Route route;
+  if (!p2p::handles(buf, count, datatype, dest, &route)) {
     counters.lib_sends++;
     return next.MPI_Send(buf, count, datatype, dest, tag, comm);
   }
   counters.sends++;
   MPI_Request r;
-  int rc = p2p::isend(buf, count, datatype, dest, tag, comm, &r, -1, /*blocking=*/true);
+  int rc = p2p::isend(buf, count, datatype, dest, tag, comm, &r, route, -1, /*blocking=*/true);
   if (rc != MPI_SUCCESS) return rc;
   return p2p::wait(&r, MPI_STATUS_IGNORE);
 }
@@ -35,10 +36,11 @@ TEMPI_EXPORT int MPI_Send(const void *buf, int count, MPI_Datatype datatype, int
 TEMPI_EXPORT int MPI_Recv(void *buf, int count, MPI_Datatype datatype, int source, int tag, MPI_Comm comm,
                           MPI_Status *status) {
   resolve_next();
-  if (p2p::handles(buf, count, datatype, source)) {
+  p2p::Route route;
+  if (p2p::handles(buf, count, datatype, source, &route)) {
     counters.recvs++;
     MPI_Request r;
-    int rc = p2p::irecv(buf, count, datatype, source, tag, comm, &r);
+    int rc = p2p::irecv(buf, count, datatype, source, tag, comm, &r, route);
     if (rc != MPI_SUCCESS) return rc;
     return p2p::wait(&r, status);
   }
@@ -52,8 +54,9 @@ TEMPI_EXPORT int MPI_Recv(void *buf, int count, MPI_Datatype datatype, int sourc
 TEMPI_EXPORT int MPI_Isend(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm,
                            MPI_Request *request) {
   resolve_next();
-  if (p2p::handles(buf, count, datatype, dest))
-    return p2p::isend(buf, count, datatype, dest, tag, comm, request);
+  p2p::Route route;
+  if (p2p::handles(buf, count, datatype, dest, &route))
+    return p2p::isend(buf, count, datatype, dest, tag, comm, request, route);
   if (state.active) p2p::progress(false);
   counters.lib_sends++;
   return next.MPI_Isend(buf, count, datatype, dest, tag, comm, request);
@@ -62,8 +65,9 @@ TEMPI_EXPORT int MPI_Isend(const void *buf, int count, MPI_Datatype datatype, in
 TEMPI_EXPORT int MPI_Irecv(void *buf, int count, MPI_Datatype datatype, int source, int tag, MPI_Comm comm,
                            MPI_Request *request) {
   resolve_next();
-  if (p2p::handles(buf, count, datatype, source))
-    return p2p::irecv(buf, count, datatype, source, tag, comm, request);
+  p2p::Route route;
+  if (p2p::handles(buf, count, datatype, source, &route))
+    return p2p::irecv(buf, count, datatype, source, tag, comm, request, route);
   if (state.active) p2p::progress(false);
   counters.lib_recvs++;
   return next.MPI_Irecv(buf, count, datatype, source, tag, comm, request);

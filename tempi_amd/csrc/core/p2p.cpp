@@ -19,6 +19,7 @@
 #include <deque>
 #include <map>
 #include <tuple>
+#include <unordered_map>
 #include <memory>
 #include <unistd.h>
 #include <vector>
@@ -267,59 +268,99 @@ void watch(Op *op) {
   }
 }
 
-// GPU work waiting for the next flush: gathers of Isends, scatters of Irecvs
-struct Pending {
-  Op *op;
+// GPU work waiting for the next flush: gathers of Isends, scatters and direct
+// copies of Irecvs. Flat arrays (no per-message allocation); one launch per
+// (kind, word width, rank) group and device at flush time.
+struct PendingList {
+  std::vector<Op *> ops;
   std::vector<tempi_hip_batch_item> items;
+  std::vector<int> itemDev;
   std::vector<tempi_hip_copy_item> copies; // direct: strided -> strided (unpack list only)
-  void *copyDst = nullptr, *copySrc = nullptr; // STAGED: D2H copy after the pack
-  size_t copyBytes = 0;
+  std::vector<int> copyDev;
+  struct Stage { // STAGED: D2H copy after the packs
+    void *dst;
+    const void *src;
+    size_t n;
+    int dev;
+  };
+  std::vector<Stage> stages;
+  bool empty() const { return ops.empty(); }
+  size_t size() const { return ops.size(); }
+  void clear() {
+    ops.clear();
+    items.clear();
+    itemDev.clear();
+    copies.clear();
+    copyDev.clear();
+    stages.clear();
+  }
+  void add_items(const Op *op, const Packer &pk, void *packed, const void *origin, int64_t count) {
+    pk.items(packed, origin, count, items);
+    itemDev.resize(items.size(), op->device);
+  }
+  void add_copy(const Op *op, const tempi_hip_copy_item &c) {
+    copies.push_back(c);
+    copyDev.push_back(op->device);
+  }
+  void queue(Op *op) {
+    op->queued = true;
+    ops.push_back(op);
+  }
 };
-std::vector<Pending> pendingPack, pendingUnpack;
+PendingList pendingPack, pendingUnpack;
 constexpr size_t kMaxPending = 512;
 constexpr size_t kEarlyFlush = 16;
 
-void flush_list(std::vector<Pending> &list, bool pack) {
+template <typename T> const T *select(const std::vector<T> &v, const std::vector<int> &dev, int d, bool all,
+                                      std::vector<T> &tmp) {
+  if (all) return v.data();
+  tmp.clear();
+  for (size_t i = 0; i < v.size(); ++i)
+    if (dev[i] == d) tmp.push_back(v[i]);
+  return tmp.data();
+}
+
+void flush_list(PendingList &list, bool pack) {
   if (list.empty()) return;
   ScopedNs timer(counters.ns_flush);
   // group by device (almost always one)
-  std::vector<int> devices;
-  for (const Pending &p : list)
-    if (std::find(devices.begin(), devices.end(), p.op->device) == devices.end()) devices.push_back(p.op->device);
-  for (int dev : devices) {
-    std::vector<tempi_hip_batch_item> items;
-    for (const Pending &p : list)
-      if (p.op->device == dev) items.insert(items.end(), p.items.begin(), p.items.end());
+  int devices[64];
+  int ndev = 0;
+  for (const Op *op : list.ops) {
+    int k = 0;
+    while (k < ndev && devices[k] != op->device) ++k;
+    if (k == ndev && ndev < 64) devices[ndev++] = op->device;
+  }
+  const bool all = ndev == 1;
+  std::vector<tempi_hip_batch_item> itmp;
+  std::vector<tempi_hip_copy_item> ctmp;
+  for (int di = 0; di < ndev; ++di) {
+    const int dev = devices[di];
+    const tempi_hip_batch_item *items = select(list.items, list.itemDev, dev, all, itmp);
+    const size_t nitems = all ? list.items.size() : itmp.size();
+    const tempi_hip_copy_item *copies = select(list.copies, list.copyDev, dev, all, ctmp);
+    const size_t ncopies = all ? list.copies.size() : ctmp.size();
     void *s = gpu::stream(dev);
     int cur = 0;
     tempi_hip_get_device(&cur);
     if (cur != dev) tempi_hip_set_device(dev);
     counters.batches++;
-    counters.batched_items += items.size();
-    gpu::check(pack ? tempi_hip_pack_batch(items.data(), int(items.size()), s)
-                    : tempi_hip_unpack_batch(items.data(), int(items.size()), s),
-               pack ? "batched pack" : "batched unpack");
-    if (!pack) {
-      std::vector<tempi_hip_copy_item> copies;
-      for (const Pending &p : list)
-        if (p.op->device == dev) copies.insert(copies.end(), p.copies.begin(), p.copies.end());
-      if (!copies.empty()) {
-        counters.batched_items += copies.size();
-        gpu::check(tempi_hip_copy_batch(copies.data(), int(copies.size()), s), "batched direct copy");
-      }
-    }
-    for (const Pending &p : list)
-      if (p.op->device == dev && p.copyBytes)
-        gpu::check(tempi_hip_memcpy_async(p.copyDst, p.copySrc, p.copyBytes, s), "staged D2H");
+    counters.batched_items += nitems + ncopies;
+    if (nitems)
+      gpu::check(pack ? tempi_hip_pack_batch(items, int(nitems), s) : tempi_hip_unpack_batch(items, int(nitems), s),
+                 pack ? "batched pack" : "batched unpack");
+    if (ncopies) gpu::check(tempi_hip_copy_batch(copies, int(ncopies), s), "batched direct copy");
+    for (const PendingList::Stage &st : list.stages)
+      if (st.dev == dev) gpu::check(tempi_hip_memcpy_async(st.dst, st.src, st.n, s), "staged D2H");
     auto b = std::make_shared<GpuBatch>();
     b->device = dev;
     b->event = get_event();
     gpu::check(tempi_hip_event_record(b->event, s), "event record");
     if (cur != dev) tempi_hip_set_device(cur);
-    for (const Pending &p : list)
-      if (p.op->device == dev) {
-        p.op->queued = false;
-        b->ops.push_back(p.op);
+    for (Op *op : list.ops)
+      if (op->device == dev) {
+        op->queued = false;
+        b->ops.push_back(op);
       }
     batches.push_back(b);
   }
@@ -332,7 +373,7 @@ void flush() {
 }
 
 struct IsendOp : Op {
-  Packer packer;
+  RecordRef rec;      // the type (kept alive: MPI_Type_free may come first)
   const char *origin; // GPU-visible
   int count, dest, tag;
   MPI_Datatype dt;
@@ -342,27 +383,22 @@ struct IsendOp : Op {
   Slab *dslab = nullptr, *hslab = nullptr;
   IpcDesc desc{};
 
-  IsendOp(const TypeRecord &rec, const char *o, int c, MPI_Datatype d, int de, int t, MPI_Comm cm, int dev,
+  IsendOp(const TypeRecord *r, const char *o, int c, MPI_Datatype d, int de, int t, MPI_Comm cm, int dev,
           Method m, int64_t b)
-      : packer(rec.desc), origin(o), count(c), dest(de), tag(t), dt(d), comm(cm), method(m), bytes(b) {
+      : rec(r->ref()), origin(o), count(c), dest(de), tag(t), dt(d), comm(cm), method(m), bytes(b) {
     device = dev;
-    Pending p;
-    p.op = this;
     if (method == Method::ONESHOT) {
       hslab = pinned_pool().get(size_t(bytes), device);
-      packer.items(hslab->dev, origin, count, p.items);
+      pendingPack.add_items(this, *rec->packer, hslab->dev, origin, count);
     } else {
       dslab = device_pool().get(size_t(bytes), device);
-      packer.items(dslab->dev, origin, count, p.items);
+      pendingPack.add_items(this, *rec->packer, dslab->dev, origin, count);
       if (method == Method::STAGED) {
         hslab = pinned_pool().get(size_t(bytes), device);
-        p.copyDst = hslab->host;
-        p.copySrc = dslab->dev;
-        p.copyBytes = size_t(bytes);
+        pendingPack.stages.push_back({hslab->host, dslab->dev, size_t(bytes), device});
       }
     }
-    queued = true;
-    pendingPack.push_back(std::move(p));
+    pendingPack.queue(this);
   }
 
   void gpu_done() override { // packed: hand it to the library
@@ -418,7 +454,7 @@ struct IsendOp : Op {
 };
 
 struct IsendDirectOp : Op {
-  Packer packer;
+  RecordRef rec;
   const char *origin;
   int count;
   MPI_Datatype dt;
@@ -426,9 +462,9 @@ struct IsendDirectOp : Op {
   std::shared_ptr<DirectShared> sh;
   bool packDone = false;
 
-  IsendDirectOp(const TypeRecord &rec, const char *o, int c, MPI_Datatype d, int dest, int tag, MPI_Comm comm,
+  IsendDirectOp(const TypeRecord *r, const char *o, int c, MPI_Datatype d, int dest, int tag, MPI_Comm comm,
                 int dev, int64_t b, const tempi_hip_desc &flat)
-      : packer(rec.desc), origin(o), count(c), dt(d), bytes(b) {
+      : rec(r->ref()), origin(o), count(c), dt(d), bytes(b) {
     device = dev;
     sh = std::make_shared<DirectShared>();
     sh->device = dev;
@@ -443,14 +479,14 @@ struct IsendDirectOp : Op {
     desc.senderWorld = state.worldRank;
     desc.senderPid = int32_t(getpid());
     desc.device = dev;
-    desc.first = reinterpret_cast<uint64_t>(o + rec.desc.start);
+    desc.first = reinterpret_cast<uint64_t>(o + rec->desc.start);
     desc.desc = flat;
     // the library may hold a send to this same process open until its
     // receive is posted (MPICH does), so the send's completion cannot wait for
     // it: the request is released now and the descriptor outlives it in `sh`
-    MPI_Request r;
-    next.MPI_Isend(&desc, int(sizeof desc), MPI_PACKED, dest, tag, comm, &r);
-    MPI_Request_free(&r);
+    MPI_Request sreq;
+    next.MPI_Isend(&desc, int(sizeof desc), MPI_PACKED, dest, tag, comm, &sreq);
+    MPI_Request_free(&sreq);
   }
   ~IsendDirectOp() override {
     if (sh) sh->sender = nullptr;
@@ -470,11 +506,8 @@ struct IsendDirectOp : Op {
     counters.direct_fallbacks++;
     sh->state = DirectShared::PACKED;
     sh->slab = device_pool().get(size_t(bytes), device);
-    Pending p;
-    p.op = this;
-    packer.items(sh->slab->dev, origin, count, p.items);
-    queued = true;
-    pendingPack.push_back(std::move(p));
+    pendingPack.add_items(this, *rec->packer, sh->slab->dev, origin, count);
+    pendingPack.queue(this);
   }
   void status(MPI_Status *s) const override {
     if (s != MPI_STATUS_IGNORE) {
@@ -575,8 +608,22 @@ void land_descriptor(const void *msg, int n, std::vector<char> &out) {
 
 constexpr size_t kDescCap = sizeof(DirectDesc) > sizeof(IpcDesc) ? sizeof(DirectDesc) : sizeof(IpcDesc);
 
+int64_t desc_bytes(const tempi_hip_desc &d) {
+  int64_t b = d.block;
+  for (int k = 0; k < d.ndims; ++k) b *= d.counts[k];
+  return b;
+}
+
+// what tempi_hip_copy_supported() decides, from descriptors that are already
+// simplified (Packer::flat): the kernel's own normalisation can only merge
+// further, so <= 3 dimensions here is <= 3 there
+bool copy_ok(const tempi_hip_desc &dst, const tempi_hip_desc &src) {
+  const int64_t b = desc_bytes(src);
+  return dst.ndims <= 3 && src.ndims <= 3 && b == desc_bytes(dst) && b < (int64_t(1) << 31);
+}
+
 struct IrecvOp : Op {
-  Packer packer;
+  RecordRef rec;
   char *origin; // GPU-visible
   int count;
   MPI_Datatype dt;
@@ -590,9 +637,9 @@ struct IrecvOp : Op {
   int64_t elems = 0;
   std::shared_ptr<DirectShared> direct; // a same-process send being copied / unpacked
 
-  IrecvOp(const TypeRecord &rec, char *o, int c, MPI_Datatype d, int source, int tag, MPI_Comm cm, int dev,
+  IrecvOp(const TypeRecord *r, char *o, int c, MPI_Datatype d, int source, int tag, MPI_Comm cm, int dev,
           int64_t b)
-      : packer(rec.desc), origin(o), count(c), dt(d), comm(cm), bytes(b) {
+      : rec(r->ref()), origin(o), count(c), dt(d), comm(cm), bytes(b) {
     device = dev;
     const size_t cap = std::max<size_t>(size_t(bytes), kDescCap);
     hslab = pinned_pool().get(cap, device);
@@ -612,13 +659,11 @@ struct IrecvOp : Op {
   }
 
   void lib_done(const MPI_Status &st) override { // arrived: queue its unpack
+    const Packer &packer = *rec->packer;
     if (fallback) { // the host copy of an IPC message we could not map
-      Pending p;
-      p.op = this;
       elems = packer.desc().size ? desc.bytes / packer.desc().size : 0;
-      packer.items(hslab->dev, origin, elems, p.items);
-      queued = true;
-      pendingUnpack.push_back(std::move(p));
+      pendingUnpack.add_items(this, packer, hslab->dev, origin, elems);
+      pendingUnpack.queue(this);
       return;
     }
     libStatus = st;
@@ -627,8 +672,6 @@ struct IrecvOp : Op {
     IpcDesc d;
     std::memcpy(&d, hslab->host, std::min<size_t>(sizeof d, size_t(n)));
     const int64_t size = packer.desc().size;
-    Pending p;
-    p.op = this;
     if (is_direct(hslab->host, n)) {
       DirectDesc dd;
       std::memcpy(&dd, hslab->host, sizeof dd);
@@ -639,23 +682,21 @@ struct IrecvOp : Op {
       tempi_hip_desc mine;
       char *first = origin + packer.desc().start;
       if (direct->state == DirectShared::PENDING && sameDevice && elems * size == dd.bytes &&
-          packer.flat(elems, &mine) &&
-          tempi_hip_copy_supported(first, reinterpret_cast<const void *>(dd.first), &mine, &dd.desc) == 1) {
+          rec->flat(elems, &mine) && copy_ok(mine, dd.desc)) {
         direct->state = DirectShared::CLAIMED;
         tempi_hip_copy_item c;
         c.dst_first = first;
         c.src_first = reinterpret_cast<const void *>(dd.first);
         c.dst = mine;
         c.src = dd.desc;
-        p.copies.push_back(c);
+        pendingUnpack.add_copy(this, c);
       } else if (direct->state == DirectShared::PACKED && sameDevice) {
-        packer.items(direct->slab->dev, origin, elems, p.items);
+        pendingUnpack.add_items(this, packer, direct->slab->dev, origin, elems);
       } else { // another device, or a shape the copy kernel does not take
         materialise_direct(direct, dd, hslab);
-        packer.items(hslab->dev, origin, elems, p.items);
+        pendingUnpack.add_items(this, packer, hslab->dev, origin, elems);
       }
-      queued = true;
-      pendingUnpack.push_back(std::move(p));
+      pendingUnpack.queue(this);
       return;
     }
     if (size_t(n) == sizeof(IpcDesc) && d.magic[0] == kMagic0 && d.magic[1] == kMagic1) {
@@ -673,14 +714,13 @@ struct IrecvOp : Op {
       }
       const char *peer = static_cast<const char *>(base) + d.offset;
       elems = size ? d.bytes / size : 0;
-      packer.items(const_cast<char *>(peer), origin, elems, p.items);
+      pendingUnpack.add_items(this, packer, const_cast<char *>(peer), origin, elems);
     } else {
       if (int64_t(n) > bytes) LOG_FATAL("message truncated: " << n << " B into " << bytes);
       elems = size ? n / size : 0;
-      packer.items(hslab->dev, origin, elems, p.items);
+      pendingUnpack.add_items(this, packer, hslab->dev, origin, elems);
     }
-    queued = true;
-    pendingUnpack.push_back(std::move(p));
+    pendingUnpack.queue(this);
   }
   void gpu_done() override {
     if (ipc) send_ack(desc);
@@ -764,7 +804,7 @@ struct LibIrecvOp : Op {
 // (the reference uses a plain counter that can collide: SURVEY F9)
 constexpr uint32_t kHandleSpace = 1u << 26;
 uint32_t nextHandle = 1;
-std::map<uint32_t, std::unique_ptr<Op>> active; // ordered: creation order
+std::unordered_map<uint32_t, std::unique_ptr<Op>> active;
 
 MPI_Request add(std::unique_ptr<Op> op) {
   while (active.count(nextHandle) || nextHandle == 0) nextHandle = (nextHandle + 1) % kHandleSpace;
@@ -835,17 +875,30 @@ void finalize() {
   pinned_pool().release_all();
 }
 
-bool handles(const void *buf, int count, MPI_Datatype dt, int peer) {
+bool handles(const void *buf, int count, MPI_Datatype dt, int peer, Route *route) {
   if (!state.active || !gpu::available() || count <= 0 || peer == MPI_PROC_NULL) return false;
   const TypeRecord *rec = type_lookup(dt);
   if (!rec || rec->desc.size == 0) return false;
   const int64_t first = rec->desc.valid ? rec->desc.start : 0;
-  return gpu::classify(static_cast<const char *>(buf) + first).device_accessible;
+  const gpu::Ptr p = gpu::classify(static_cast<const char *>(buf) + first);
+  if (!p.device_accessible) return false;
+  route->rec = rec;
+  route->ptr = p;
+  return true;
 }
 
+namespace {
+// packed bytes of `count` elements: the type size for a strided record
+// (homogeneous MPI_Pack_size adds no header), else the library's answer
+int64_t packed_bytes(const TypeRecord *rec, int count, MPI_Datatype dt, MPI_Comm comm) {
+  if (rec->desc.valid) return rec->desc.size * int64_t(count);
+  return pack_size(count, dt, comm);
+}
+} // namespace
+
 int isend(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Comm comm, MPI_Request *req,
-          int force, bool blocking) {
-  const TypeRecord *rec = type_lookup(dt);
+          const Route &route, int force, bool blocking) {
+  const TypeRecord *rec = route.rec;
   ScopedNs timer(counters.ns_isend);
   if (pendingPack.size() >= kMaxPending) flush(); // (no progress(): consecutive Isends share a launch)
   counters.isends++;
@@ -853,13 +906,22 @@ int isend(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Co
     *req = add(std::make_unique<LibIsendOp>(buf, count, dt, dest, tag, comm));
     return MPI_SUCCESS;
   }
-  const gpu::Ptr p = gpu::classify(static_cast<const char *>(buf) + rec->desc.start);
-  const int64_t bytes = pack_size(count, dt, comm);
-  const bool colocated = topology::colocated(comm, dest);
+  const gpu::Ptr &p = route.ptr;
+  const int64_t bytes = packed_bytes(rec, count, dt, comm);
+  const char *origin = static_cast<const char *>(p.dptr) - rec->desc.start;
+  const int destWorld = topology::world_rank(comm, dest);
+  // a non-blocking send to this same process: the receiver copies directly
+  tempi_hip_desc flat;
+  if (directEnabled && !blocking && force < 0 && destWorld == state.worldRank && rec->flat(count, &flat)) {
+    counters.send_direct++;
+    *req = add(std::make_unique<IsendDirectOp>(rec, origin, count, dt, dest, tag, comm, p.device, bytes, flat));
+    return MPI_SUCCESS;
+  }
+  const bool colocated = topology::colocated_world(destWorld);
   modelBlock = std::min<int64_t>(std::max<int64_t>(1, rec->desc.block), 512);
   Method m = choose(bytes, colocated);
   if (force >= 0) m = Method(force);
-  if (m == Method::IPC && (!colocated || ipc_broken(topology::world_rank(comm, dest)))) m = Method::ONESHOT;
+  if (m == Method::IPC && (!colocated || ipc_broken(destWorld))) m = Method::ONESHOT;
   if (m == Method::DEVICE && !gpuAwareLibrary) m = colocated ? Method::IPC : Method::STAGED;
   switch (m) {
   case Method::ONESHOT: counters.send_oneshot++; break;
@@ -868,25 +930,17 @@ int isend(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Co
   case Method::IPC: counters.send_ipc++; break;
   default: break;
   }
-  const char *origin = static_cast<const char *>(p.dptr) - rec->desc.start;
-  // a non-blocking send to this same process: the receiver copies directly
-  tempi_hip_desc flat;
-  if (directEnabled && !blocking && force < 0 && topology::world_rank(comm, dest) == state.worldRank &&
-      Packer(rec->desc).flat(count, &flat)) {
-    counters.send_direct++;
-    *req = add(std::make_unique<IsendDirectOp>(*rec, origin, count, dt, dest, tag, comm, p.device, bytes, flat));
-    return MPI_SUCCESS;
-  }
   int cur = 0;
   tempi_hip_get_device(&cur);
   if (cur != p.device) tempi_hip_set_device(p.device);
-  *req = add(std::make_unique<IsendOp>(*rec, origin, count, dt, dest, tag, comm, p.device, m, bytes));
+  *req = add(std::make_unique<IsendOp>(rec, origin, count, dt, dest, tag, comm, p.device, m, bytes));
   if (cur != p.device) tempi_hip_set_device(cur);
   return MPI_SUCCESS;
 }
 
-int irecv(void *buf, int count, MPI_Datatype dt, int source, int tag, MPI_Comm comm, MPI_Request *req) {
-  const TypeRecord *rec = type_lookup(dt);
+int irecv(void *buf, int count, MPI_Datatype dt, int source, int tag, MPI_Comm comm, MPI_Request *req,
+          const Route &route) {
+  const TypeRecord *rec = route.rec;
   // start queued gathers (a burst of Isends shares this launch); the rest of
   // progress is left to the waits, so a burst of Irecvs stays O(1) each
   if (!pendingPack.empty()) flush_list(pendingPack, true);
@@ -896,10 +950,10 @@ int irecv(void *buf, int count, MPI_Datatype dt, int source, int tag, MPI_Comm c
     *req = add(std::make_unique<LibIrecvOp>(buf, count, dt, source, tag, comm));
     return MPI_SUCCESS;
   }
-  const gpu::Ptr p = gpu::classify(static_cast<char *>(buf) + rec->desc.start);
-  const int64_t bytes = pack_size(count, dt, comm);
+  const gpu::Ptr &p = route.ptr;
+  const int64_t bytes = packed_bytes(rec, count, dt, comm);
   char *origin = static_cast<char *>(p.dptr) - rec->desc.start;
-  *req = add(std::make_unique<IrecvOp>(*rec, origin, count, dt, source, tag, comm, p.device, bytes));
+  *req = add(std::make_unique<IrecvOp>(rec, origin, count, dt, source, tag, comm, p.device, bytes));
   // keep the GPU busy while the caller is still posting: launch arrived
   // messages' copies / unpacks once a launch's worth has queued up
   if (pendingUnpack.size() >= kEarlyFlush) flush_list(pendingUnpack, false);

@@ -36,24 +36,34 @@
 // (device buffer, or a blocking MPI_Recv of any buffer).
 #pragma once
 
+#include "gpu.hpp"
+
 #include <mpi.h>
 
 namespace tempi {
+struct TypeRecord;
 namespace p2p {
 
 void init();
 void finalize();
 
+// what handles() found out, handed on to isend / irecv
+struct Route {
+  const TypeRecord *rec = nullptr;
+  gpu::Ptr ptr; // the first byte the type touches
+};
+
 // true when TEMPI handles this send / receive (otherwise: library)
-bool handles(const void *buf, int count, MPI_Datatype dt, int peer);
+bool handles(const void *buf, int count, MPI_Datatype dt, int peer, Route *route);
 
 // force: -1 = choose by TEMPI_DATATYPE_* / AUTO; else a forced method
 // (0 ONESHOT, 1 STAGED, 2 DEVICE, 3 IPC)
 // blocking = true (MPI_Send) never takes the DIRECT route, whose completion
 // needs the matching receive
 int isend(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Comm comm, MPI_Request *req,
-          int force = -1, bool blocking = false);
-int irecv(void *buf, int count, MPI_Datatype dt, int source, int tag, MPI_Comm comm, MPI_Request *req);
+          const Route &route, int force = -1, bool blocking = false);
+int irecv(void *buf, int count, MPI_Datatype dt, int source, int tag, MPI_Comm comm, MPI_Request *req,
+          const Route &route);
 
 bool is_tempi_request(MPI_Request r);
 // drive every TEMPI operation one step; returns true if anything moved.

@@ -10,7 +10,7 @@ namespace tempi {
 
 namespace {
 std::mutex mtx;
-std::unordered_map<MPI_Datatype, std::unique_ptr<TypeRecord>> cache;
+std::unordered_map<MPI_Datatype, std::shared_ptr<TypeRecord>> cache;
 } // namespace
 
 const TypeRecord *type_commit(MPI_Datatype t) {
@@ -19,10 +19,11 @@ const TypeRecord *type_commit(MPI_Datatype t) {
     auto it = cache.find(t);
     if (it != cache.end()) return it->second.get();
   }
-  auto rec = std::make_unique<TypeRecord>();
+  auto rec = std::make_shared<TypeRecord>();
   rec->desc = canonicalise(t);
   if (rec->desc.valid) {
     rec->packer = std::make_unique<Packer>(rec->desc);
+    rec->flat1ok = rec->packer->flat(1, &rec->flat1);
     LOG_SPEW("type " << t << " -> " << rec->desc.str());
   } else {
     LOG_DEBUG("type " << t << " is not a strided block; library handles it");

@@ -13,9 +13,26 @@
 
 namespace tempi {
 
-struct TypeRecord {
+struct TypeRecord;
+// in-flight operations hold their type's record: MPI_Type_free may come
+// before the operation completes
+typedef std::shared_ptr<const TypeRecord> RecordRef;
+
+struct TypeRecord : std::enable_shared_from_this<TypeRecord> {
   StridedBlock desc;
   std::unique_ptr<Packer> packer; // null when !desc.valid (library handles it)
+  tempi_hip_desc flat1{};         // one element as a single descriptor
+  bool flat1ok = false;
+
+  RecordRef ref() const { return shared_from_this(); }
+  // `count` elements as one descriptor (Packer::flat; cached for count 1)
+  bool flat(int64_t count, tempi_hip_desc *out) const {
+    if (count == 1) {
+      *out = flat1;
+      return flat1ok;
+    }
+    return packer && packer->flat(count, out);
+  }
 };
 
 // analyse + cache (no-op when already cached); returns the record

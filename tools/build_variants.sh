@@ -18,3 +18,8 @@ wait
 g++ -O2 -std=c++17 -Iinclude -o tools/_variants/kbench tools/kbench.cpp -ldl
 g++ -O2 -std=c++17 -Iinclude -o tools/_variants/hbench tools/hbench.cpp -ldl
 ls tools/_variants
+# hostbench: built like the apps (hipcc, static libstdc++: conda's older
+# libstdc++ sits on the MPI rpath)
+hipcc -O2 -std=c++17 -Iinclude -I/opt/conda/include -o tools/_variants/hostbench tools/hostbench.cpp \
+  -Ltempi_amd/lib -ltempi_hip -L/opt/conda/lib -lmpi -static-libstdc++ \
+  -Wl,-rpath,'$ORIGIN/../../tempi_amd/lib' -Wl,-rpath,/opt/conda/lib
