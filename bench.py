@@ -298,13 +298,27 @@ def halo(args, mpi, world):
         "busiest_peer_bytes_per_iter": r["max_peer_bytes_per_iter"],
         "rank0_phase_us": r.get("rank0_us_per_iter"),
     }
-    if world > 1:
+    out["payload_GBps_all_ranks"] = round(r["total_bytes_per_iter"] / t / 1e9, 1)
+    # rank 0's own share: messages to itself are one strided -> strided copy
+    # (read + write each payload byte once in HBM); messages to a peer are a
+    # pack (read + write) here and a scatter on the peer that pulls the
+    # packed bytes over xGMI (read there + write there)
+    if world == 1:
+        hbm_bytes = 2.0 * r["total_bytes_per_iter"]
+        lb = hbm_bytes / (HBM_PEAK_GBS * 1e9)
+        out["roofline"] = {"bound": "hbm", "algorithmic_bytes_per_iter": int(hbm_bytes),
+                           "lower_bound_us": round(lb * 1e6, 1), "achieved_GBps": round(hbm_bytes / t / 1e9, 1),
+                           "peak_GBps": HBM_PEAK_GBS, "frac": round(lb / t, 4),
+                           "note": ("all 26 neighbours are this rank: every message is one strided->strided "
+                                    "copy (2 x payload bytes); 24-byte x-face rows touch a 64-byte DRAM sector "
+                                    "per row on both sides, so the sector-level bound is ~2.7x higher for "
+                                    "those faces")}
+    else:
         # xGMI: the busiest point-to-point link carries max_peer bytes per iteration
-        out["xgmi"] = {"busiest_link_GBps": round(r["busiest_link_GBps"], 2), "link_peak_GBps": XGMI_LINK_GBS,
-                       "frac": round(r["busiest_link_GBps"] / XGMI_LINK_GBS, 4),
-                       "lower_bound_us": round(r["max_peer_bytes_per_iter"] / (XGMI_LINK_GBS * 1e9) * 1e6, 1)}
-    # HBM: pack + unpack of every byte = 4 x payload per iteration per rank
-    out["hbm_equiv_GBps_per_rank"] = round(4 * r["total_bytes_per_iter"] / world / t / 1e9, 1)
+        lb = r["max_peer_bytes_per_iter"] / (XGMI_LINK_GBS * 1e9)
+        out["roofline"] = {"bound": "xgmi", "busiest_link_GBps": round(r["busiest_link_GBps"], 2),
+                           "link_peak_GBps": XGMI_LINK_GBS, "frac": round(r["busiest_link_GBps"] / XGMI_LINK_GBS, 4),
+                           "lower_bound_us": round(lb * 1e6, 1)}
     return out
 
 

@@ -309,7 +309,7 @@ struct PendingList {
 };
 PendingList pendingPack, pendingUnpack;
 constexpr size_t kMaxPending = 512;
-constexpr size_t kEarlyFlush = 16;
+size_t earlyFlush = 32; // TEMPI_EARLY_FLUSH
 
 template <typename T> const T *select(const std::vector<T> &v, const std::vector<int> &dev, int d, bool all,
                                       std::vector<T> &tmp) {
@@ -826,6 +826,7 @@ std::vector<MPI_Status> pollSt;
 void init() {
   gpuAwareLibrary = std::getenv("TEMPI_MPI_GPU_AWARE") != nullptr;
   directEnabled = std::getenv("TEMPI_NO_DIRECT") == nullptr;
+  if (const char *s = std::getenv("TEMPI_EARLY_FLUSH")) earlyFlush = size_t(std::max(1, std::atoi(s)));
   directShared.clear();
   systemPerformanceLoaded = import_system_performance(&systemPerformance);
   modelCache.clear();
@@ -956,7 +957,7 @@ int irecv(void *buf, int count, MPI_Datatype dt, int source, int tag, MPI_Comm c
   *req = add(std::make_unique<IrecvOp>(rec, origin, count, dt, source, tag, comm, p.device, bytes));
   // keep the GPU busy while the caller is still posting: launch arrived
   // messages' copies / unpacks once a launch's worth has queued up
-  if (pendingUnpack.size() >= kEarlyFlush) flush_list(pendingUnpack, false);
+  if (pendingUnpack.size() >= earlyFlush) flush_list(pendingUnpack, false);
   counters.ns_irecv += now_ns() - t0;
   return MPI_SUCCESS;
 }

@@ -636,6 +636,13 @@ struct CSide {
 
 struct CArgs {
   CSide s, d;
+  // PAIRED items: a second (src, dst) of exactly the same two shapes, moved
+  // by the same lanes right after the first. In a halo the two opposite faces
+  // of one buffer pair up this way, and the sector one copy writes is the
+  // sector the other just read (x faces: [0,24) and [24,48) of each row):
+  // the write then lands on a line already in L2 and goes back to HBM whole,
+  // instead of as a partial-sector write (a read-modify-write in DRAM)
+  char *s2, *d2; // nullptr: not paired
   uint32_t nwords;
 };
 
@@ -659,6 +666,31 @@ template <int W> __device__ __forceinline__ void copy_body(const CArgs &a, uint3
   constexpr int CW = 16 / W * TEMPI_COPY_U;
   constexpr bool nt = W == 16;
   const uint32_t tile = uint32_t(kBlock) * CW;
+  if (a.s2) {
+    for (uint32_t base = blk * tile; base < a.nwords; base += nblk * tile) {
+      WT v[CW], v2[CW];
+      int64_t so[CW], dof[CW];
+#pragma unroll
+      for (int j = 0; j < CW; ++j) {
+        const uint32_t q = base + uint32_t(j) * kBlock + threadIdx.x;
+        so[j] = q < a.nwords ? side_offset<W>(q, a.s) : 0;
+        dof[j] = q < a.nwords ? side_offset<W>(q, a.d) : 0;
+        if (q < a.nwords) {
+          v[j] = ld(reinterpret_cast<const WT *>(a.s.first + so[j]), false);
+          v2[j] = ld(reinterpret_cast<const WT *>(a.s2 + so[j]), false);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < CW; ++j) {
+        const uint32_t q = base + uint32_t(j) * kBlock + threadIdx.x;
+        if (q < a.nwords) {
+          st(reinterpret_cast<WT *>(a.d.first + dof[j]), v[j], false);
+          st(reinterpret_cast<WT *>(a.d2 + dof[j]), v2[j], false);
+        }
+      }
+    }
+    return;
+  }
   for (uint32_t base = blk * tile; base < a.nwords; base += nblk * tile) {
     WT v[CW];
 #pragma unroll
@@ -739,8 +771,43 @@ bool plan_copy(void *dst, const void *src, const tempi_hip_desc *dd, const tempi
   if (!make_side(const_cast<char *>(static_cast<const char *>(src)), ns, w, &job->a.s)) return false;
   if (!make_side(static_cast<char *>(dst), nd, w, &job->a.d)) return false;
   job->a.nwords = uint32_t(bytes / w);
+  job->a.s2 = job->a.d2 = nullptr;
   job->w = w;
   return true;
+}
+
+bool same_shape(const CSide &x, const CSide &y) {
+  if (x.wpr != y.wpr) return false;
+  for (int k = 0; k < kCopyND - 1; ++k)
+    if (x.cnt[k] != y.cnt[k]) return false;
+  for (int k = 0; k < kCopyND; ++k)
+    if (x.stride[k] != y.stride[k]) return false;
+  return true;
+}
+
+#ifndef TEMPI_COPY_PAIR
+#define TEMPI_COPY_PAIR 1
+#endif
+// pair items of identical shapes (see CArgs::s2); greedy, order-preserving
+std::vector<CopyJob> pair_jobs(const std::vector<CopyJob> &in) {
+  if (!TEMPI_COPY_PAIR) return in;
+  std::vector<CopyJob> out;
+  std::vector<char> used(in.size(), 0);
+  for (size_t i = 0; i < in.size(); ++i) {
+    if (used[i]) continue;
+    CopyJob j = in[i];
+    for (size_t k = i + 1; k < in.size() && k < i + 64; ++k) {
+      if (used[k] || in[k].a.nwords != j.a.nwords || !same_shape(in[k].a.s, j.a.s) ||
+          !same_shape(in[k].a.d, j.a.d))
+        continue;
+      j.a.s2 = in[k].a.s.first;
+      j.a.d2 = in[k].a.d.first;
+      used[k] = 1;
+      break;
+    }
+    out.push_back(j);
+  }
+  return out;
 }
 
 uint32_t copy_blocks(const CopyJob &j) {
@@ -805,11 +872,11 @@ int tempi_hip_copy_batch(const tempi_hip_copy_item *items, int n, void *stream) 
     if (groups[wi].empty()) continue;
     int e = 0;
     switch (wi) {
-    case 0: e = launch_copy_group<1>(groups[wi], s); break;
-    case 1: e = launch_copy_group<2>(groups[wi], s); break;
-    case 2: e = launch_copy_group<4>(groups[wi], s); break;
-    case 3: e = launch_copy_group<8>(groups[wi], s); break;
-    default: e = launch_copy_group<16>(groups[wi], s); break;
+    case 0: e = launch_copy_group<1>(pair_jobs(groups[wi]), s); break;
+    case 1: e = launch_copy_group<2>(pair_jobs(groups[wi]), s); break;
+    case 2: e = launch_copy_group<4>(pair_jobs(groups[wi]), s); break;
+    case 3: e = launch_copy_group<8>(pair_jobs(groups[wi]), s); break;
+    default: e = launch_copy_group<16>(pair_jobs(groups[wi]), s); break;
     }
     if (e) return e;
   }
