@@ -18,7 +18,7 @@ HIPFLAGS := --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Iinclude -Wall
 CXXFLAGS := -std=c++17 -O2 -g -fPIC -fvisibility=hidden -Wall -Wextra -Wno-unused-parameter \
             -Iinclude -I$(MPI_HOME)/include
 
-APPS := $(LIB)/libtempi_apps.so $(LIB)/halo_exchange $(LIB)/pingpong_nd $(LIB)/measure_system
+APPS := $(LIB)/libtempi_apps.so $(LIB)/halo_exchange $(LIB)/pingpong_nd $(LIB)/alltoallv_sparse $(LIB)/measure_system
 
 all: $(LIB)/libtempi.so $(APPS) oracle
 
@@ -42,11 +42,19 @@ $(LIB)/libtempi.so: $(CORE_OBJ) $(LIB)/libtempi_hip.so
 	    -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,$(MPI_HOME)/lib -Wl,--enable-new-dtags
 
 # applications link -ltempi BEFORE the MPI library, like any TEMPI user
-$(LIB)/libtempi_apps.so: apps/halo_lib.cpp $(LIB)/libtempi.so
-	$(HIPCC) --offload-arch=gfx950 -O2 -std=c++17 -fPIC -shared -Iinclude -I$(MPI_HOME)/include -o $@ $< \
+$(LIB)/libtempi_apps.so: apps/halo_lib.cpp apps/bench_lib.cpp $(LIB)/libtempi.so
+	$(HIPCC) --offload-arch=gfx950 -O2 -std=c++17 -fPIC -shared -Iinclude -I$(MPI_HOME)/include -o $@ apps/halo_lib.cpp apps/bench_lib.cpp \
 	    -L$(LIB) -ltempi -L$(MPI_HOME)/lib -lmpi -static-libstdc++ -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,$(MPI_HOME)/lib
 
 $(LIB)/halo_exchange: apps/halo_exchange_main.cpp $(LIB)/libtempi_apps.so
+	$(HIPCC) --offload-arch=gfx950 -O2 -std=c++17 -Iinclude -I$(MPI_HOME)/include -o $@ $< -L$(LIB) -ltempi_apps \
+	    -ltempi -L$(MPI_HOME)/lib -lmpi -static-libstdc++ -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,$(MPI_HOME)/lib
+
+$(LIB)/pingpong_nd: apps/pingpong_nd.cpp $(LIB)/libtempi_apps.so
+	$(HIPCC) --offload-arch=gfx950 -O2 -std=c++17 -Iinclude -I$(MPI_HOME)/include -o $@ $< -L$(LIB) -ltempi_apps \
+	    -ltempi -L$(MPI_HOME)/lib -lmpi -static-libstdc++ -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,$(MPI_HOME)/lib
+
+$(LIB)/alltoallv_sparse: apps/alltoallv_sparse.cpp $(LIB)/libtempi_apps.so
 	$(HIPCC) --offload-arch=gfx950 -O2 -std=c++17 -Iinclude -I$(MPI_HOME)/include -o $@ $< -L$(LIB) -ltempi_apps \
 	    -ltempi -L$(MPI_HOME)/lib -lmpi -static-libstdc++ -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,$(MPI_HOME)/lib
 

@@ -1,0 +1,246 @@
+// apps/bench_lib.cpp -- configs 3 and 5 as library calls (libtempi_apps.so),
+// so that bench.py can run them inside the driver's torch.distributed launch
+// and the CLIs (apps/pingpong_nd.cpp, apps/alltoallv_sparse.cpp) under mpiexec.
+//
+// tempi_bench_pingpong: the reference's bench_mpi_pingpong_nd
+//   (/root/reference/bin/bench_mpi_pingpong_nd.cpp:146-197):
+//   MPI_Type_vector(total/bl, bl, stride, MPI_BYTE), count 1, device buffers,
+//   rank 0 -> 1 -> 0 with MPI_Send / MPI_Recv; one-way time = trimean of the
+//   round trips / 2. Ranks other than 0 and 1 only take part in the barriers.
+//   check: every block holds rank 0's bytes afterwards, every gap its owner's.
+//
+// tempi_bench_alltoallv: the reference's bench_alltoallv_random_sparse
+//   (/root/reference/bin/bench_alltoallv_random_sparse.cpp:100-222): an
+//   MPI_BYTE MPI_Alltoallv of device buffers whose counts are the matrix of
+//   SquareMat::make_random_sparse(size, round(density*size), 1, 10, scale,
+//   seed) (/root/reference/support/squaremat.cpp:52-75, restated here with
+//   the same srand/rand and std::shuffle(default_random_engine) calls, so the
+//   matrix is the reference's own); time = max over ranks, min over
+//   iterations, as there. check: every received byte is the sender's pattern.
+#include <hip/hip_runtime.h>
+#include <mpi.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <numeric>
+#include <random>
+#include <vector>
+
+#define HIPCHECK(x)                                                                                \
+  do {                                                                                             \
+    hipError_t e_ = (x);                                                                           \
+    if (e_ != hipSuccess) {                                                                        \
+      std::fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_));              \
+      MPI_Abort(MPI_COMM_WORLD, 1);                                                                \
+    }                                                                                              \
+  } while (0)
+
+#define EXPORT extern "C" __attribute__((visibility("default")))
+
+namespace {
+
+double trimean(std::vector<double> v) {
+  if (v.empty()) return 0;
+  std::sort(v.begin(), v.end());
+  auto pct = [&](double p) {
+    const double idx = p * double(v.size() - 1);
+    const size_t lo = size_t(std::floor(idx)), hi = size_t(std::ceil(idx));
+    return v[lo] + (v[hi] - v[lo]) * (idx - double(lo));
+  };
+  return (pct(0.25) + 2 * pct(0.5) + pct(0.75)) / 4;
+}
+
+const char *method_name() {
+  if (std::getenv("TEMPI_DATATYPE_ONESHOT")) return "ONESHOT";
+  if (std::getenv("TEMPI_DATATYPE_STAGED")) return "STAGED";
+  if (std::getenv("TEMPI_DATATYPE_IPC")) return "IPC";
+  if (std::getenv("TEMPI_DATATYPE_DEVICE")) return "DEVICE";
+  if (std::getenv("TEMPI_DISABLE")) return "LIBRARY";
+  return "AUTO";
+}
+
+// SquareMat::make_random_sparse (row-major ranks x ranks)
+std::vector<int64_t> random_sparse(int ranks, int rowNnz, int lb, int ub, int scale, int seed) {
+  srand(unsigned(seed));
+  std::default_random_engine dre(static_cast<std::default_random_engine::result_type>(seed));
+  rowNnz = std::min(rowNnz, ranks);
+  std::vector<int64_t> mat(size_t(ranks) * size_t(ranks), 0);
+  std::vector<size_t> rowInd(static_cast<size_t>(ranks));
+  std::iota(rowInd.begin(), rowInd.end(), size_t(0));
+  for (int r = 0; r < ranks; ++r) {
+    std::shuffle(rowInd.begin(), rowInd.end(), dre);
+    for (int i = 0; i < rowNnz; ++i) mat[size_t(r) * size_t(ranks) + rowInd[size_t(i)]] = (lb + rand() % (ub - lb)) * scale;
+  }
+  return mat;
+}
+
+__host__ __device__ inline unsigned char a2av_byte(int64_t i, int src, int dst) {
+  return (unsigned char)((i * 31 + src * 7 + dst * 13) & 0xFF);
+}
+
+} // namespace
+
+EXPORT int tempi_bench_pingpong(int iters, long total, long bl, long stride, int check, int setDevice, char *json,
+                                int jsonCap) {
+  int rank, size;
+  MPI_Comm_rank(MPI_COMM_WORLD, &rank);
+  MPI_Comm_size(MPI_COMM_WORLD, &size);
+  if (size < 2 || bl <= 0 || total < bl || stride < bl) return 2;
+  const int nblocks = int(total / bl);
+  if (setDevice) {
+    int ndev = 0;
+    HIPCHECK(hipGetDeviceCount(&ndev));
+    HIPCHECK(hipSetDevice(rank % ndev));
+  }
+  MPI_Datatype t;
+  MPI_Type_vector(nblocks, int(bl), int(stride), MPI_BYTE, &t);
+  MPI_Type_commit(&t);
+  MPI_Aint lb, ext;
+  MPI_Type_get_extent(t, &lb, &ext);
+  char *buf;
+  HIPCHECK(hipMalloc(&buf, size_t(ext)));
+  std::vector<unsigned char> h(static_cast<size_t>(ext));
+  for (size_t i = 0; i < h.size(); ++i) h[i] = (unsigned char)((i * 131 + size_t(rank) * 7) & 0xFF);
+  HIPCHECK(hipMemcpy(buf, h.data(), h.size(), hipMemcpyHostToDevice));
+
+  std::vector<double> times;
+  long errors = 0;
+  for (int i = 0; i < iters + 2; ++i) {
+    MPI_Barrier(MPI_COMM_WORLD);
+    const double t0 = MPI_Wtime();
+    if (rank == 0) {
+      MPI_Send(buf, 1, t, 1, 0, MPI_COMM_WORLD);
+      MPI_Recv(buf, 1, t, 1, 0, MPI_COMM_WORLD, MPI_STATUS_IGNORE);
+    } else if (rank == 1) {
+      MPI_Recv(buf, 1, t, 0, 0, MPI_COMM_WORLD, MPI_STATUS_IGNORE);
+      MPI_Send(buf, 1, t, 0, 0, MPI_COMM_WORLD);
+    }
+    const double el = MPI_Wtime() - t0;
+    if (i >= 2) times.push_back(el);
+  }
+  if (check && rank < 2) {
+    // every block now holds rank 0's original bytes; the gaps keep each
+    // rank's own pattern
+    std::vector<unsigned char> g(static_cast<size_t>(ext));
+    HIPCHECK(hipMemcpy(g.data(), buf, g.size(), hipMemcpyDeviceToHost));
+    for (long b = 0; b < nblocks; ++b)
+      for (long k = 0; k < stride && b * stride + k < long(ext); ++k) {
+        const size_t i = size_t(b * stride + k);
+        const unsigned char exp0 = (unsigned char)((i * 131) & 0xFF);
+        const unsigned char mine = (unsigned char)((i * 131 + size_t(rank) * 7) & 0xFF);
+        if (g[i] != (k < bl ? exp0 : mine)) ++errors;
+      }
+  }
+  MPI_Allreduce(MPI_IN_PLACE, &errors, 1, MPI_LONG, MPI_SUM, MPI_COMM_WORLD);
+  if (rank == 0 && json && jsonCap > 0) {
+    const double oneway = trimean(times) / 2;
+    std::snprintf(json, size_t(jsonCap),
+                  "{\"total\": %ld, \"block\": %ld, \"stride\": %ld, \"iters\": %d, \"oneway_us\": %.2f, "
+                  "\"GBps\": %.3f, \"checked\": %s, \"errors\": %ld, \"method\": \"%s\"}",
+                  total, bl, stride, iters, oneway * 1e6, double(total) / oneway / 1e9, check ? "true" : "false",
+                  errors, method_name());
+  }
+  MPI_Type_free(&t);
+  HIPCHECK(hipFree(buf));
+  return errors ? 3 : 0;
+}
+
+__global__ void a2av_fill(unsigned char *buf, const int64_t *displ, const int64_t *count, int n, int src) {
+  for (int d = 0; d < n; ++d)
+    for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < count[d]; i += int64_t(gridDim.x) * blockDim.x)
+      buf[displ[d] + i] = a2av_byte(i, src, d);
+}
+
+EXPORT int tempi_bench_alltoallv(int iters, int scale, double density, int seed, int check, int setDevice,
+                                 char *json, int jsonCap) {
+  int rank, size;
+  MPI_Comm_rank(MPI_COMM_WORLD, &rank);
+  MPI_Comm_size(MPI_COMM_WORLD, &size);
+  if (setDevice) {
+    int ndev = 0;
+    HIPCHECK(hipGetDeviceCount(&ndev));
+    HIPCHECK(hipSetDevice(rank % ndev));
+  }
+  const int rowNnz = int(density * size + 0.5);
+  const std::vector<int64_t> mat = random_sparse(size, rowNnz, 1, 10, scale, seed);
+  auto M = [&](int r, int c) { return mat[size_t(r) * size_t(size) + size_t(c)]; };
+  std::vector<int> sc(static_cast<size_t>(size)), rc(static_cast<size_t>(size)), sd(static_cast<size_t>(size)), rd(static_cast<size_t>(size));
+  int64_t sbytes = 0, rbytes = 0, maxPair = 0, total = 0;
+  for (int p = 0; p < size; ++p) {
+    sc[size_t(p)] = int(M(rank, p));
+    rc[size_t(p)] = int(M(p, rank));
+    sd[size_t(p)] = int(sbytes);
+    rd[size_t(p)] = int(rbytes);
+    sbytes += sc[size_t(p)];
+    rbytes += rc[size_t(p)];
+  }
+  for (int r = 0; r < size; ++r)
+    for (int c = 0; c < size; ++c) {
+      total += M(r, c);
+      if (r != c) maxPair = std::max(maxPair, M(r, c));
+    }
+  // busiest link: bytes out of (or into) one GPU to other GPUs
+  int64_t maxOut = 0;
+  for (int r = 0; r < size; ++r) {
+    int64_t o = 0, in = 0;
+    for (int c = 0; c < size; ++c)
+      if (c != r) {
+        o += M(r, c);
+        in += M(c, r);
+      }
+    maxOut = std::max(maxOut, std::max(o, in));
+  }
+  unsigned char *sbuf, *rbuf;
+  HIPCHECK(hipMalloc(&sbuf, size_t(std::max<int64_t>(sbytes, 1))));
+  HIPCHECK(hipMalloc(&rbuf, size_t(std::max<int64_t>(rbytes, 1))));
+  {
+    std::vector<int64_t> hd(static_cast<size_t>(size)), hc(static_cast<size_t>(size));
+    for (int p = 0; p < size; ++p) {
+      hd[size_t(p)] = sd[size_t(p)];
+      hc[size_t(p)] = sc[size_t(p)];
+    }
+    int64_t *dd, *dc;
+    HIPCHECK(hipMalloc(&dd, sizeof(int64_t) * size_t(size)));
+    HIPCHECK(hipMalloc(&dc, sizeof(int64_t) * size_t(size)));
+    HIPCHECK(hipMemcpy(dd, hd.data(), sizeof(int64_t) * size_t(size), hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(dc, hc.data(), sizeof(int64_t) * size_t(size), hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(a2av_fill, dim3(256), dim3(256), 0, 0, sbuf, dd, dc, size, rank);
+    HIPCHECK(hipMemset(rbuf, 0xEE, size_t(std::max<int64_t>(rbytes, 1))));
+    HIPCHECK(hipDeviceSynchronize());
+    HIPCHECK(hipFree(dd));
+    HIPCHECK(hipFree(dc));
+  }
+  std::vector<double> times;
+  for (int i = 0; i < iters + 1; ++i) {
+    MPI_Barrier(MPI_COMM_WORLD);
+    const double t0 = MPI_Wtime();
+    MPI_Alltoallv(sbuf, sc.data(), sd.data(), MPI_BYTE, rbuf, rc.data(), rd.data(), MPI_BYTE, MPI_COMM_WORLD);
+    double el = MPI_Wtime() - t0;
+    MPI_Allreduce(MPI_IN_PLACE, &el, 1, MPI_DOUBLE, MPI_MAX, MPI_COMM_WORLD);
+    if (i >= 1) times.push_back(el);
+  }
+  long errors = 0;
+  if (check) {
+    std::vector<unsigned char> h(size_t(std::max<int64_t>(rbytes, 1)));
+    HIPCHECK(hipMemcpy(h.data(), rbuf, h.size(), hipMemcpyDeviceToHost));
+    for (int p = 0; p < size; ++p)
+      for (int64_t i = 0; i < rc[size_t(p)]; ++i)
+        if (h[size_t(rd[size_t(p)] + i)] != a2av_byte(i, p, rank)) ++errors;
+    MPI_Allreduce(MPI_IN_PLACE, &errors, 1, MPI_LONG, MPI_SUM, MPI_COMM_WORLD);
+  }
+  if (rank == 0 && json && jsonCap > 0) {
+    const double tmin = times.empty() ? 0 : *std::min_element(times.begin(), times.end());
+    std::snprintf(json, size_t(jsonCap),
+                  "{\"ranks\": %d, \"scale\": %d, \"density\": %.4f, \"row_nnz\": %d, \"seed\": %d, \"iters\": %d, "
+                  "\"min_us\": %.2f, \"trimean_us\": %.2f, \"total_bytes\": %lld, \"max_pairwise_bytes\": %lld, "
+                  "\"max_gpu_out_or_in_bytes\": %lld, \"checked\": %s, \"errors\": %ld}",
+                  size, scale, density, rowNnz, seed, iters, tmin * 1e6, trimean(times) * 1e6, (long long)total,
+                  (long long)maxPair, (long long)maxOut, check ? "true" : "false", errors);
+  }
+  HIPCHECK(hipFree(sbuf));
+  HIPCHECK(hipFree(rbuf));
+  return errors ? 3 : 0;
+}

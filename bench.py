@@ -161,6 +161,10 @@ def run_traffic_passes(args, kernel_substr):
 
     if not shutil.which("rocprofv3"):
         return None
+    # already under a profiler: a nested rocprofv3 would exec from a process
+    # whose GPU the outer profiler's preload has initialised
+    if any(k.startswith("ROCPROF") for k in os.environ) or "rocprof" in os.environ.get("LD_PRELOAD", ""):
+        return None
     out = {}
     for counter in ("FETCH_SIZE", "WRITE_SIZE"):
         d = tempfile.mkdtemp(prefix="tempi_pmc_", dir=os.path.join(ROOT, "gpurun_out") if os.path.isdir(
