@@ -20,6 +20,9 @@ iteration) run through MPI_Isend/MPI_Irecv/MPI_Wait on the same ranks
 (strong scaling of the fixed grid), with its xGMI roofline. Under torchrun
 the ranks are wired into one MPI job by tempi_amd.pmi.
 
+At N > 1 the line also carries "pingpong" (config 3, ranks 0 <-> 1) and
+"alltoallv" (config 5, all ranks), each with its xGMI fraction.
+
 Other modes (not the driver's line):
   --sweep FILE   the config-2 sweep (block 1 B - 4 KiB, 2D and 3D, 1 MiB -
                  1 GiB), one JSON record per point, written to FILE
@@ -53,6 +56,9 @@ def parse():
     p.add_argument("--no-halo", action="store_true")
     p.add_argument("--halo-grid", type=int, default=512)
     p.add_argument("--halo-iters", type=int, default=10)
+    p.add_argument("--pp-iters", type=int, default=50)
+    p.add_argument("--a2av-iters", type=int, default=20)
+    p.add_argument("--no-p2p", action="store_true", help="skip configs 3 and 5 at N > 1")
     p.add_argument("--sweep", default=None, help="run the config-2 sweep and write JSON records here")
     p.add_argument("--inner", action="store_true", help=argparse.SUPPRESS)  # child for --traffic
     return p.parse_args()
@@ -326,6 +332,67 @@ def halo(args, mpi, world):
     return out
 
 
+def apps_lib():
+    import ctypes
+
+    import tempi_amd
+
+    L = ctypes.CDLL(os.path.join(tempi_amd.LIBDIR, "libtempi_apps.so"), mode=ctypes.RTLD_GLOBAL)
+    L.tempi_bench_pingpong.argtypes = [ctypes.c_int, ctypes.c_long, ctypes.c_long, ctypes.c_long, ctypes.c_int,
+                                       ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
+    L.tempi_bench_alltoallv.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_int, ctypes.c_int,
+                                        ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
+    return L
+
+
+def pingpong(args, world):
+    """Config 3 between ranks 0 and 1 (every rank calls; others only barrier):
+    strided vector(total/bl, bl, 512) MPI_Send/MPI_Recv of device buffers,
+    AUTO method (IPC between co-located GPUs), one-way time."""
+    import ctypes
+
+    L = apps_lib()
+    out = []
+    for total, bl in ((4 << 20, 512), (4 << 20, 64), (1 << 20, 8), (1024, 8)):
+        buf = ctypes.create_string_buffer(1024)
+        rc = L.tempi_bench_pingpong(args.pp_iters, total, bl, 512, 0, 0, buf, 1024)
+        if rc != 0:
+            raise SystemExit(f"pingpong failed rc={rc}")
+        if buf.value:
+            r = json.loads(buf.value.decode())
+            r["xgmi_frac"] = round(r["GBps"] / XGMI_LINK_GBS, 4)
+            out.append(r)
+    return {"workload": ("config 3: MPI_Type_vector(total/bl, bl, 512, MPI_BYTE) MPI_Send/MPI_Recv ping-pong "
+                         "rank 0 <-> 1, device buffers, one-way = trimean(round trip)/2"),
+            "link_peak_GBps": XGMI_LINK_GBS, "points": out}
+
+
+def alltoallv(args, world):
+    """Config 5: MPI_BYTE MPI_Alltoallv of device buffers with the
+    reference's random sparse count matrix (seed 101), min over iterations
+    of the max over ranks."""
+    import ctypes
+
+    L = apps_lib()
+    out = []
+    for scale, density in ((100000, 1.0), (100000, 0.5), (1000, 1.0)):
+        buf = ctypes.create_string_buffer(1024)
+        rc = L.tempi_bench_alltoallv(args.a2av_iters, scale, density, 101, 0, 0, buf, 1024)
+        if rc != 0:
+            raise SystemExit(f"alltoallv failed rc={rc}")
+        if buf.value:
+            r = json.loads(buf.value.decode())
+            # every GPU pair has its own xGMI link: the largest pairwise
+            # message bounds the exchange
+            lb = r["max_pairwise_bytes"] / (XGMI_LINK_GBS * 1e9)
+            r["lower_bound_us"] = round(lb * 1e6, 2)
+            r["xgmi_frac"] = round(lb / (r["min_us"] * 1e-6), 4) if r["min_us"] > 0 else None
+            out.append(r)
+    return {"workload": ("config 5: bench-mpi-random-alltoallv, SquareMat::make_random_sparse(size, "
+                         "round(density*size), 1, 10, scale, 101) byte counts, device buffers"),
+            "points": out}
+
+
 def sweep(args, mpi, torch, dev, path):
     """Config-2 sweep: 2D subarray and 3D subarray, block 1 B - 4 KiB."""
     recs = []
@@ -410,6 +477,12 @@ def main():
             h = halo(args, mpi, world)
             if rank == 0:
                 rec["halo"] = h
+        if world > 1 and not args.no_p2p:
+            pp = pingpong(args, world)
+            a2 = alltoallv(args, world)
+            if rank == 0:
+                rec["pingpong"] = pp
+                rec["alltoallv"] = a2
         if rank == 0 and world == 1:
             if not args.no_traffic:
                 tr = run_traffic_passes(args, "pack_kernel")

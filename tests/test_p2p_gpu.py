@@ -79,3 +79,12 @@ def test_neighbor_collectives_device(gpu, ranks, env):
     copies."""
     rc, out = mpi_launch.run(ranks, mpi_launch.py("neighbor.py", "--device"), env=env, timeout=240)
     assert rc == 0 and "RESULT errors=0" in out, out[-3000:]
+
+
+@pytest.mark.parametrize("ranks,scale,density", [(2, 100000, 1.0), (3, 1000, 0.5), (4, 10, 1.0), (4, 100000, 0.25)])
+def test_alltoallv_sparse_app(gpu, ranks, scale, density):
+    """config 5 app: the reference's random sparse matrices, every byte checked"""
+    rc, out = mpi_launch.run(ranks, [os.path.join(LIB, "alltoallv_sparse"), "3", "--scale", str(scale), "--density",
+                                     str(density), "--check"], timeout=240)
+    r = _json_line(out)
+    assert rc == 0 and r["checked"] and r["errors"] == 0, out[-3000:]
