@@ -139,9 +139,15 @@ int main(int argc, char **argv) {
   std::vector<std::vector<Point>> packD, unpackD, packH, unpackH;
   double launch = 0;
   const size_t maxBytes = size_t(1) << maxLog;
+  // the 2-D tables' strided side: vector(bytes/bl, bl, 512) spans
+  // (bytes/bl - 1) * 512 + bl bytes, 2 GiB for the 4 MiB row at bl = 1
+  const int maxTableLog = quick ? 18 : 22;
+  const size_t tableExtent = ((size_t(1) << maxTableLog) - 1) * 512 + 1;
+  const size_t devBytes = std::max(4 * maxBytes, tableExtent);
   char *dev, *dev2, *host;
-  HIPCHECK(hipMalloc(&dev, 4 * maxBytes));
+  HIPCHECK(hipMalloc(&dev, devBytes));
   HIPCHECK(hipMalloc(&dev2, 4 * maxBytes));
+  HIPCHECK(hipMemset(dev, 0, devBytes));
   HIPCHECK(hipHostMalloc(reinterpret_cast<void **>(&host), 4 * maxBytes, hipHostMallocMapped));
   std::vector<char> pageable(maxBytes);
 
@@ -166,7 +172,7 @@ int main(int argc, char **argv) {
       }));
     }
     // 2-D pack tables (device only, rank 0)
-    for (int i = 0; 2 * i + 6 <= (quick ? 18 : 22); ++i) {
+    for (int i = 0; 2 * i + 6 <= maxTableLog; ++i) {
       const int64_t bytes = int64_t(1) << (2 * i + 6);
       std::vector<Point> pd, ud, ph, uh;
       for (int j = 0; j <= 9; ++j) {
@@ -174,6 +180,12 @@ int main(int argc, char **argv) {
         MPI_Datatype t;
         MPI_Type_vector(int(bytes / bl), bl, 512, MPI_BYTE, &t);
         MPI_Type_commit(&t);
+        MPI_Aint tlb, text;
+        MPI_Type_get_true_extent(t, &tlb, &text);
+        if (tlb < 0 || size_t(tlb + text) > devBytes || size_t(bytes) > 4 * maxBytes) {
+          std::fprintf(stderr, "internal error: table point %lld B / %d B exceeds the buffers\n", (long long)bytes, bl);
+          MPI_Abort(MPI_COMM_WORLD, 3);
+        }
         auto pk = [&](char *dst) {
           return [&, dst] {
             int pos = 0;

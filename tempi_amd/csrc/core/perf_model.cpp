@@ -8,6 +8,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <dlfcn.h>
 #include <fstream>
 #include <limits>
 #include <map>
@@ -345,21 +346,40 @@ bool from_json(const std::string &text, SystemPerformance *sp, std::string *err)
 
 static std::string perf_path() { return env.cacheDir + "/perf.json"; }
 
-bool import_system_performance(SystemPerformance *sp) {
-  std::ifstream f(perf_path());
-  if (!f) {
-    LOG_DEBUG("no " << perf_path() << ": AUTO uses the built-in policy");
-    return false;
-  }
+// the model shipped with the library: measured on an MI355X node by
+// apps/measure_system (tempi_amd/data/perf_mi355x.json, found next to
+// lib/libtempi.so as ../data/)
+static std::string shipped_path() {
+  Dl_info info;
+  if (!dladdr(reinterpret_cast<void *>(&shipped_path), &info) || !info.dli_fname) return "";
+  std::string lib = info.dli_fname;
+  const size_t slash = lib.rfind('/');
+  if (slash == std::string::npos) return "";
+  return lib.substr(0, slash) + "/../data/perf_mi355x.json";
+}
+
+static bool load_file(const std::string &path, SystemPerformance *sp) {
+  std::ifstream f(path);
+  if (!f) return false;
   std::stringstream ss;
   ss << f.rdbuf();
   std::string err;
   if (!from_json(ss.str(), sp, &err)) {
-    LOG_ERROR("ignoring " << perf_path() << ": " << err << " (re-run tools/measure_system)");
+    LOG_ERROR("ignoring " << path << ": " << err << " (re-run measure_system)");
     return false;
   }
-  LOG_DEBUG("loaded " << perf_path());
+  LOG_DEBUG("loaded " << path);
   return true;
+}
+
+bool import_system_performance(SystemPerformance *sp) {
+  // this node's own measurement first (TEMPI_CACHE_DIR/perf.json, as in the
+  // reference), then the shipped MI355X model unless TEMPI_NO_SHIPPED_PERF;
+  // with neither, AUTO uses the built-in policy (the reference stops: F10)
+  if (load_file(perf_path(), sp)) return true;
+  if (!std::getenv("TEMPI_NO_SHIPPED_PERF") && load_file(shipped_path(), sp)) return true;
+  LOG_DEBUG("no perf.json: AUTO uses the built-in policy");
+  return false;
 }
 
 bool export_system_performance(const SystemPerformance &sp) {

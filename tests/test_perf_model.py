@@ -99,3 +99,21 @@ def test_iid_accepts_random_eventually():
 
 def test_iid_rejects_periodic():
     assert not iid([1.0, 2.0] * 50, perms=2000)
+
+
+def test_shipped_mi355x_model():
+    """tempi_amd/data/perf_mi355x.json (apps/measure_system on an MI355X box,
+    2 ranks sharing one GPU) parses, round-trips, and has every curve the
+    reference's schema names (measure_system.cpp:100-132)."""
+    import os
+
+    import tempi_amd
+
+    path = os.path.join(tempi_amd.ROOT, "tempi_amd", "data", "perf_mi355x.json")
+    doc = json.load(open(path))
+    for k in ("d2h", "h2d", "intraNodeCpuCpuPingpong", "intraNodeGpuGpuPingpong"):
+        assert len(doc[k]) == 24 and all(p["time"] > 0 for p in doc[k]), k
+    for k in ("packDevice", "unpackDevice", "packHost", "unpackHost"):
+        assert len(doc[k]) == 9 and all(len(r) == 10 for r in doc[k]), k
+    out = ctypes.create_string_buffer(1 << 17)
+    assert L.tempi_perf_roundtrip(open(path, "rb").read(), out, 1 << 17) == 0
