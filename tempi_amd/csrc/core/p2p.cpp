@@ -125,7 +125,7 @@ bool model_choice(int64_t bytes, bool colocated, int64_t block, Method *out) {
   }
   const SystemPerformance &sp = systemPerformance;
   const Opt o = model_oneshot(sp, colocated, bytes, block);
-  const Opt d = model_device(sp, colocated, bytes, block);
+  const Opt d = model_device(sp, colocated, bytes, block, !gpuAwareLibrary);
   const Opt s = model_staged(sp, colocated, bytes, block);
   Method best = Method::ONESHOT;
   double t = o.ok ? o.v : 1e300;

@@ -4,6 +4,7 @@
 #include "env.hpp"
 #include "log.hpp"
 
+#include <algorithm>
 #include <cctype>
 #include <cmath>
 #include <cstdlib>
@@ -109,10 +110,20 @@ Opt model_oneshot(const SystemPerformance &sp, bool colocated, int64_t bytes, in
 }
 
 // /root/reference/src/internal/measure_system.cpp:118-132
-Opt model_device(const SystemPerformance &sp, bool colocated, int64_t bytes, int64_t bl) {
-  return sum({interp_2d_opt(sp.packDevice, bytes, bl),
-              interp_time_opt(colocated ? sp.intraNodeGpuGpuPingpong : sp.interNodeGpuGpuPingpong, bytes),
-              interp_2d_opt(sp.unpackDevice, bytes, bl)});
+// viaTempi: the GPU-GPU ping-pong curve was measured through TEMPI's own IPC
+// transport (apps/measure_system.cpp: no GPU-aware library underneath), so it
+// already contains a contiguous gather and scatter; those (the 512-byte-block
+// column of the tables, i.e. contiguous at stride 512) are taken out before
+// the type's own pack and unpack are added, or the model would count the
+// kernels twice and under-rate the IPC path
+Opt model_device(const SystemPerformance &sp, bool colocated, int64_t bytes, int64_t bl, bool viaTempi) {
+  const Opt pp = interp_time_opt(colocated ? sp.intraNodeGpuGpuPingpong : sp.interNodeGpuGpuPingpong, bytes);
+  Opt transfer = pp;
+  if (viaTempi && pp.ok) {
+    const Opt own = sum({interp_2d_opt(sp.packDevice, bytes, 512), interp_2d_opt(sp.unpackDevice, bytes, 512)});
+    if (own.ok) transfer = Opt::of(std::max(pp.v - own.v, 0.05 * pp.v));
+  }
+  return sum({interp_2d_opt(sp.packDevice, bytes, bl), transfer, interp_2d_opt(sp.unpackDevice, bytes, bl)});
 }
 
 // /root/reference/src/internal/sender.cpp:239-249

@@ -61,7 +61,8 @@ double interp_2d(const std::vector<std::vector<IidTime>> &a, int64_t bytes, int6
 // end-to-end models of one strided message (seconds); unknown when a curve
 // is missing
 Opt model_oneshot(const SystemPerformance &sp, bool colocated, int64_t bytes, int64_t blockLength);
-Opt model_device(const SystemPerformance &sp, bool colocated, int64_t bytes, int64_t blockLength);
+Opt model_device(const SystemPerformance &sp, bool colocated, int64_t bytes, int64_t blockLength,
+                 bool viaTempi = false);
 Opt model_staged(const SystemPerformance &sp, bool colocated, int64_t bytes, int64_t blockLength);
 
 std::string to_json(const SystemPerformance &sp);

@@ -314,6 +314,89 @@ __global__ __launch_bounds__(kBlock) void unpack_kernel(const KArgs<ND> a) {
   unpack_body<W, ND>(a, blockIdx.x, gridDim.x);
 }
 
+// ------------------------------------------------- dense-window gather (pack)
+//
+// Narrow rows packed tightly (block b < 8 bytes or byte-aligned, inner stride
+// s <= kDenseRatio * b): every 64-byte DRAM sector of the strided side holds
+// payload, so reading the whole window costs no more HBM traffic than reading
+// the rows, but the per-word path spends one 1/2/4-byte load instruction per
+// row. Here a workgroup's 4 KiB of packed output covers rows [rl, rh] of one
+// inner segment, whose window (<= 32 KiB + s) the workgroup streams into LDS
+// with 16-byte coalesced loads; each lane then gathers its 16 output bytes
+// from LDS (ds_read_u8) and writes them with one 16-byte store -- the "LDS
+// staging to transpose narrow strided blocks into wide contiguous writes" of
+// the design. A tile whose rows straddle two segments of an outer dimension
+// takes the per-word path (pack_body). The window's aligned 16-byte ends lie
+// in the 16-byte chunks holding the first / last payload byte, and every gap
+// inside it is shorter than 64 bytes between two payload bytes, so no byte
+// outside pages the type already touches is read. Byte-for-byte identical to
+// pack_body (type-map order).
+constexpr int kDenseRatio = 8;
+constexpr int kDenseLds = kBlock * 16 * kDenseRatio + 512;
+constexpr int kDenseMaxBlock = 32;
+
+template <int ND>
+__global__ __launch_bounds__(kBlock) void pack_dense_kernel(const KArgs<ND> a) {
+  __shared__ uint4 win[kDenseLds / 16];
+  const uint32_t blk = blockIdx.x;
+  const uint32_t c0 = blk * kBlock; // first chunk of this tile
+  const uint32_t c1 = min(c0 + uint32_t(kBlock), a.nchunks);
+  // packed bytes of the tile (W = 1: words are bytes)
+  const int64_t qlo = max(int64_t(c0) * 16 - int64_t(a.head), int64_t(0));
+  const int64_t qhi = min(int64_t(c1) * 16 - int64_t(a.head), int64_t(a.nwords)) - 1;
+  const uint32_t rl = mdiv(uint32_t(qlo), a.mwpr), rh = mdiv(uint32_t(qhi), a.mwpr);
+  bool oneSegment = true;
+  if (ND >= 2) oneSegment = mdiv(rl, a.mcnt[0]) == mdiv(rh, a.mcnt[0]);
+  if (!oneSegment) { // uniform: the per-word path for this tile only
+    pack_body<1, ND>(a, blk, gridDim.x);
+    return;
+  }
+  uint32_t dig[ND > 0 ? ND : 1];
+  const int64_t offLo = row_offset<ND>(rl, a, dig);
+  const char *first = a.strided + offLo;
+  const char *A = reinterpret_cast<const char *>(reinterpret_cast<uintptr_t>(first) & ~uintptr_t(15));
+  const int64_t span = int64_t(rh - rl) * a.stride[0] + a.wpr; // bytes from first row to end of last
+  const int64_t winEnd = (first - A) + span;                  // bytes from A
+  const uint32_t nvec = uint32_t((winEnd + 15) / 16);
+  for (uint32_t v = threadIdx.x; v < nvec; v += kBlock)
+    win[v] = ld(reinterpret_cast<const uint4 *>(A) + v, true);
+  __syncthreads();
+  const unsigned char *w8 = reinterpret_cast<const unsigned char *>(win);
+  const uint32_t base = uint32_t(first - A);
+  const uint32_t c = c0 + threadIdx.x;
+  if (c >= c1) return;
+  const int64_t q0 = int64_t(c) * 16 - a.head;
+  const int64_t stride = a.stride[0];
+  if (q0 >= 0 && q0 + 16 <= int64_t(a.nwords)) {
+    uint32_t row = mdiv(uint32_t(q0), a.mwpr);
+    uint32_t w = uint32_t(q0) - row * a.wpr;
+    int64_t idx = int64_t(base) + int64_t(row - rl) * stride + w;
+    union {
+      uint4 v;
+      unsigned char b[16];
+    } out;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      out.b[j] = w8[idx];
+      if (++w == a.wpr) {
+        w = 0;
+        idx += stride - int64_t(a.wpr) + 1;
+      } else {
+        ++idx;
+      }
+    }
+    st(reinterpret_cast<uint4 *>(a.chunk0 + size_t(c) * 16), out.v, kNtPacked);
+  } else { // first / last chunk of the object: only its bytes
+    for (int j = 0; j < 16; ++j) {
+      const int64_t q = q0 + j;
+      if (q < 0 || q >= int64_t(a.nwords)) continue;
+      const uint32_t row = mdiv(uint32_t(q), a.mwpr);
+      const uint32_t w = uint32_t(q) - row * a.wpr;
+      a.chunk0[size_t(c) * 16 + size_t(j)] = w8[int64_t(base) + int64_t(row - rl) * stride + w];
+    }
+  }
+}
+
 // Many objects in ONE launch (e.g. the 26 x nQuants faces of a halo step):
 // the descriptors travel in the kernel arguments (<= 4 KiB), each object owns
 // a contiguous range of workgroups, and a workgroup finds its object with a
@@ -519,9 +602,42 @@ int launch_w(bool pack, char *packed, char *first, const Norm &n, hipStream_t s)
   }
 }
 
+#ifndef TEMPI_DENSE
+#define TEMPI_DENSE 1
+#endif
+// narrow rows packed tightly enough for pack_dense_kernel (see there)
+bool dense_ok(const Norm &n, int w) {
+  if (!TEMPI_DENSE || w >= 8 || n.nd < 1 || n.block > kDenseMaxBlock) return false;
+  const int64_t s = n.str[n.nd - 1], b = n.block; // innermost dimension
+  if (s <= 0 || s > kDenseRatio * b) return false;
+  // outer dimensions: inner segments long enough that few tiles straddle two
+  return n.nd == 1 || n.cnt[n.nd - 1] * b >= 4 * 4096;
+}
+
+template <int ND> int launch_dense_nd(char *packed, char *first, const Norm &n, hipStream_t s) {
+  KArgs<ND> a;
+  uint32_t blocks;
+  make_args<1, ND>(packed, first, n, &a, &blocks);
+  if (blocks == 0) return 0;
+  hipLaunchKernelGGL((pack_dense_kernel<ND>), dim3(blocks), dim3(kBlock), 0, s, a);
+  return int(hipGetLastError());
+}
+
+int launch_dense(char *packed, char *first, const Norm &n, hipStream_t s) {
+  switch (n.nd) {
+  case 1: return launch_dense_nd<1>(packed, first, n, s);
+  case 2: return launch_dense_nd<2>(packed, first, n, s);
+  case 3: return launch_dense_nd<3>(packed, first, n, s);
+  case 4: return launch_dense_nd<4>(packed, first, n, s);
+  case 5: return launch_dense_nd<5>(packed, first, n, s);
+  default: return int(hipErrorInvalidValue);
+  }
+}
+
 int launch_one(bool pack, char *packed, char *first, const Norm &n, hipStream_t s) {
   const int w = word_width(reinterpret_cast<uintptr_t>(packed),
                            reinterpret_cast<uintptr_t>(first), n);
+  if (pack && dense_ok(n, w)) return launch_dense(packed, first, n, s);
   switch (w) {
   case 1: return launch_w<1>(pack, packed, first, n, s);
   case 2: return launch_w<2>(pack, packed, first, n, s);
