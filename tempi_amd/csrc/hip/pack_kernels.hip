@@ -316,13 +316,13 @@ __global__ __launch_bounds__(kBlock) void unpack_kernel(const KArgs<ND> a) {
 
 // ------------------------------------------------- dense-window gather (pack)
 //
-// Narrow rows packed tightly (block b < 8 bytes or byte-aligned, inner stride
+// Narrow rows packed tightly (1- or 2-byte words, inner stride
 // s <= kDenseRatio * b): every 64-byte DRAM sector of the strided side holds
 // payload, so reading the whole window costs no more HBM traffic than reading
 // the rows, but the per-word path spends one 1/2/4-byte load instruction per
 // row. Here a workgroup's 4 KiB of packed output covers rows [rl, rh] of one
-// inner segment, whose window (<= 32 KiB + s) the workgroup streams into LDS
-// with 16-byte coalesced loads; each lane then gathers its 16 output bytes
+// inner segment, whose window the workgroup streams into LDS
+// with 16-byte coalesced loads (<= 16 KiB + s); each lane then gathers its 16 output bytes
 // from LDS (ds_read_u8) and writes them with one 16-byte store -- the "LDS
 // staging to transpose narrow strided blocks into wide contiguous writes" of
 // the design. A tile whose rows straddle two segments of an outer dimension
@@ -331,7 +331,7 @@ __global__ __launch_bounds__(kBlock) void unpack_kernel(const KArgs<ND> a) {
 // inside it is shorter than 64 bytes between two payload bytes, so no byte
 // outside pages the type already touches is read. Byte-for-byte identical to
 // pack_body (type-map order).
-constexpr int kDenseRatio = 8;
+constexpr int kDenseRatio = 4;
 constexpr int kDenseLds = kBlock * 16 * kDenseRatio + 512;
 constexpr int kDenseMaxBlock = 32;
 
@@ -607,7 +607,10 @@ int launch_w(bool pack, char *packed, char *first, const Norm &n, hipStream_t s)
 #endif
 // narrow rows packed tightly enough for pack_dense_kernel (see there)
 bool dense_ok(const Norm &n, int w) {
-  if (!TEMPI_DENSE || w >= 8 || n.nd < 1 || n.block > kDenseMaxBlock) return false;
+  // measured (tools/kbench.cpp): wins for 1- and 2-byte words at stride <= 4
+  // blocks (1 B : 2 B 2.3x, 3 B : 7 B +11%); 4-byte words are already at the
+  // sector bound on the per-word path, and wider windows lose
+  if (!TEMPI_DENSE || w > 2 || n.nd < 1 || n.block > kDenseMaxBlock) return false;
   const int64_t s = n.str[n.nd - 1], b = n.block; // innermost dimension
   if (s <= 0 || s > kDenseRatio * b) return false;
   // outer dimensions: inner segments long enough that few tiles straddle two

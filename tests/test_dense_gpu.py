@@ -1,6 +1,6 @@
-"""The dense-window gather (pack_dense_kernel, pack_kernels.hip): narrow rows
-(block < 8 B or byte-aligned) at inner stride <= 8 x block, taken for
-MPI_Pack. Checked byte-exact against oracle/typemap.c on 1-D, 2-D and 3-D
+"""The dense-window gather (pack_dense_kernel, pack_kernels.hip): 1- and
+2-byte-word rows at inner stride <= 4 x block, taken for MPI_Pack (the other
+shapes here exercise the per-word path beside it). Checked byte-exact against oracle/typemap.c on 1-D, 2-D and 3-D
 shapes, tiles that straddle outer-dimension segments, odd packed positions
 (head / tail chunks), odd buffer alignment and counts > 1; plus a large 1-D
 case through an exact strided torch view."""

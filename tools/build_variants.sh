@@ -12,8 +12,7 @@ build() { # name flags...
     -Wl,-rpath,/opt/rocm/lib &
 }
 build cur
-build nopair -DTEMPI_COPY_PAIR=0
-build cu2 -DTEMPI_COPY_U=2
+build nodense -DTEMPI_DENSE=0
 wait
 g++ -O2 -std=c++17 -Iinclude -o tools/_variants/kbench tools/kbench.cpp -ldl
 g++ -O2 -std=c++17 -Iinclude -o tools/_variants/hbench tools/hbench.cpp -ldl
