@@ -94,6 +94,19 @@ template <> struct Word<16> { typedef uint4 T; };
 #define TEMPI_NT 3
 #endif
 constexpr bool kNtPacked = TEMPI_NT >= 1;
+// word widths (bit W/1: 1, 2, 4, 8) that use the interleaved, LDS-transposed
+// kernels (pack_il_kernel / unpack_il_kernel); measured on MI355X
+// (tools/kbench.cpp, profiles/r01/kbench_il_s2.jsonl): unpack gains for every
+// width (1 B : 2 B x2.4, 24-byte halo rows +20%), pack only for 1-byte words
+#ifndef TEMPI_PACK_IL_WIDTHS
+#define TEMPI_PACK_IL_WIDTHS 1
+#endif
+#ifndef TEMPI_UNPACK_IL_WIDTHS
+#define TEMPI_UNPACK_IL_WIDTHS (1 | 2 | 4 | 8)
+#endif
+constexpr bool il_width(bool pack, int w) {
+  return w <= 8 && ((pack ? TEMPI_PACK_IL_WIDTHS : TEMPI_UNPACK_IL_WIDTHS) & w) != 0;
+}
 template <int W> struct NtStrided { static constexpr bool value = TEMPI_NT == 2 || (TEMPI_NT == 3 && W == 16); };
 
 // chunks each lane keeps in flight per grid-stride step
@@ -217,12 +230,13 @@ __device__ void partial_chunk(uint32_t c, const KArgs<ND> &a) {
   }
 }
 
-// workgroup `blk` of `nblk` working on one object (grid-stride over its chunks)
-template <int W, int ND>
+// workgroup `blk` of `nblk` working on one object (grid-stride over its
+// chunks, U chunks per lane per step; U = 1 makes workgroup blk handle exactly
+// chunks [blk * kBlock, (blk + 1) * kBlock) when nblk covers the object)
+template <int W, int ND, int U = Unroll<W>::U>
 __device__ __forceinline__ void pack_body(const KArgs<ND> &a, uint32_t blk, uint32_t nblk) {
   typedef typename Word<W>::T WT;
   constexpr int CW = 16 / W;
-  constexpr int U = Unroll<W>::U;
   typedef typename ChunkT<W, true>::U Buf;
   const uint32_t step = nblk * (kBlock * U);
   for (uint32_t base = blk * (kBlock * U); base < a.nchunks; base += step) {
@@ -262,11 +276,10 @@ __device__ __forceinline__ void pack_body(const KArgs<ND> &a, uint32_t blk, uint
   }
 }
 
-template <int W, int ND>
+template <int W, int ND, int U = Unroll<W>::U>
 __device__ __forceinline__ void unpack_body(const KArgs<ND> &a, uint32_t blk, uint32_t nblk) {
   typedef typename Word<W>::T WT;
   constexpr int CW = 16 / W;
-  constexpr int U = Unroll<W>::U;
   typedef typename ChunkT<W, false>::U Buf;
   const uint32_t step = nblk * (kBlock * U);
   for (uint32_t base = blk * (kBlock * U); base < a.nchunks; base += step) {
@@ -314,6 +327,87 @@ __global__ __launch_bounds__(kBlock) void unpack_kernel(const KArgs<ND> a) {
   unpack_body<W, ND>(a, blockIdx.x, gridDim.x);
 }
 
+// ------------------------------------------- wave-interleaved scatter (unpack)
+//
+// For 1- and 2-byte words the chunk-per-lane scatter has every store
+// instruction of a wave touch 64 different rows, 16/W rows apart, so each
+// cache line of the strided side is written by 16/W separate instructions.
+// Here the workgroup's 4 KiB of packed input is staged in LDS (one 16-byte
+// load per lane), and store instruction j of a wave writes the 64 CONSECUTIVE
+// words j*64 .. j*64+63 of the wave's 1 KiB: neighbouring rows, so one
+// instruction covers a line and every line is written once. Tiles holding the
+// object's partial first / last chunk take the chunk-per-lane path.
+template <int W, int ND>
+__device__ __forceinline__ void unpack_il_tile(const KArgs<ND> &a, uint32_t tileIdx, uint32_t ntiles) {
+  typedef typename Word<W>::T WT;
+  constexpr int CW = 16 / W;
+  __shared__ uint4 tile[kBlock];
+  const uint32_t c0 = tileIdx * kBlock;
+  const uint32_t c1 = min(c0 + uint32_t(kBlock), a.nchunks);
+  const bool clean = c1 - c0 == uint32_t(kBlock) && int64_t(c0) * CW - a.head >= 0 &&
+                     int64_t(c1) * CW - a.head <= int64_t(a.nwords);
+  if (!clean) { // uniform: this tile's chunks, one per lane
+    unpack_body<W, ND, 1>(a, tileIdx, ntiles);
+    return;
+  }
+  tile[threadIdx.x] = ld(reinterpret_cast<const uint4 *>(a.chunk0 + size_t(c0 + threadIdx.x) * 16), kNtPacked);
+  __syncthreads();
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const WT *src = reinterpret_cast<const WT *>(tile + wave * 64);
+  const uint32_t qw = uint32_t(int64_t(c0 + wave * 64) * CW - a.head); // first word of this wave
+#pragma unroll
+  for (int j = 0; j < CW; ++j) {
+    const uint32_t t = uint32_t(j) * 64 + lane;
+    const uint32_t q = qw + t;
+    const uint32_t row = mdiv(q, a.mwpr);
+    const uint32_t w = q - row * a.wpr;
+    uint32_t dig[ND > 0 ? ND : 1];
+    const int64_t off = row_offset<ND>(row, a, dig) + int64_t(w) * W;
+    st(reinterpret_cast<WT *>(a.strided + off), src[t], false);
+  }
+}
+
+// the gather twin of unpack_il_kernel: load instruction j of a wave reads 64
+// consecutive words (neighbouring rows), the words are transposed through LDS,
+// and every lane writes one 16-byte packed chunk
+template <int W, int ND>
+__device__ __forceinline__ void pack_il_tile(const KArgs<ND> &a, uint32_t tileIdx, uint32_t ntiles) {
+  typedef typename Word<W>::T WT;
+  constexpr int CW = 16 / W;
+  __shared__ uint4 tile[kBlock];
+  const uint32_t c0 = tileIdx * kBlock;
+  const uint32_t c1 = min(c0 + uint32_t(kBlock), a.nchunks);
+  const bool clean = c1 - c0 == uint32_t(kBlock) && int64_t(c0) * CW - a.head >= 0 &&
+                     int64_t(c1) * CW - a.head <= int64_t(a.nwords);
+  if (!clean) { // uniform: this tile's chunks, one per lane
+    pack_body<W, ND, 1>(a, tileIdx, ntiles);
+    return;
+  }
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  WT *dst = reinterpret_cast<WT *>(tile + wave * 64);
+  const uint32_t qw = uint32_t(int64_t(c0 + wave * 64) * CW - a.head);
+  WT v[CW];
+#pragma unroll
+  for (int j = 0; j < CW; ++j) {
+    const uint32_t q = qw + uint32_t(j) * 64 + lane;
+    const uint32_t row = mdiv(q, a.mwpr);
+    const uint32_t w = q - row * a.wpr;
+    uint32_t dig[ND > 0 ? ND : 1];
+    v[j] = *reinterpret_cast<const WT *>(a.strided + row_offset<ND>(row, a, dig) + int64_t(w) * W);
+  }
+#pragma unroll
+  for (int j = 0; j < CW; ++j) dst[uint32_t(j) * 64 + lane] = v[j];
+  __syncthreads();
+  st(reinterpret_cast<uint4 *>(a.chunk0 + size_t(c0 + threadIdx.x) * 16), tile[threadIdx.x], kNtPacked);
+}
+
+template <int W, int ND> __global__ __launch_bounds__(kBlock) void pack_il_kernel(const KArgs<ND> a) {
+  pack_il_tile<W, ND>(a, blockIdx.x, gridDim.x);
+}
+template <int W, int ND> __global__ __launch_bounds__(kBlock) void unpack_il_kernel(const KArgs<ND> a) {
+  unpack_il_tile<W, ND>(a, blockIdx.x, gridDim.x);
+}
+
 // ------------------------------------------------- dense-window gather (pack)
 //
 // Narrow rows packed tightly (1- or 2-byte words, inner stride
@@ -348,7 +442,7 @@ __global__ __launch_bounds__(kBlock) void pack_dense_kernel(const KArgs<ND> a) {
   bool oneSegment = true;
   if (ND >= 2) oneSegment = mdiv(rl, a.mcnt[0]) == mdiv(rh, a.mcnt[0]);
   if (!oneSegment) { // uniform: the per-word path for this tile only
-    pack_body<1, ND>(a, blk, gridDim.x);
+    pack_body<1, ND, 1>(a, blk, gridDim.x);
     return;
   }
   uint32_t dig[ND > 0 ? ND : 1];
@@ -426,6 +520,15 @@ template <int W, int ND>
 __global__ __launch_bounds__(kBlock) void pack_batch_kernel(const BatchArgs<ND> b) {
   const uint32_t i = find_item<ND>(b, blockIdx.x);
   pack_body<W, ND>(b.item[i], blockIdx.x - b.first[i], b.first[i + 1] - b.first[i]);
+}
+
+template <int W, int ND> __global__ __launch_bounds__(kBlock) void pack_il_batch_kernel(const BatchArgs<ND> b) {
+  const uint32_t i = find_item<ND>(b, blockIdx.x);
+  pack_il_tile<W, ND>(b.item[i], blockIdx.x - b.first[i], b.first[i + 1] - b.first[i]);
+}
+template <int W, int ND> __global__ __launch_bounds__(kBlock) void unpack_il_batch_kernel(const BatchArgs<ND> b) {
+  const uint32_t i = find_item<ND>(b, blockIdx.x);
+  unpack_il_tile<W, ND>(b.item[i], blockIdx.x - b.first[i], b.first[i + 1] - b.first[i]);
 }
 
 template <int W, int ND>
@@ -544,6 +647,7 @@ struct Job {
 };
 
 template <int W, int ND> int launch_batch_nd(bool pack, const std::vector<Job> &jobs, hipStream_t s) {
+  const bool il = il_width(pack, W); // il kernels: one 4 KiB tile per workgroup
   BatchArgs<ND> b;
   b.nitems = 0;
   uint32_t total = 0;
@@ -551,7 +655,12 @@ template <int W, int ND> int launch_batch_nd(bool pack, const std::vector<Job> &
     if (!b.nitems) return 0;
     b.first[b.nitems] = total;
     if (total) {
-      if (pack)
+      if (il)
+        if (pack)
+          hipLaunchKernelGGL((pack_il_batch_kernel<W, ND>), dim3(total), dim3(kBlock), 0, s, b);
+        else
+          hipLaunchKernelGGL((unpack_il_batch_kernel<W, ND>), dim3(total), dim3(kBlock), 0, s, b);
+      else if (pack)
         hipLaunchKernelGGL((pack_batch_kernel<W, ND>), dim3(total), dim3(kBlock), 0, s, b);
       else
         hipLaunchKernelGGL((unpack_batch_kernel<W, ND>), dim3(total), dim3(kBlock), 0, s, b);
@@ -564,6 +673,7 @@ template <int W, int ND> int launch_batch_nd(bool pack, const std::vector<Job> &
     KArgs<ND> a;
     uint32_t blocks;
     make_args<W, ND>(j.packed, j.first, j.n, &a, &blocks);
+    if (il) blocks = (a.nchunks + kBlock - 1) / kBlock;
     if (!blocks) continue;
     if (uint64_t(total) + blocks >= (uint64_t(1) << 31))
       if (int e = flush()) return e;
@@ -637,10 +747,44 @@ int launch_dense(char *packed, char *first, const Norm &n, hipStream_t s) {
   }
 }
 
+template <int W, int ND> int launch_il_nd(bool pack, char *packed, char *first, const Norm &n, hipStream_t s) {
+  KArgs<ND> a;
+  uint32_t blocks;
+  make_args<W, ND>(packed, first, n, &a, &blocks);
+  blocks = (a.nchunks + kBlock - 1) / kBlock; // one tile per workgroup, no grid-stride
+  if (blocks == 0) return 0;
+  if (pack)
+    hipLaunchKernelGGL((pack_il_kernel<W, ND>), dim3(blocks), dim3(kBlock), 0, s, a);
+  else
+    hipLaunchKernelGGL((unpack_il_kernel<W, ND>), dim3(blocks), dim3(kBlock), 0, s, a);
+  return int(hipGetLastError());
+}
+
+template <int W> int launch_il(bool pack, char *packed, char *first, const Norm &n, hipStream_t s) {
+  switch (n.nd) {
+  case 0: return launch_il_nd<W, 0>(pack, packed, first, n, s);
+  case 1: return launch_il_nd<W, 1>(pack, packed, first, n, s);
+  case 2: return launch_il_nd<W, 2>(pack, packed, first, n, s);
+  case 3: return launch_il_nd<W, 3>(pack, packed, first, n, s);
+  case 4: return launch_il_nd<W, 4>(pack, packed, first, n, s);
+  case 5: return launch_il_nd<W, 5>(pack, packed, first, n, s);
+  default: return int(hipErrorInvalidValue);
+  }
+}
+
 int launch_one(bool pack, char *packed, char *first, const Norm &n, hipStream_t s) {
   const int w = word_width(reinterpret_cast<uintptr_t>(packed),
                            reinterpret_cast<uintptr_t>(first), n);
   if (pack && dense_ok(n, w)) return launch_dense(packed, first, n, s);
+  if (il_width(pack, w)) {
+    switch (w) {
+    case 1: return launch_il<1>(pack, packed, first, n, s);
+    case 2: return launch_il<2>(pack, packed, first, n, s);
+    case 4: return launch_il<4>(pack, packed, first, n, s);
+    case 8: return launch_il<8>(pack, packed, first, n, s);
+    default: break;
+    }
+  }
   switch (w) {
   case 1: return launch_w<1>(pack, packed, first, n, s);
   case 2: return launch_w<2>(pack, packed, first, n, s);

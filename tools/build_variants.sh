@@ -12,7 +12,7 @@ build() { # name flags...
     -Wl,-rpath,/opt/rocm/lib &
 }
 build cur
-build nodense -DTEMPI_DENSE=0
+build base -DTEMPI_DENSE=0 -DTEMPI_PACK_IL_WIDTHS=0 -DTEMPI_UNPACK_IL_WIDTHS=0
 wait
 g++ -O2 -std=c++17 -Iinclude -o tools/_variants/kbench tools/kbench.cpp -ldl
 g++ -O2 -std=c++17 -Iinclude -o tools/_variants/hbench tools/hbench.cpp -ldl

@@ -11,7 +11,7 @@ step tests
 timeout -k 10 900 python -u -m pytest tests -m gpu -q --maxfail=8 --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1
 rc=$?; tail -3 $O/gpu_tests.log; [ $rc -eq 0 ] || exit $rc
 step kbench
-SHAPES="512:2097152:1024 4096:262144:4160 64:16777216:128 8:67108864:16 24:512:2386944:512:4608 1:268435456:2 3:89478485:7 1073741824"
+SHAPES="512:2097152:1024 4096:262144:4160 64:16777216:128 8:67108864:16 24:512:2386944:512:4608 1:268435456:2 3:89478485:7 2:134217728:4 1:134217728:8 4:67108864:16 1073741824"
 rm -f $O/kbench.jsonl $O/pingpong.jsonl
 for v in $(ls tools/_variants/ | sed -n 's/^libtempi_hip_\(.*\)\.so$/\1/p'); do
   timeout -k 10 120 tools/_variants/kbench tools/_variants/libtempi_hip_$v.so 10 $SHAPES >> $O/kbench.jsonl || exit 5
