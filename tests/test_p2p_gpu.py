@@ -51,9 +51,12 @@ def test_pingpong_nd(gpu, method, total, block):
     (1, "48", {"TEMPI_NO_DIRECT": "1"}, []), (2, "40", {"TEMPI_FAULT_IPC_OPEN": "1"}, []),
     (4, "32", {"TEMPI_DATATYPE_ONESHOT": "1"}, []),
     (1, "48", {}, ["--neighbor"]), (2, "40", {}, ["--neighbor"]), (4, "32", {}, ["--neighbor"]),
-    (3, "30", {}, ["--neighbor"])])
+    (3, "30", {}, ["--neighbor"]),
+    # x split (the 24-byte faces cross ranks, as at 8 ranks on (2, 2, 2))
+    (2, "64 16 16", {}, []), (4, "64 64 16", {}, []), (4, "64 64 16", {}, ["--neighbor"]),
+    (4, "64 64 16", {"TEMPI_DATATYPE_STAGED": "1"}, [])])
 def test_halo_exchange_content(gpu, ranks, grid, env, extra):
-    rc, out = mpi_launch.run(ranks, [os.path.join(LIB, "halo_exchange"), "2", grid, "--quants", "2", "--check"] + extra,
+    rc, out = mpi_launch.run(ranks, [os.path.join(LIB, "halo_exchange"), "2"] + grid.split() + ["--quants", "2", "--check"] + extra,
                              env=env, timeout=300)
     r = _json_line(out)
     assert rc == 0 and r["checked"] and r["errors"] == 0, out[-3000:]
