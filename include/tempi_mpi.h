@@ -27,6 +27,8 @@
  *   MPI_Wait         src/wait.cpp:11-16              progress TEMPI requests
  *   MPI_Waitall      (not interposed: F8)            progress TEMPI requests
  *   MPI_Test         (not interposed: F8)            progress TEMPI requests
+ *   MPI_Testall / _Testany / _Waitany / _Testsome / _Waitsome / MPI_Request_free
+ *                    (not interposed: F8)            understand TEMPI requests
  *   MPI_Alltoallv    src/alltoallv.cpp:14-68         device-buffer alltoallv
  *   MPI_Neighbor_alltoallw  src/neighbor_alltoallw.cpp:11-18 (-> internal/
  *                    neighbor_alltoallw.cpp:19-77)   per-edge Isend/Irecv when
@@ -74,6 +76,14 @@ int MPI_Irecv(void *buf, int count, MPI_Datatype datatype, int source, int tag, 
 int MPI_Wait(MPI_Request *request, MPI_Status *status);
 int MPI_Waitall(int count, MPI_Request array_of_requests[], MPI_Status array_of_statuses[]);
 int MPI_Test(MPI_Request *request, int *flag, MPI_Status *status);
+int MPI_Testall(int count, MPI_Request array_of_requests[], int *flag, MPI_Status array_of_statuses[]);
+int MPI_Testany(int count, MPI_Request array_of_requests[], int *index, int *flag, MPI_Status *status);
+int MPI_Waitany(int count, MPI_Request array_of_requests[], int *index, MPI_Status *status);
+int MPI_Testsome(int incount, MPI_Request array_of_requests[], int *outcount, int array_of_indices[],
+                 MPI_Status array_of_statuses[]);
+int MPI_Waitsome(int incount, MPI_Request array_of_requests[], int *outcount, int array_of_indices[],
+                 MPI_Status array_of_statuses[]);
+int MPI_Request_free(MPI_Request *request);
 int MPI_Alltoallv(const void *sendbuf, const int sendcounts[], const int sdispls[],
                   MPI_Datatype sendtype, void *recvbuf, const int recvcounts[], const int rdispls[],
                   MPI_Datatype recvtype, MPI_Comm comm);

@@ -123,3 +123,135 @@ TEMPI_EXPORT int MPI_Waitall(int count, MPI_Request requests[], MPI_Status statu
   }
   return err;
 }
+
+// ---------------------------------------------------------------------------
+// The rest of the completion family. The reference interposes none of these
+// (SURVEY F8), so a TEMPI request handed to them would reach the library;
+// here they understand TEMPI requests and keep TEMPI operations moving.
+
+namespace {
+
+bool any_tempi(int count, const MPI_Request *requests) {
+  for (int i = 0; i < count; ++i)
+    if (p2p::is_tempi_request(requests[i])) return true;
+  return false;
+}
+
+// one request, non-blocking: 1 = completed (request released, status set)
+int test_one(MPI_Request *r, MPI_Status *st, int *err) {
+  int flag = 0;
+  const int rc = p2p::is_tempi_request(*r) ? p2p::test(r, &flag, st) : next.MPI_Test(r, &flag, st);
+  if (rc != MPI_SUCCESS) {
+    *err = rc;
+    return 1;
+  }
+  return flag;
+}
+
+MPI_Status *at(MPI_Status *statuses, int i) {
+  return statuses == MPI_STATUSES_IGNORE ? MPI_STATUS_IGNORE : &statuses[i];
+}
+
+} // namespace
+
+TEMPI_EXPORT int MPI_Testall(int count, MPI_Request requests[], int *flag, MPI_Status statuses[]) {
+  resolve_next();
+  if (!state.active || (!any_tempi(count, requests) && !p2p::busy()))
+    return next.MPI_Testall(count, requests, flag, statuses);
+  p2p::progress();
+  // all or nothing: look first, complete only when every request is done
+  for (int i = 0; i < count; ++i) {
+    if (requests[i] == MPI_REQUEST_NULL) continue;
+    int done = 0;
+    if (p2p::is_tempi_request(requests[i]))
+      done = p2p::peek(requests[i]);
+    else
+      next.MPI_Request_get_status(requests[i], &done, MPI_STATUS_IGNORE);
+    if (!done) {
+      *flag = 0;
+      return MPI_SUCCESS;
+    }
+  }
+  int err = MPI_SUCCESS;
+  for (int i = 0; i < count; ++i) {
+    if (requests[i] == MPI_REQUEST_NULL) continue;
+    int e = MPI_SUCCESS;
+    test_one(&requests[i], at(statuses, i), &e);
+    if (e != MPI_SUCCESS) err = MPI_ERR_IN_STATUS;
+  }
+  *flag = 1;
+  return err;
+}
+
+TEMPI_EXPORT int MPI_Testany(int count, MPI_Request requests[], int *index, int *flag, MPI_Status *status) {
+  resolve_next();
+  if (!state.active || (!any_tempi(count, requests) && !p2p::busy()))
+    return next.MPI_Testany(count, requests, index, flag, status);
+  p2p::progress();
+  bool anyActive = false;
+  for (int i = 0; i < count; ++i) {
+    if (requests[i] == MPI_REQUEST_NULL) continue;
+    anyActive = true;
+    int err = MPI_SUCCESS;
+    if (test_one(&requests[i], status, &err)) {
+      *index = i;
+      *flag = 1;
+      return err;
+    }
+  }
+  *index = MPI_UNDEFINED;
+  *flag = anyActive ? 0 : 1;
+  return MPI_SUCCESS;
+}
+
+TEMPI_EXPORT int MPI_Waitany(int count, MPI_Request requests[], int *index, MPI_Status *status) {
+  resolve_next();
+  if (!state.active || (!any_tempi(count, requests) && !p2p::busy()))
+    return next.MPI_Waitany(count, requests, index, status);
+  for (;;) {
+    int flag = 0;
+    const int rc = MPI_Testany(count, requests, index, &flag, status);
+    if (rc != MPI_SUCCESS || flag) return rc;
+  }
+}
+
+TEMPI_EXPORT int MPI_Testsome(int incount, MPI_Request requests[], int *outcount, int indices[],
+                              MPI_Status statuses[]) {
+  resolve_next();
+  if (!state.active || (!any_tempi(incount, requests) && !p2p::busy()))
+    return next.MPI_Testsome(incount, requests, outcount, indices, statuses);
+  p2p::progress();
+  bool anyActive = false;
+  int n = 0, err = MPI_SUCCESS;
+  for (int i = 0; i < incount; ++i) {
+    if (requests[i] == MPI_REQUEST_NULL) continue;
+    anyActive = true;
+    int e = MPI_SUCCESS;
+    if (test_one(&requests[i], at(statuses, n), &e)) {
+      if (e != MPI_SUCCESS) err = MPI_ERR_IN_STATUS;
+      indices[n++] = i;
+    }
+  }
+  *outcount = anyActive ? n : MPI_UNDEFINED;
+  return err;
+}
+
+TEMPI_EXPORT int MPI_Waitsome(int incount, MPI_Request requests[], int *outcount, int indices[],
+                              MPI_Status statuses[]) {
+  resolve_next();
+  if (!state.active || (!any_tempi(incount, requests) && !p2p::busy()))
+    return next.MPI_Waitsome(incount, requests, outcount, indices, statuses);
+  for (;;) {
+    const int rc = MPI_Testsome(incount, requests, outcount, indices, statuses);
+    if (rc != MPI_SUCCESS || *outcount != 0) return rc;
+  }
+}
+
+TEMPI_EXPORT int MPI_Request_free(MPI_Request *request) {
+  resolve_next();
+  if (state.active && p2p::is_tempi_request(*request)) {
+    p2p::release(request);
+    return MPI_SUCCESS;
+  }
+  return next.MPI_Request_free(request);
+}

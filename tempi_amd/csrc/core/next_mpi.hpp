@@ -27,6 +27,12 @@
   X(MPI_Waitall)                                                               \
   X(MPI_Test)                                                                  \
   X(MPI_Testsome)                                                              \
+  X(MPI_Testall)                                                               \
+  X(MPI_Testany)                                                               \
+  X(MPI_Waitany)                                                               \
+  X(MPI_Waitsome)                                                              \
+  X(MPI_Request_free)                                                          \
+  X(MPI_Request_get_status)                                                    \
   X(MPI_Alltoallv)                                                             \
   X(MPI_Neighbor_alltoallv)                                                    \
   X(MPI_Neighbor_alltoallw)                                                    \

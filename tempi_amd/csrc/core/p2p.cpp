@@ -255,6 +255,7 @@ struct Op {
   int device = 0;
   MPI_Request lib = MPI_REQUEST_NULL;          // outstanding library request
   bool watched = false;                        // in libWatch
+  bool detached = false;                       // MPI_Request_free'd: dropped when done
   bool done = false;
 };
 
@@ -805,6 +806,7 @@ struct LibIrecvOp : Op {
 constexpr uint32_t kHandleSpace = 1u << 26;
 uint32_t nextHandle = 1;
 std::unordered_map<uint32_t, std::unique_ptr<Op>> active;
+std::vector<uint32_t> detachedOps; // freed by the application, still running
 
 MPI_Request add(std::unique_ptr<Op> op) {
   while (active.count(nextHandle) || nextHandle == 0) nextHandle = (nextHandle + 1) % kHandleSpace;
@@ -855,6 +857,7 @@ void finalize() {
     }
   }
   active.clear();
+  detachedOps.clear();
   libWatch.clear();
   for (auto &b : batches)
     if (b->event) tempi_hip_event_destroy(b->event);
@@ -967,6 +970,24 @@ bool is_tempi_request(MPI_Request r) {
   return h != 0 && h < kHandleSpace && active.count(h);
 }
 
+bool peek(MPI_Request r) {
+  auto it = active.find(uint32_t(r));
+  return it != active.end() && it->second->done;
+}
+
+void release(MPI_Request *req) {
+  auto it = active.find(uint32_t(*req));
+  if (it != active.end()) {
+    if (it->second->done) {
+      active.erase(it);
+    } else {
+      it->second->detached = true;
+      detachedOps.push_back(uint32_t(*req));
+    }
+  }
+  *req = MPI_REQUEST_NULL;
+}
+
 bool progress(bool full) {
   bool moved = false;
   counters.progress_passes++;
@@ -1068,6 +1089,19 @@ bool progress(bool full) {
   //    is about to wait for them (light passes from MPI_Isend / MPI_Irecv
   //    only queue them, so a burst of receives shares one launch)
   if (!pendingUnpack.empty() && (full || pendingUnpack.size() >= kMaxPending)) flush_list(pendingUnpack, false);
+  // 4. operations the application freed with MPI_Request_free
+  if (!detachedOps.empty()) {
+    size_t w = 0;
+    for (uint32_t h : detachedOps) {
+      auto it = active.find(h);
+      if (it == active.end()) continue;
+      if (it->second->done)
+        active.erase(it);
+      else
+        detachedOps[w++] = h;
+    }
+    detachedOps.resize(w);
+  }
   return moved;
 }
 

@@ -66,6 +66,10 @@ int irecv(void *buf, int count, MPI_Datatype dt, int source, int tag, MPI_Comm c
           const Route &route);
 
 bool is_tempi_request(MPI_Request r);
+// complete? (no progress, no release: MPI_Testall's all-or-nothing rule)
+bool peek(MPI_Request r);
+// MPI_Request_free: the operation finishes in the background; *req = NULL
+void release(MPI_Request *req);
 // drive every TEMPI operation one step; returns true if anything moved.
 // full = false (from MPI_Isend / MPI_Irecv) leaves arrived messages' unpacks
 // queued so that a burst shares one launch; waits use full = true

@@ -71,7 +71,7 @@ class MPI:
         for n in ("BYTE", "CHAR", "SHORT", "INT", "LONG", "FLOAT", "DOUBLE", "PACKED", "INT64_T",
                   "UINT8_T", "COMM_WORLD", "COMM_SELF", "REQUEST_NULL", "ORDER_C", "ORDER_FORTRAN",
                   "SUCCESS", "ERR_TRUNCATE", "ANY_SOURCE", "ANY_TAG", "SUM", "MAX", "MIN",
-                  "DATATYPE_NULL", "PROC_NULL"):
+                  "DATATYPE_NULL", "PROC_NULL", "UNDEFINED"):
             setattr(self, n, self.const("MPI_" + n))
         self.STATUS_IGNORE = ctypes.c_void_p(self.const("MPI_STATUS_IGNORE"))
         self.STATUSES_IGNORE = ctypes.c_void_p(self.const("MPI_STATUSES_IGNORE"))
@@ -273,6 +273,43 @@ class MPI:
         arr = (self.Request * max(n, 1))(*reqs)
         self._call("MPI_Waitall", n, arr, self.STATUSES_IGNORE)
         return list(arr)[:n]
+
+    def _reqs(self, reqs):
+        return (self.Request * max(len(reqs), 1))(*reqs)
+
+    def Testall(self, reqs):
+        arr, flag = self._reqs(reqs), ctypes.c_int(0)
+        self._call("MPI_Testall", len(reqs), arr, ctypes.byref(flag), self.STATUSES_IGNORE)
+        return bool(flag.value), list(arr)[:len(reqs)]
+
+    def Testany(self, reqs):
+        arr, idx, flag = self._reqs(reqs), ctypes.c_int(-1), ctypes.c_int(0)
+        self._call("MPI_Testany", len(reqs), arr, ctypes.byref(idx), ctypes.byref(flag), self.STATUS_IGNORE)
+        return idx.value, bool(flag.value), list(arr)[:len(reqs)]
+
+    def Waitany(self, reqs):
+        arr, idx = self._reqs(reqs), ctypes.c_int(-1)
+        self._call("MPI_Waitany", len(reqs), arr, ctypes.byref(idx), self.STATUS_IGNORE)
+        return idx.value, list(arr)[:len(reqs)]
+
+    def _some(self, fn, reqs):
+        n = len(reqs)
+        arr, out = self._reqs(reqs), ctypes.c_int(0)
+        idx = (ctypes.c_int * max(n, 1))()
+        self._call(fn, n, arr, ctypes.byref(out), idx, self.STATUSES_IGNORE)
+        k = out.value
+        return (list(idx)[:k] if k >= 0 else None), list(arr)[:n]
+
+    def Testsome(self, reqs):
+        return self._some("MPI_Testsome", reqs)
+
+    def Waitsome(self, reqs):
+        return self._some("MPI_Waitsome", reqs)
+
+    def Request_free(self, req):
+        r = self.Request(req)
+        self._call("MPI_Request_free", ctypes.byref(r))
+        return r.value
 
     def Test(self, req):
         r = self.Request(req)

@@ -27,6 +27,13 @@ def test_neighbor_collectives_host(ranks):
     assert rc == 0 and "RESULT errors=0" in out, out[-3000:]
 
 
+def test_completion_family_host():
+    """MPI_Testall/Testany/Waitany/Testsome/Waitsome/Request_free through the
+    interposer with host buffers (library requests only)."""
+    rc, out = mpi_launch.run(2, mpi_launch.py("completion.py"), timeout=180)
+    assert rc == 0 and "RESULT errors=0" in out, out[-3000:]
+
+
 def test_mpi_under_torchrun():
     """bench.py's multi-GPU launch is torch.distributed.run, not mpiexec: the
     ranks are wired into one MPI job by tempi_amd.pmi (PMI-1 server)."""

@@ -91,3 +91,11 @@ def test_alltoallv_sparse_app(gpu, ranks, scale, density):
                                      str(density), "--check"], timeout=240)
     r = _json_line(out)
     assert rc == 0 and r["checked"] and r["errors"] == 0, out[-3000:]
+
+
+@pytest.mark.parametrize("method", ["AUTO", "ONESHOT", "IPC", "STAGED"])
+def test_completion_family_device(gpu, method):
+    """TEMPI device requests mixed with library requests through
+    MPI_Testall / Testany / Waitany / Testsome / Waitsome / Request_free"""
+    rc, out = mpi_launch.run(2, mpi_launch.py("completion.py", "--device"), env=METHODS[method], timeout=240)
+    assert rc == 0 and "RESULT errors=0" in out, out[-3000:]
