@@ -88,33 +88,16 @@ int tagUb = 32767;
 bool gpuAwareLibrary = false;
 int64_t ipcMinBytes = 4 * 1024;
 
-// IPC slabs lent to a receiver, released when its ack arrives. The
-// descriptor is kept here: it is the buffer of a send whose request was freed
-// at once, and the ack proves it was delivered.
+// acks the sender is waiting for before reusing a device slab
 struct PendingAck {
+  MPI_Request req;
   Slab *slab;
   int peer;     // world rank of the receiver
-  int tag;      // ctrlComm tag for a host re-send of the bytes (NACK)
+  int tag;      // ack tag
   int64_t bytes;
+  int code;     // received ack payload
 };
-std::unordered_map<uint64_t, PendingAck> pendingAcks; // by slab id (unique in this process)
-std::unordered_map<uint64_t, std::unique_ptr<char[]>> pendingDescs; // the descriptors in flight
-
-// Acks arrive in ONE mailbox: a single receive (any source, kAckTag) on the
-// private communicator, re-posted after every ack, instead of one receive per
-// lent slab in every MPI_Testsome. Payload: slab id, code (0 = pulled,
-// 1 = could not map it: send the bytes through the host on the descriptor's
-// re-send tag).
-constexpr int kAckTag = 0;
-struct AckMsg {
-  uint64_t slabId;
-  int64_t code;
-};
-AckMsg mailbox{};
-MPI_Request mailboxReq = MPI_REQUEST_NULL;
-void post_mailbox() {
-  next.MPI_Irecv(&mailbox, int(sizeof mailbox), MPI_BYTE, MPI_ANY_SOURCE, kAckTag, ctrlComm, &mailboxReq);
-}
+std::vector<std::unique_ptr<PendingAck>> pendingAcks; // stable addresses: Irecv targets
 
 // peer slabs mapped into this process: (world rank, slab id) -> base
 std::map<std::pair<int, uint64_t>, void *> ipcOpen;
@@ -212,11 +195,14 @@ void *peer_pointer(const IpcDesc &d) {
   return p;
 }
 
-// to the sender's mailbox (16 bytes: sent eagerly, so the blocking send
-// returns at once)
+// ack payload: 0 = pulled, release the slab; 1 = could not map it, send the
+// bytes through the host on (ctrlComm, ackTag)
+int ackCodes[2] = {0, 1};
+
 void send_ack(const IpcDesc &d, int code = 0) {
-  AckMsg m{d.slabId, code};
-  next.MPI_Send(&m, int(sizeof m), MPI_BYTE, d.senderWorld, kAckTag, ctrlComm);
+  MPI_Request r;
+  next.MPI_Isend(&ackCodes[code], 1, MPI_INT, d.senderWorld, d.ackTag, ctrlComm, &r);
+  MPI_Request_free(&r);
 }
 
 // ---------------------------------------------------------------- operations
@@ -435,21 +421,17 @@ struct IsendOp : Op {
       desc.bytes = bytes;
       desc.senderWorld = state.worldRank;
       desc.senderPid = int32_t(getpid());
-      desc.ackTag = 1 + int32_t(dslab->id % uint32_t(tagUb - 1)); // never the mailbox tag
+      desc.ackTag = int32_t(dslab->id % uint32_t(tagUb));
       desc.rawPtr = reinterpret_cast<uint64_t>(dslab->dev);
       std::memcpy(desc.handle, slab_ipc_handle(dslab), sizeof desc.handle);
-      // the slab is reused once the receiver acknowledges (mailbox); the send
-      // itself is complete now: the user's bytes are in the slab
+      // the slab is reused once the receiver acknowledges (private comm)
       const int peer = topology::world_rank(comm, dest);
-      pendingAcks[dslab->id] = PendingAck{dslab, peer, desc.ackTag, bytes};
-      std::unique_ptr<char[]> copy(new char[sizeof desc]);
-      std::memcpy(copy.get(), &desc, sizeof desc);
-      MPI_Request r;
-      next.MPI_Isend(copy.get(), int(sizeof desc), MPI_PACKED, dest, tag, comm, &r);
-      MPI_Request_free(&r);
-      pendingDescs[dslab->id] = std::move(copy);
+      pendingAcks.push_back(std::unique_ptr<PendingAck>(new PendingAck{MPI_REQUEST_NULL, dslab, peer, desc.ackTag, bytes, -1}));
+      PendingAck &pa = *pendingAcks.back();
+      next.MPI_Irecv(&pa.code, 1, MPI_INT, peer, desc.ackTag, ctrlComm, &pa.req);
       dslab = nullptr;
-      done = true;
+      next.MPI_Isend(&desc, int(sizeof desc), MPI_PACKED, dest, tag, comm, &lib);
+      watch(this);
       break;
     }
     default:
@@ -836,7 +818,8 @@ MPI_Request add(std::unique_ptr<Op> op) {
 
 // scratch for progress()
 std::vector<MPI_Request> pollReqs;
-std::vector<Op *> pollOps;   // nullptr: the ack mailbox
+std::vector<Op *> pollOps;   // nullptr: a pending ack
+std::vector<size_t> pollAck; // index into pendingAcks
 std::vector<int> pollIdx;
 std::vector<MPI_Status> pollSt;
 
@@ -855,9 +838,6 @@ void init() {
   int *ub = nullptr;
   MPI_Comm_get_attr(MPI_COMM_WORLD, MPI_TAG_UB, &ub, &flag);
   if (flag && ub) tagUb = *ub;
-  pendingAcks.clear();
-  pendingDescs.clear();
-  post_mailbox();
 }
 
 void finalize() {
@@ -886,13 +866,9 @@ void finalize() {
     progress();
     if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(30)) {
       LOG_WARN(pendingAcks.size() << " IPC slab(s) never acknowledged; abandoning");
+      for (auto &pa : pendingAcks) MPI_Cancel(&pa->req);
       pendingAcks.clear();
     }
-  }
-  pendingDescs.clear();
-  if (mailboxReq != MPI_REQUEST_NULL) {
-    MPI_Cancel(&mailboxReq);
-    next.MPI_Wait(&mailboxReq, MPI_STATUS_IGNORE);
   }
   for (void *e : eventPool) tempi_hip_event_destroy(e);
   eventPool.clear();
@@ -1052,13 +1028,16 @@ bool progress(bool full) {
   // 2. every outstanding library request in one MPI_Testsome
   pollReqs.clear();
   pollOps.clear();
+  pollAck.clear();
   for (Op *op : libWatch) {
     pollReqs.push_back(op->lib);
     pollOps.push_back(op);
+    pollAck.push_back(0);
   }
-  if (mailboxReq != MPI_REQUEST_NULL) {
-    pollReqs.push_back(mailboxReq);
+  for (size_t i = 0; i < pendingAcks.size(); ++i) {
+    pollReqs.push_back(pendingAcks[i]->req);
     pollOps.push_back(nullptr);
+    pollAck.push_back(i);
   }
   if (!pollReqs.empty()) {
     const int n = int(pollReqs.size());
@@ -1067,14 +1046,14 @@ bool progress(bool full) {
     int outcount = 0;
     next.MPI_Testsome(n, pollReqs.data(), &outcount, pollIdx.data(), pollSt.data());
     if (outcount == MPI_UNDEFINED) outcount = 0;
-    bool mail = false;
+    std::vector<size_t> ackedSlots;
     for (int k = 0; k < outcount; ++k) {
       const size_t i = size_t(pollIdx[size_t(k)]);
       if (Op *op = pollOps[i]) {
         op->lib = MPI_REQUEST_NULL;
         op->lib_done(pollSt[size_t(k)]);
       } else {
-        mail = true;
+        ackedSlots.push_back(pollAck[i]);
       }
       moved = true;
     }
@@ -1088,29 +1067,21 @@ bool progress(bool full) {
       }
       libWatch.resize(w);
     }
-    // acks: drain the mailbox (several may be queued), re-posting it each time
-    while (mail) {
-      mailboxReq = MPI_REQUEST_NULL;
-      auto it = pendingAcks.find(mailbox.slabId);
-      if (it == pendingAcks.end()) {
-        LOG_WARN("ack for an unknown slab " << mailbox.slabId);
-      } else {
-        PendingAck &pa = it->second;
-        if (mailbox.code == 1) { // the receiver could not map the slab: send the bytes through the host
-          mark_ipc_broken(pa.peer);
-          Slab *h = pinned_pool().get(size_t(pa.bytes), pa.slab->device);
-          gpu::check(tempi_hip_memcpy(h->host, pa.slab->dev, size_t(pa.bytes)), "ipc fallback D2H");
-          next.MPI_Send(h->host, int(pa.bytes), MPI_PACKED, pa.peer, pa.tag, ctrlComm); // receive already posted
-          pinned_pool().put(h);
-        }
-        device_pool().put(pa.slab);
-        pendingDescs.erase(mailbox.slabId);
-        pendingAcks.erase(it);
+    // release acknowledged slabs (highest index first keeps indices valid)
+    std::sort(ackedSlots.rbegin(), ackedSlots.rend());
+    for (size_t a : ackedSlots) {
+      PendingAck &pa = *pendingAcks[a];
+      pa.req = MPI_REQUEST_NULL;
+      if (pa.code == 1) { // the receiver could not map the slab: send the bytes through the host
+        mark_ipc_broken(pa.peer);
+        Slab *h = pinned_pool().get(size_t(pa.bytes), pa.slab->device);
+        gpu::check(tempi_hip_memcpy(h->host, pa.slab->dev, size_t(pa.bytes)), "ipc fallback D2H");
+        next.MPI_Send(h->host, int(pa.bytes), MPI_PACKED, pa.peer, pa.tag, ctrlComm); // receive already posted
+        pinned_pool().put(h);
       }
-      post_mailbox();
-      int flag = 0;
-      next.MPI_Test(&mailboxReq, &flag, MPI_STATUS_IGNORE);
-      mail = flag != 0;
+      device_pool().put(pa.slab);
+      pendingAcks[a] = std::move(pendingAcks.back());
+      pendingAcks.pop_back();
     }
   }
   counters.ns_testsome += now_ns() - t0;
