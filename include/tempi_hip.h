@@ -142,11 +142,6 @@ int tempi_hip_memset_async(void *dst, int value, size_t n, void *stream);
 int tempi_hip_ipc_get_handle(void *handle_out, void *devptr);
 int tempi_hip_ipc_open_handle(void **devptr, const void *handle);
 int tempi_hip_ipc_close_handle(void *devptr);
-/* inter-process events (same 64-byte handles): the sender records one after
-   filling a slab, the receiver's stream waits on it (tempi_hip_stream_wait_event)
-   before reading the slab, so no host round trip orders the two */
-int tempi_hip_ipc_event_create(void **event, void *handle_out);
-int tempi_hip_ipc_event_open(void **event, const void *handle);
 
 const char *tempi_hip_error_string(int status);
 

@@ -72,7 +72,6 @@ void SlabPool::put(Slab *s) {
 void SlabPool::release_all() {
   std::lock_guard<std::mutex> g(mtx_);
   for (Slab *s : all_) {
-    if (s->ipcEvent) tempi_hip_event_destroy(s->ipcEvent);
     if (kind_ == DEVICE)
       tempi_hip_free(s->dev);
     else
@@ -100,19 +99,6 @@ const unsigned char *slab_ipc_handle(Slab *s) {
     s->ipcReady = true;
   }
   return s->ipc;
-}
-
-void *slab_ipc_event(Slab *s) {
-  if (s->ipcEventState == 0) {
-    int cur = 0;
-    tempi_hip_get_device(&cur);
-    if (cur != s->device) tempi_hip_set_device(s->device);
-    const int e = tempi_hip_ipc_event_create(&s->ipcEvent, s->ipcEventHandle);
-    if (cur != s->device) tempi_hip_set_device(cur);
-    if (e != 0) LOG_DEBUG("no inter-process events: " << tempi_hip_error_string(e));
-    s->ipcEventState = e == 0 ? 1 : -1;
-  }
-  return s->ipcEventState == 1 ? s->ipcEvent : nullptr;
 }
 
 } // namespace tempi

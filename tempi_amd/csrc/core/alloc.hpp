@@ -28,11 +28,6 @@ struct Slab {
   uint32_t id = 0;      // process-unique
   bool ipcReady = false;
   unsigned char ipc[64]; // IPC handle of `dev` (device pools)
-  // inter-process event recorded after each fill (IPC transport); 0 = not
-  // made yet, 1 = ready, -1 = the runtime refused (no early descriptors)
-  int ipcEventState = 0;
-  void *ipcEvent = nullptr;
-  unsigned char ipcEventHandle[64];
 };
 
 class SlabPool {
@@ -60,9 +55,5 @@ SlabPool &pinned_pool();
 
 // IPC handle for a device slab (computed once)
 const unsigned char *slab_ipc_handle(Slab *s);
-// the slab's inter-process event (made once), or nullptr when unsupported
-void *slab_ipc_event(Slab *s);
-// the slab's inter-process event (made once), or nullptr when unsupported
-void *slab_ipc_event(Slab *s);
 
 } // namespace tempi

@@ -42,21 +42,11 @@ struct IpcDesc {
   int32_t senderWorld;
   int32_t senderPid;
   int32_t ackTag;
-  int32_t flags; // kDescEvent: `event` names the slab's fill; wait on it
+  int32_t pad;
   uint64_t rawPtr; // valid inside the sender's own process
   unsigned char handle[TEMPI_HIP_IPC_HANDLE_BYTES];
-  unsigned char event[TEMPI_HIP_IPC_HANDLE_BYTES]; // inter-process event handle
 };
-static_assert(sizeof(IpcDesc) == 192, "descriptor size");
-constexpr int32_t kDescEvent = 1;
-
-// EARLY descriptors (IPC between processes): the descriptor leaves as soon
-// as the gather is LAUNCHED, carrying an inter-process event recorded after
-// it; the receiver's stream waits on that event before its scatter reads the
-// slab. The sender's own completion still waits for the gather (the user's
-// buffer is read by it). Without inter-process events the descriptor leaves
-// when the gather has completed, as before. TEMPI_NO_EARLY_DESC turns it off.
-bool earlyDesc = true;
+static_assert(sizeof(IpcDesc) == 128, "descriptor size");
 
 // DIRECT (a send to this same process): the descriptor names the sender's
 // object itself, and the receiver copies it strided -> strided into its own
@@ -205,24 +195,6 @@ void *peer_pointer(const IpcDesc &d) {
   return p;
 }
 
-// the sender slab's inter-process event (early descriptors), opened once per
-// slab; nullptr when it cannot be (the receive then asks for a host re-send)
-std::map<std::pair<int, uint64_t>, void *> ipcEvents;
-void *peer_event(const IpcDesc &d) {
-  auto key = std::make_pair(int(d.senderWorld), d.slabId);
-  auto it = ipcEvents.find(key);
-  if (it != ipcEvents.end()) return it->second;
-  void *ev = nullptr;
-  const int e = tempi_hip_ipc_event_open(&ev, d.event);
-  if (e != 0) {
-    LOG_WARN("cannot open rank " << d.senderWorld << "'s event: " << tempi_hip_error_string(e));
-    mark_ipc_broken(d.senderWorld);
-    return nullptr;
-  }
-  ipcEvents[key] = ev;
-  return ev;
-}
-
 // ack payload: 0 = pulled, release the slab; 1 = could not map it, send the
 // bytes through the host on (ctrlComm, ackTag)
 int ackCodes[2] = {0, 1};
@@ -279,7 +251,6 @@ struct Op {
   virtual void status(MPI_Status *s) const = 0;
   virtual void stalled() {}                    // waited on and still incomplete after a pass
   virtual void peer_done() {}                  // (direct sends) the receiver's copy ran
-  virtual void launched(void *stream) {}       // its queued GPU work was just launched on `stream`
   bool queued = false;                         // GPU work not launched yet
   int device = 0;
   MPI_Request lib = MPI_REQUEST_NULL;          // outstanding library request
@@ -314,7 +285,6 @@ struct PendingList {
     int dev;
   };
   std::vector<Stage> stages;
-  std::vector<std::pair<void *, int>> waits; // (inter-process event, device): waited on before the launches
   bool empty() const { return ops.empty(); }
   size_t size() const { return ops.size(); }
   void clear() {
@@ -324,7 +294,6 @@ struct PendingList {
     copies.clear();
     copyDev.clear();
     stages.clear();
-    waits.clear();
   }
   void add_items(const Op *op, const Packer &pk, void *packed, const void *origin, int64_t count) {
     pk.items(packed, origin, count, items);
@@ -378,17 +347,12 @@ void flush_list(PendingList &list, bool pack) {
     if (cur != dev) tempi_hip_set_device(dev);
     counters.batches++;
     counters.batched_items += nitems + ncopies;
-    for (const auto &w : list.waits) // peers' gathers these scatters read
-      if (w.second == dev) gpu::check(tempi_hip_stream_wait_event(s, w.first), "wait on peer event");
     if (nitems)
       gpu::check(pack ? tempi_hip_pack_batch(items, int(nitems), s) : tempi_hip_unpack_batch(items, int(nitems), s),
                  pack ? "batched pack" : "batched unpack");
     if (ncopies) gpu::check(tempi_hip_copy_batch(copies, int(ncopies), s), "batched direct copy");
     for (const PendingList::Stage &st : list.stages)
       if (st.dev == dev) gpu::check(tempi_hip_memcpy_async(st.dst, st.src, st.n, s), "staged D2H");
-    if (pack)
-      for (Op *op : list.ops)
-        if (op->device == dev) op->launched(s);
     auto b = std::make_shared<GpuBatch>();
     b->device = dev;
     b->event = get_event();
@@ -438,48 +402,7 @@ struct IsendOp : Op {
     pendingPack.queue(this);
   }
 
-  // early descriptor state (IPC between processes)
-  bool early = false, gpuDone = false, libDone = false;
-
-  void post_desc(void *event) {
-    desc.magic[0] = kMagic0;
-    desc.magic[1] = kMagic1;
-    desc.slabId = dslab->id;
-    desc.offset = 0;
-    desc.bytes = bytes;
-    desc.senderWorld = state.worldRank;
-    desc.senderPid = int32_t(getpid());
-    desc.ackTag = int32_t(dslab->id % uint32_t(tagUb));
-    desc.flags = event ? kDescEvent : 0;
-    desc.rawPtr = reinterpret_cast<uint64_t>(dslab->dev);
-    std::memcpy(desc.handle, slab_ipc_handle(dslab), sizeof desc.handle);
-    if (event) std::memcpy(desc.event, dslab->ipcEventHandle, sizeof desc.event);
-    // the slab is reused once the receiver acknowledges (private comm)
-    const int peer = topology::world_rank(comm, dest);
-    pendingAcks.push_back(std::unique_ptr<PendingAck>(new PendingAck{MPI_REQUEST_NULL, dslab, peer, desc.ackTag, bytes, -1}));
-    PendingAck &pa = *pendingAcks.back();
-    next.MPI_Irecv(&pa.code, 1, MPI_INT, peer, desc.ackTag, ctrlComm, &pa.req);
-    dslab = nullptr;
-    next.MPI_Isend(&desc, int(sizeof desc), MPI_PACKED, dest, tag, comm, &lib);
-    watch(this);
-  }
-
-  void launched(void *stream) override {
-    if (method != Method::IPC || !earlyDesc) return;
-    if (topology::world_rank(comm, dest) == state.worldRank) return; // one process: stream order suffices
-    void *ev = slab_ipc_event(dslab);
-    if (!ev) return;
-    gpu::check(tempi_hip_event_record(ev, stream), "ipc event record");
-    early = true;
-    post_desc(ev);
-  }
-
   void gpu_done() override { // packed: hand it to the library
-    if (early) { // the descriptor left at launch; the user's buffer is read now
-      gpuDone = true;
-      done = libDone;
-      return;
-    }
     switch (method) {
     case Method::ONESHOT:
     case Method::STAGED:
@@ -490,19 +413,32 @@ struct IsendOp : Op {
       next.MPI_Isend(dslab->dev, int(bytes), MPI_PACKED, dest, tag, comm, &lib);
       watch(this);
       break;
-    case Method::IPC:
-      post_desc(nullptr);
+    case Method::IPC: {
+      desc.magic[0] = kMagic0;
+      desc.magic[1] = kMagic1;
+      desc.slabId = dslab->id;
+      desc.offset = 0;
+      desc.bytes = bytes;
+      desc.senderWorld = state.worldRank;
+      desc.senderPid = int32_t(getpid());
+      desc.ackTag = int32_t(dslab->id % uint32_t(tagUb));
+      desc.rawPtr = reinterpret_cast<uint64_t>(dslab->dev);
+      std::memcpy(desc.handle, slab_ipc_handle(dslab), sizeof desc.handle);
+      // the slab is reused once the receiver acknowledges (private comm)
+      const int peer = topology::world_rank(comm, dest);
+      pendingAcks.push_back(std::unique_ptr<PendingAck>(new PendingAck{MPI_REQUEST_NULL, dslab, peer, desc.ackTag, bytes, -1}));
+      PendingAck &pa = *pendingAcks.back();
+      next.MPI_Irecv(&pa.code, 1, MPI_INT, peer, desc.ackTag, ctrlComm, &pa.req);
+      dslab = nullptr;
+      next.MPI_Isend(&desc, int(sizeof desc), MPI_PACKED, dest, tag, comm, &lib);
+      watch(this);
       break;
+    }
     default:
       break;
     }
   }
   void lib_done(const MPI_Status &) override {
-    if (early) {
-      libDone = true;
-      done = gpuDone;
-      return;
-    }
     if (dslab) device_pool().put(dslab);
     if (hslab) pinned_pool().put(hslab);
     dslab = hslab = nullptr;
@@ -769,12 +705,6 @@ struct IrecvOp : Op {
       desc = d;
       if (d.bytes > bytes) LOG_FATAL("message truncated: " << d.bytes << " B into " << bytes);
       void *base = peer_pointer(d);
-      // an early descriptor: the slab is ready once the sender's event fires
-      void *ready = nullptr;
-      if (base && (d.flags & kDescEvent) && d.senderPid != int32_t(getpid())) {
-        ready = peer_event(d);
-        if (!ready) base = nullptr;
-      }
       if (!base) { // cannot map the sender's slab: ask for the bytes via the host
         ipc = false;
         fallback = true;
@@ -785,7 +715,6 @@ struct IrecvOp : Op {
       }
       const char *peer = static_cast<const char *>(base) + d.offset;
       elems = size ? d.bytes / size : 0;
-      if (ready) pendingUnpack.waits.push_back({ready, device});
       pendingUnpack.add_items(this, packer, const_cast<char *>(peer), origin, elems);
     } else {
       if (int64_t(n) > bytes) LOG_FATAL("message truncated: " << n << " B into " << bytes);
@@ -899,7 +828,6 @@ std::vector<MPI_Status> pollSt;
 void init() {
   gpuAwareLibrary = std::getenv("TEMPI_MPI_GPU_AWARE") != nullptr;
   directEnabled = std::getenv("TEMPI_NO_DIRECT") == nullptr;
-  earlyDesc = std::getenv("TEMPI_NO_EARLY_DESC") == nullptr;
   if (const char *s = std::getenv("TEMPI_EARLY_FLUSH")) earlyFlush = size_t(std::max(1, std::atoi(s)));
   directShared.clear();
   systemPerformanceLoaded = import_system_performance(&systemPerformance);
@@ -946,8 +874,6 @@ void finalize() {
   eventPool.clear();
   for (auto &kv : ipcOpen) tempi_hip_ipc_close_handle(kv.second);
   ipcOpen.clear();
-  for (auto &kv : ipcEvents) tempi_hip_event_destroy(kv.second);
-  ipcEvents.clear();
   if (ctrlComm != MPI_COMM_NULL) MPI_Comm_free(&ctrlComm);
   device_pool().release_all();
   pinned_pool().release_all();
@@ -1148,8 +1074,6 @@ bool progress(bool full) {
       pa.req = MPI_REQUEST_NULL;
       if (pa.code == 1) { // the receiver could not map the slab: send the bytes through the host
         mark_ipc_broken(pa.peer);
-        // (an early descriptor may have left before the gather finished)
-        gpu::check(tempi_hip_stream_synchronize(gpu::stream(pa.slab->device)), "ipc fallback sync");
         Slab *h = pinned_pool().get(size_t(pa.bytes), pa.slab->device);
         gpu::check(tempi_hip_memcpy(h->host, pa.slab->dev, size_t(pa.bytes)), "ipc fallback D2H");
         next.MPI_Send(h->host, int(pa.bytes), MPI_PACKED, pa.peer, pa.tag, ctrlComm); // receive already posted

@@ -147,32 +147,6 @@ int tempi_hip_ipc_open_handle(void **devptr, const void *handle) {
 }
 int tempi_hip_ipc_close_handle(void *devptr) { RET(hipIpcCloseMemHandle(devptr)); }
 
-int tempi_hip_ipc_event_create(void **event, void *handle_out) {
-  static_assert(sizeof(hipIpcEventHandle_t) <= TEMPI_HIP_IPC_HANDLE_BYTES, "ipc event handle size");
-  hipEvent_t e = nullptr;
-  hipError_t r = hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventInterprocess);
-  if (r != hipSuccess) RET(r);
-  hipIpcEventHandle_t h;
-  std::memset(&h, 0, sizeof h);
-  r = hipIpcGetEventHandle(&h, e);
-  if (r != hipSuccess) {
-    (void)hipEventDestroy(e);
-    RET(r);
-  }
-  std::memset(handle_out, 0, TEMPI_HIP_IPC_HANDLE_BYTES);
-  std::memcpy(handle_out, &h, sizeof h);
-  *event = e;
-  return 0;
-}
-int tempi_hip_ipc_event_open(void **event, const void *handle) {
-  hipIpcEventHandle_t h;
-  std::memcpy(&h, handle, sizeof h);
-  hipEvent_t e = nullptr;
-  hipError_t r = hipIpcOpenEventHandle(&e, h);
-  *event = e;
-  RET(r);
-}
-
 const char *tempi_hip_error_string(int status) {
   return hipGetErrorString(static_cast<hipError_t>(status));
 }
