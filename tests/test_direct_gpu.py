@@ -283,3 +283,22 @@ def test_self_direct_into_library_receives(mpi, gpu):
             typezoo.free(mpi, *it_)
     finally:
         typezoo.free(mpi, *tt)
+
+
+def test_self_any_source_any_tag_and_type_freed_in_flight(mpi, gpu):
+    """A direct send matched by an MPI_ANY_SOURCE / MPI_ANY_TAG device receive,
+    with both datatypes freed (MPI_Type_free) while the operations are still
+    in flight: the transport keeps its own reference to the type record."""
+    import torch
+
+    recipe, count = "subarray(C,[40,38,512],[30,3,24],[5,3,24],byte)", 2
+    tm, origin, tt, src, dst, exp = _setup(mpi, gpu, recipe, count, 41)
+    t = tt[0]
+    t2, temps2, basic2 = typezoo.build(mpi, recipe)
+    r = mpi.Irecv(dst.data_ptr() + origin, count, t2, mpi.ANY_SOURCE, mpi.ANY_TAG)
+    s = mpi.Isend(src.data_ptr() + origin, count, t, 0, 77)
+    typezoo.free(mpi, *tt)
+    typezoo.free(mpi, t2, temps2, basic2)
+    assert mpi.Waitall([r, s]) == [mpi.REQUEST_NULL] * 2
+    torch.cuda.synchronize()
+    assert np.array_equal(dst.cpu().numpy(), exp)
