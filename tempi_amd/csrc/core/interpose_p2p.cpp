@@ -24,6 +24,7 @@ TEMPI_EXPORT int MPI_Send(const void *buf, int count, MPI_Datatype datatype, int
   p2p::Route route;
   if (!p2p::handles(buf, count, datatype, dest, &route)) {
     counters.lib_sends++;
+    if (state.active && p2p::send_gated(comm, dest)) p2p::drain_sends(comm, dest); // keep send order
     return next.MPI_Send(buf, count, datatype, dest, tag, comm);
   }
   counters.sends++;
@@ -57,7 +58,11 @@ TEMPI_EXPORT int MPI_Isend(const void *buf, int count, MPI_Datatype datatype, in
   p2p::Route route;
   if (p2p::handles(buf, count, datatype, dest, &route))
     return p2p::isend(buf, count, datatype, dest, tag, comm, request, route);
-  if (state.active) p2p::progress(false);
+  if (state.active) {
+    p2p::progress(false);
+    if (p2p::send_gated(comm, dest)) // behind a send still gathering: keep send order
+      return p2p::isend_host(buf, count, datatype, dest, tag, comm, request);
+  }
   counters.lib_sends++;
   return next.MPI_Isend(buf, count, datatype, dest, tag, comm, request);
 }

@@ -251,7 +251,10 @@ struct Op {
   virtual void status(MPI_Status *s) const = 0;
   virtual void stalled() {}                    // waited on and still incomplete after a pass
   virtual void peer_done() {}                  // (direct sends) the receiver's copy ran
+  virtual void post() {}                       // (sends) hand the message to the library
   bool queued = false;                         // GPU work not launched yet
+  bool ready = false;                          // (sends in a gate) post() may run
+  bool posted = false;                         // (sends) post() has run
   int device = 0;
   MPI_Request lib = MPI_REQUEST_NULL;          // outstanding library request
   bool watched = false;                        // in libWatch
@@ -266,6 +269,67 @@ void watch(Op *op) {
   if (!op->watched && op->lib != MPI_REQUEST_NULL) {
     op->watched = true;
     libWatch.push_back(op);
+  }
+}
+
+// MPI's non-overtaking rule: sends from this process to one (comm, dest) reach
+// the library in call order. An IsendOp reaches it only when its gather has
+// run (gpu_done), so while one is still gathering, any later send to the same
+// peer -- even one that could go at once (a direct descriptor, a
+// library-packed type, a host buffer) -- queues behind it in that peer's gate
+// and is posted when everything ahead of it has been. Gates are keyed by
+// (comm, dest); ops never leave a gate before posting, and nothing waits on a
+// receiver to post, so a gate always drains. (The reference lets such sends
+// overtake; SURVEY F-list.)
+struct SendGate {
+  std::vector<Op *> q;
+  size_t head = 0;
+  bool busy() const { return head < q.size(); }
+};
+std::unordered_map<uint64_t, SendGate> gates;
+size_t gatedOps = 0; // ops in any gate: 0 means every send may post at once
+
+uint64_t gate_key(MPI_Comm comm, int dest) {
+  uint64_t c = 0;
+  std::memcpy(&c, &comm, std::min(sizeof comm, sizeof c));
+  return (c * 0x9e3779b97f4a7c15ull) ^ uint64_t(uint32_t(dest));
+}
+
+bool gate_busy(uint64_t key) {
+  if (!gatedOps) return false;
+  auto it = gates.find(key);
+  return it != gates.end() && it->second.busy();
+}
+
+void gate_enter(uint64_t key, Op *op) {
+  gates[key].q.push_back(op);
+  ++gatedOps;
+}
+
+// post every op at the head of the gate that may go
+void gate_advance(uint64_t key) {
+  SendGate &g = gates[key];
+  while (g.busy() && g.q[g.head]->ready) {
+    Op *op = g.q[g.head++];
+    --gatedOps;
+    op->posted = true;
+    op->post();
+  }
+  if (!g.busy()) {
+    g.q.clear();
+    g.head = 0;
+  }
+}
+
+// a send that could post at once: now, unless an earlier send to the same
+// peer is still gathering
+void post_or_queue(uint64_t key, Op *op) {
+  op->ready = true;
+  if (gate_busy(key)) {
+    gate_enter(key, op);
+  } else {
+    op->posted = true;
+    op->post();
   }
 }
 
@@ -384,10 +448,14 @@ struct IsendOp : Op {
   Slab *dslab = nullptr, *hslab = nullptr;
   IpcDesc desc{};
 
+  uint64_t key;
+
   IsendOp(const TypeRecord *r, const char *o, int c, MPI_Datatype d, int de, int t, MPI_Comm cm, int dev,
           Method m, int64_t b)
-      : rec(r->ref()), origin(o), count(c), dest(de), tag(t), dt(d), comm(cm), method(m), bytes(b) {
+      : rec(r->ref()), origin(o), count(c), dest(de), tag(t), dt(d), comm(cm), method(m), bytes(b),
+        key(gate_key(cm, de)) {
     device = dev;
+    gate_enter(key, this);
     if (method == Method::ONESHOT) {
       hslab = pinned_pool().get(size_t(bytes), device);
       pendingPack.add_items(this, *rec->packer, hslab->dev, origin, count);
@@ -402,7 +470,11 @@ struct IsendOp : Op {
     pendingPack.queue(this);
   }
 
-  void gpu_done() override { // packed: hand it to the library
+  void gpu_done() override { // packed: hand it to the library (in order)
+    ready = true;
+    gate_advance(key);
+  }
+  void post() override {
     switch (method) {
     case Method::ONESHOT:
     case Method::STAGED:
@@ -482,18 +554,27 @@ struct IsendDirectOp : Op {
     desc.device = dev;
     desc.first = reinterpret_cast<uint64_t>(o + rec->desc.start);
     desc.desc = flat;
+    this->dest = dest;
+    this->tag = tag;
+    this->comm = comm;
+    post_or_queue(gate_key(comm, dest), this);
+  }
+  int dest, tag;
+  MPI_Comm comm;
+  void post() override {
     // the library may hold a send to this same process open until its
     // receive is posted (MPICH does), so the send's completion cannot wait for
     // it: the request is released now and the descriptor outlives it in `sh`
     MPI_Request sreq;
-    next.MPI_Isend(&desc, int(sizeof desc), MPI_PACKED, dest, tag, comm, &sreq);
+    next.MPI_Isend(&sh->desc, int(sizeof sh->desc), MPI_PACKED, dest, tag, comm, &sreq);
     MPI_Request_free(&sreq);
+    maybe_done();
   }
   ~IsendDirectOp() override {
     if (sh) sh->sender = nullptr;
   }
   void maybe_done() {
-    done = sh->state == DirectShared::DONE || (sh->state == DirectShared::PACKED && packDone);
+    done = posted && (sh->state == DirectShared::DONE || (sh->state == DirectShared::PACKED && packDone));
   }
   void gpu_done() override {
     packDone = true;
@@ -744,11 +825,39 @@ struct IrecvOp : Op {
 struct LibIsendOp : Op {
   std::vector<char> buf;
   MPI_Datatype dt;
-  LibIsendOp(const void *b, int c, MPI_Datatype d, int dest, int tag, MPI_Comm comm) : dt(d) {
+  int n = 0, dest, tag;
+  MPI_Comm comm;
+  LibIsendOp(const void *b, int c, MPI_Datatype d, int de, int t, MPI_Comm cm) : dt(d), dest(de), tag(t), comm(cm) {
     buf.resize(size_t(std::max<int64_t>(pack_size(c, d, comm), 1)));
-    int pos = 0;
-    tempi::pack(b, c, d, buf.data(), int(buf.size()), &pos, comm);
-    next.MPI_Isend(buf.data(), pos, MPI_PACKED, dest, tag, comm, &lib);
+    tempi::pack(b, c, d, buf.data(), int(buf.size()), &n, comm);
+    post_or_queue(gate_key(comm, dest), this);
+  }
+  void post() override {
+    next.MPI_Isend(buf.data(), n, MPI_PACKED, dest, tag, comm, &lib);
+    watch(this);
+  }
+  void lib_done(const MPI_Status &) override { done = true; }
+  void status(MPI_Status *s) const override {
+    if (s != MPI_STATUS_IGNORE) {
+      s->MPI_ERROR = MPI_SUCCESS;
+      MPI_Status_set_elements(s, dt, 0);
+    }
+  }
+};
+
+// a host-buffer send queued behind a gathering send to the same peer
+struct HostIsendOp : Op {
+  const void *buf;
+  int count, dest, tag;
+  MPI_Datatype dt;
+  MPI_Comm comm;
+  HostIsendOp(const void *b, int c, MPI_Datatype d, int de, int t, MPI_Comm cm)
+      : buf(b), count(c), dest(de), tag(t), dt(d), comm(cm) {
+    ready = true;
+    gate_enter(gate_key(comm, dest), this);
+  }
+  void post() override {
+    next.MPI_Isend(buf, count, dt, dest, tag, comm, &lib);
     watch(this);
   }
   void lib_done(const MPI_Status &) override { done = true; }
@@ -858,6 +967,8 @@ void finalize() {
   }
   active.clear();
   detachedOps.clear();
+  gates.clear();
+  gatedOps = 0;
   libWatch.clear();
   for (auto &b : batches)
     if (b->event) tempi_hip_event_destroy(b->event);
@@ -963,6 +1074,19 @@ int irecv(void *buf, int count, MPI_Datatype dt, int source, int tag, MPI_Comm c
   if (pendingUnpack.size() >= earlyFlush) flush_list(pendingUnpack, false);
   counters.ns_irecv += now_ns() - t0;
   return MPI_SUCCESS;
+}
+
+bool send_gated(MPI_Comm comm, int dest) { return gate_busy(gate_key(comm, dest)); }
+
+int isend_host(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Comm comm, MPI_Request *req) {
+  counters.lib_sends++;
+  *req = add(std::make_unique<HostIsendOp>(buf, count, dt, dest, tag, comm));
+  return MPI_SUCCESS;
+}
+
+void drain_sends(MPI_Comm comm, int dest) {
+  const uint64_t key = gate_key(comm, dest);
+  while (gate_busy(key)) progress();
 }
 
 bool is_tempi_request(MPI_Request r) {

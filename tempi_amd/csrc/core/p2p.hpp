@@ -65,6 +65,14 @@ int isend(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Co
 int irecv(void *buf, int count, MPI_Datatype dt, int source, int tag, MPI_Comm comm, MPI_Request *req,
           const Route &route);
 
+// Send order for sends TEMPI does not carry (host buffers): while an earlier
+// TEMPI send to (comm, dest) is still gathering, a library send there would
+// overtake it. send_gated() says so; isend_host() then queues the host send
+// behind it (a TEMPI request) and drain_sends() waits until it has left.
+bool send_gated(MPI_Comm comm, int dest);
+int isend_host(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Comm comm, MPI_Request *req);
+void drain_sends(MPI_Comm comm, int dest);
+
 bool is_tempi_request(MPI_Request r);
 // complete? (no progress, no release: MPI_Testall's all-or-nothing rule)
 bool peek(MPI_Request r);

@@ -27,6 +27,13 @@ def test_neighbor_collectives_host(ranks):
     assert rc == 0 and "RESULT errors=0" in out, out[-3000:]
 
 
+@pytest.mark.parametrize("n", [1, 2])
+def test_send_order_host(n):
+    """the send-order program on host buffers (library path end to end)"""
+    rc, out = mpi_launch.run(n, mpi_launch.py("order.py"), timeout=180)
+    assert rc == 0 and "RESULT errors=0" in out, out[-3000:]
+
+
 def test_completion_family_host():
     """MPI_Testall/Testany/Waitany/Testsome/Waitsome/Request_free through the
     interposer with host buffers (library requests only)."""

@@ -99,3 +99,16 @@ def test_completion_family_device(gpu, method):
     MPI_Testall / Testany / Waitany / Testsome / Waitsome / Request_free"""
     rc, out = mpi_launch.run(2, mpi_launch.py("completion.py", "--device"), env=METHODS[method], timeout=240)
     assert rc == 0 and "RESULT errors=0" in out, out[-3000:]
+
+
+@pytest.mark.parametrize("n,method", [(2, "AUTO"), (2, "ONESHOT"), (2, "IPC"), (2, "STAGED"), (1, "AUTO"),
+                                      (1, "NO_DIRECT")])
+def test_send_order_across_routes(gpu, n, method):
+    """MPI non-overtaking: a gathered strided send, a host send, a
+    library-packed irregular send and another strided send to one peer with
+    one tag are matched in call order (a blocking host send behind them too)"""
+    env = dict(METHODS.get(method, {}))
+    if method == "NO_DIRECT":
+        env["TEMPI_NO_DIRECT"] = "1"
+    rc, out = mpi_launch.run(n, mpi_launch.py("order.py", "--device"), env=env, timeout=240)
+    assert rc == 0 and "RESULT errors=0" in out, out[-3000:]
