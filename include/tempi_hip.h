@@ -113,6 +113,9 @@ int tempi_hip_pointer_info(const void *p, tempi_hip_ptrinfo *out);
 
 /* streams and events (opaque handles) */
 int tempi_hip_stream_create(void **stream); /* non-blocking stream */
+/* non-blocking stream at the device's highest priority (high != 0) or the
+   default one */
+int tempi_hip_stream_create_priority(void **stream, int high);
 int tempi_hip_stream_destroy(void *stream);
 int tempi_hip_stream_synchronize(void *stream);
 int tempi_hip_stream_wait_event(void *stream, void *event);

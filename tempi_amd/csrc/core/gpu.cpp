@@ -3,6 +3,8 @@
 
 #include "log.hpp"
 
+#include <algorithm>
+#include <cstdlib>
 #include <mutex>
 #include <vector>
 
@@ -12,9 +14,19 @@ namespace gpu {
 namespace {
 int nDevices = 0;
 std::mutex mtx;
-std::vector<void *> streams;
+std::vector<void *> streams; // [device * kMaxLanes + lane]
 std::vector<void *> evStart, evStop;
+int nLanes = 3;
+bool highPriority = true; // TEMPI_NO_STREAM_PRIORITY
 } // namespace
+
+int lanes() { return nLanes; }
+
+void choose_lanes(int ranksOnNode) {
+  nLanes = ranksOnNode > nDevices ? 1 : 3;
+  if (const char *e = std::getenv("TEMPI_STREAMS")) nLanes = std::min(kMaxLanes, std::max(1, std::atoi(e)));
+  LOG_DEBUG("stream lanes: " << nLanes);
+}
 
 bool available() { return nDevices > 0; }
 
@@ -23,7 +35,9 @@ void init() {
   if (tempi_hip_device_count(&n) != 0) n = 0;
   nDevices = n;
   std::lock_guard<std::mutex> g(mtx);
-  streams.assign(size_t(n), nullptr);
+  streams.assign(size_t(n) * kMaxLanes, nullptr);
+  nLanes = 1; // until choose_lanes()
+  highPriority = std::getenv("TEMPI_NO_STREAM_PRIORITY") == nullptr;
   LOG_DEBUG("visible GPUs: " << n);
 }
 
@@ -52,19 +66,22 @@ Ptr classify(const void *p) {
   return r;
 }
 
-void *stream(int device) {
-  if (device < 0 || device >= nDevices) return nullptr;
+void *stream(int device, int lane) {
+  if (device < 0 || device >= nDevices || lane < 0 || lane >= kMaxLanes) return nullptr;
+  const size_t i = size_t(device) * kMaxLanes + size_t(lane);
   std::lock_guard<std::mutex> g(mtx);
-  if (!streams[size_t(device)]) {
+  if (!streams[i]) {
     int cur = 0;
     tempi_hip_get_device(&cur);
     if (cur != device) tempi_hip_set_device(device);
     void *s = nullptr;
-    check(tempi_hip_stream_create(&s), "stream create");
+    // with several lanes, lane 0 (gathers whose packed bytes a peer is
+    // waiting for) outranks the scatter lanes
+    check(tempi_hip_stream_create_priority(&s, nLanes > 1 && lane == 0 && highPriority), "stream create");
     if (cur != device) tempi_hip_set_device(cur);
-    streams[size_t(device)] = s;
+    streams[i] = s;
   }
-  return streams[size_t(device)];
+  return streams[i];
 }
 
 void profiling_events(int device, void **start, void **stop) {

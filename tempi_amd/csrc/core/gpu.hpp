@@ -28,8 +28,18 @@ struct Ptr {
 };
 Ptr classify(const void *p);
 
-// the TEMPI stream of a device (created on first use); nullptr on failure
-void *stream(int device);
+// the TEMPI stream of a device (created on first use); nullptr on failure.
+// lane 0 carries every synchronous operation and the batched gathers; the
+// transport spreads batched scatters / copies over lanes 1 .. lanes()-1 so
+// that one batch's tail overlaps the next batch's start.
+constexpr int kMaxLanes = 4;
+void *stream(int device, int lane = 0);
+// lanes in use: TEMPI_STREAMS (1 .. kMaxLanes) if set, else 3 -- or 1 when
+// the node runs more ranks than it has visible GPUs, i.e. ranks share a GPU
+// (concurrent kernels from several processes' lanes measured 15-50 % slower
+// than one stream each; alone on its GPU, 3 lanes are 12 % faster: DESIGN §6)
+int lanes();
+void choose_lanes(int ranksOnNode); // at MPI_Init, after topology::init
 
 // a timing event pair owned by TEMPI for `device` (created on first use)
 void profiling_events(int device, void **start, void **stop);

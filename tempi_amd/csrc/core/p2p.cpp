@@ -239,6 +239,7 @@ struct Op;
 struct GpuBatch {
   void *event = nullptr;
   int device = 0;
+  int lane = 0;
   bool complete = false;
   std::vector<Op *> ops; // whose GPU work this batch carries (alive until gpu_done)
 };
@@ -349,6 +350,7 @@ struct PendingList {
     int dev;
   };
   std::vector<Stage> stages;
+  bool afterPack = false; // (unpack list) holds a scatter of a gather still on lane 0
   bool empty() const { return ops.empty(); }
   size_t size() const { return ops.size(); }
   void clear() {
@@ -358,6 +360,7 @@ struct PendingList {
     copies.clear();
     copyDev.clear();
     stages.clear();
+    afterPack = false;
   }
   void add_items(const Op *op, const Packer &pk, void *packed, const void *origin, int64_t count) {
     pk.items(packed, origin, count, items);
@@ -385,9 +388,19 @@ template <typename T> const T *select(const std::vector<T> &v, const std::vector
   return tmp.data();
 }
 
+int nextLane = 0; // round robin over the scatter lanes
+
 void flush_list(PendingList &list, bool pack) {
   if (list.empty()) return;
   ScopedNs timer(counters.ns_flush);
+  // gathers (and anything ordered after one) run on lane 0; scatters and
+  // copies take the other lanes in turn, so consecutive batches overlap
+  int lane = 0;
+  if (!pack && list.afterPack) flush_list(pendingPack, true); // that gather goes first
+  if (!pack && !list.afterPack && gpu::lanes() > 1) {
+    lane = 1 + nextLane;
+    nextLane = (nextLane + 1) % (gpu::lanes() - 1);
+  }
   // group by device (almost always one)
   int devices[64];
   int ndev = 0;
@@ -405,7 +418,7 @@ void flush_list(PendingList &list, bool pack) {
     const size_t nitems = all ? list.items.size() : itmp.size();
     const tempi_hip_copy_item *copies = select(list.copies, list.copyDev, dev, all, ctmp);
     const size_t ncopies = all ? list.copies.size() : ctmp.size();
-    void *s = gpu::stream(dev);
+    void *s = gpu::stream(dev, lane);
     int cur = 0;
     tempi_hip_get_device(&cur);
     if (cur != dev) tempi_hip_set_device(dev);
@@ -419,6 +432,7 @@ void flush_list(PendingList &list, bool pack) {
       if (st.dev == dev) gpu::check(tempi_hip_memcpy_async(st.dst, st.src, st.n, s), "staged D2H");
     auto b = std::make_shared<GpuBatch>();
     b->device = dev;
+    b->lane = lane;
     b->event = get_event();
     gpu::check(tempi_hip_event_record(b->event, s), "event record");
     if (cur != dev) tempi_hip_set_device(cur);
@@ -773,7 +787,9 @@ struct IrecvOp : Op {
         c.src = dd.desc;
         pendingUnpack.add_copy(this, c);
       } else if (direct->state == DirectShared::PACKED && sameDevice) {
+        // the sender's gather runs on lane 0: so does this scatter, after it
         pendingUnpack.add_items(this, packer, direct->slab->dev, origin, elems);
+        pendingUnpack.afterPack = true;
       } else { // another device, or a shape the copy kernel does not take
         materialise_direct(direct, dd, hslab);
         pendingUnpack.add_items(this, packer, hslab->dev, origin, elems);
@@ -935,6 +951,7 @@ std::vector<MPI_Status> pollSt;
 } // namespace
 
 void init() {
+  gpu::choose_lanes(topology::ranks_on_node());
   gpuAwareLibrary = std::getenv("TEMPI_MPI_GPU_AWARE") != nullptr;
   directEnabled = std::getenv("TEMPI_NO_DIRECT") == nullptr;
   if (const char *s = std::getenv("TEMPI_EARLY_FLUSH")) earlyFlush = size_t(std::max(1, std::atoi(s)));
@@ -1125,12 +1142,12 @@ bool progress(bool full) {
     flush_list(pendingUnpack, false);
     moved = true;
   }
-  // 1. GPU events, in launch order (one stream per device: a later event of
-  //    the same device cannot complete before an earlier one)
+  // 1. GPU events, in launch order (a later event of the same stream cannot
+  //    complete before an earlier one)
   uint64_t t0 = now_ns();
-  uint64_t blocked = 0; // devices (bit per device < 64) with an incomplete batch
+  uint64_t blocked = 0; // streams (bit per device x lane) with an incomplete batch
   for (auto &b : batches) {
-    const uint64_t bit = uint64_t(1) << (b->device & 63);
+    const uint64_t bit = uint64_t(1) << ((b->device * gpu::kMaxLanes + b->lane) & 63);
     if (b->complete || (blocked & bit)) continue;
     const int q = tempi_hip_event_query(b->event);
     if (q == 1) {

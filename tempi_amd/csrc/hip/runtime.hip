@@ -69,6 +69,15 @@ int tempi_hip_stream_create(void **stream) {
   *stream = s;
   RET(e);
 }
+int tempi_hip_stream_create_priority(void **stream, int high) {
+  int least = 0, greatest = 0;
+  hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+  if (e != hipSuccess) return int(e);
+  hipStream_t s = nullptr;
+  e = hipStreamCreateWithPriority(&s, hipStreamNonBlocking, high ? greatest : least);
+  *stream = s;
+  RET(e);
+}
 int tempi_hip_stream_destroy(void *stream) { RET(hipStreamDestroy(static_cast<hipStream_t>(stream))); }
 int tempi_hip_stream_synchronize(void *stream) {
   RET(hipStreamSynchronize(static_cast<hipStream_t>(stream)));

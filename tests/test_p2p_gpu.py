@@ -54,7 +54,12 @@ def test_pingpong_nd(gpu, method, total, block):
     (3, "30", {}, ["--neighbor"]),
     # x split (the 24-byte faces cross ranks, as at 8 ranks on (2, 2, 2))
     (2, "64 16 16", {}, []), (4, "64 64 16", {}, []), (4, "64 64 16", {}, ["--neighbor"]),
-    (4, "64 64 16", {"TEMPI_DATATYPE_STAGED": "1"}, [])])
+    (4, "64 64 16", {"TEMPI_DATATYPE_STAGED": "1"}, []),
+    # ranks sharing this box's one GPU get one stream lane; force the
+    # multi-lane configuration of one rank per GPU (scatters on lanes 1-3)
+    (2, "40", {"TEMPI_STREAMS": "4"}, []), (4, "64 64 16", {"TEMPI_STREAMS": "3"}, []),
+    (4, "32", {"TEMPI_STREAMS": "3"}, ["--neighbor"]), (2, "40", {"TEMPI_STREAMS": "3", "TEMPI_NO_DIRECT": "1"}, []),
+    (1, "48", {"TEMPI_STREAMS": "1"}, [])])
 def test_halo_exchange_content(gpu, ranks, grid, env, extra):
     rc, out = mpi_launch.run(ranks, [os.path.join(LIB, "halo_exchange"), "2"] + grid.split() + ["--quants", "2", "--check"] + extra,
                              env=env, timeout=300)
@@ -102,7 +107,7 @@ def test_completion_family_device(gpu, method):
 
 
 @pytest.mark.parametrize("n,method", [(2, "AUTO"), (2, "ONESHOT"), (2, "IPC"), (2, "STAGED"), (1, "AUTO"),
-                                      (1, "NO_DIRECT")])
+                                      (1, "NO_DIRECT"), (2, "LANES")])
 def test_send_order_across_routes(gpu, n, method):
     """MPI non-overtaking: a gathered strided send, a host send, a
     library-packed irregular send and another strided send to one peer with
@@ -110,5 +115,7 @@ def test_send_order_across_routes(gpu, n, method):
     env = dict(METHODS.get(method, {}))
     if method == "NO_DIRECT":
         env["TEMPI_NO_DIRECT"] = "1"
+    if method == "LANES":
+        env["TEMPI_STREAMS"] = "3"
     rc, out = mpi_launch.run(n, mpi_launch.py("order.py", "--device"), env=env, timeout=240)
     assert rc == 0 and "RESULT errors=0" in out, out[-3000:]
