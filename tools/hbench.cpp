@@ -119,7 +119,9 @@ int main(int argc, char **argv) {
       {"all26", [](const Region &) { return true; }},
   };
 
+  const char *only = std::getenv("HBENCH_ONLY"); // one class (profiling runs)
   for (const Cls &c : classes) {
+    if (only && std::strcmp(only, c.name) != 0) continue;
     std::vector<tempi_hip_batch_item> pk, up;
     std::vector<tempi_hip_copy_item> cp;
     long long payload = 0, off = 0;
