@@ -240,6 +240,7 @@ struct GpuBatch {
   void *event = nullptr;
   int device = 0;
   int lane = 0;
+  bool scatter = false;
   bool complete = false;
   std::vector<Op *> ops; // whose GPU work this batch carries (alive until gpu_done)
 };
@@ -378,6 +379,8 @@ struct PendingList {
 PendingList pendingPack, pendingUnpack;
 constexpr size_t kMaxPending = 512;
 size_t earlyFlush = 32; // TEMPI_EARLY_FLUSH
+size_t firstFlush = 16;  // TEMPI_FIRST_FLUSH: the same while no scatter batch is in flight
+int scattersInFlight = 0; // scatter / copy batches launched and not yet seen complete
 
 template <typename T> const T *select(const std::vector<T> &v, const std::vector<int> &dev, int d, bool all,
                                       std::vector<T> &tmp) {
@@ -433,6 +436,8 @@ void flush_list(PendingList &list, bool pack) {
     auto b = std::make_shared<GpuBatch>();
     b->device = dev;
     b->lane = lane;
+    b->scatter = !pack;
+    if (!pack) ++scattersInFlight;
     b->event = get_event();
     gpu::check(tempi_hip_event_record(b->event, s), "event record");
     if (cur != dev) tempi_hip_set_device(cur);
@@ -955,6 +960,9 @@ void init() {
   gpuAwareLibrary = std::getenv("TEMPI_MPI_GPU_AWARE") != nullptr;
   directEnabled = std::getenv("TEMPI_NO_DIRECT") == nullptr;
   if (const char *s = std::getenv("TEMPI_EARLY_FLUSH")) earlyFlush = size_t(std::max(1, std::atoi(s)));
+  firstFlush = std::min<size_t>(16, earlyFlush);
+  if (const char *s = std::getenv("TEMPI_FIRST_FLUSH")) firstFlush = size_t(std::max(1, std::atoi(s)));
+  scattersInFlight = 0;
   directShared.clear();
   systemPerformanceLoaded = import_system_performance(&systemPerformance);
   modelCache.clear();
@@ -990,6 +998,7 @@ void finalize() {
   for (auto &b : batches)
     if (b->event) tempi_hip_event_destroy(b->event);
   batches.clear();
+  scattersInFlight = 0;
   while (!pendingAcks.empty()) {
     progress();
     if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(30)) {
@@ -1088,7 +1097,8 @@ int irecv(void *buf, int count, MPI_Datatype dt, int source, int tag, MPI_Comm c
   *req = add(std::make_unique<IrecvOp>(rec, origin, count, dt, source, tag, comm, p.device, bytes));
   // keep the GPU busy while the caller is still posting: launch arrived
   // messages' copies / unpacks once a launch's worth has queued up
-  if (pendingUnpack.size() >= earlyFlush) flush_list(pendingUnpack, false);
+  // (sooner while the GPU has no scatter work: the first batch starts early)
+  if (pendingUnpack.size() >= (scattersInFlight ? earlyFlush : firstFlush)) flush_list(pendingUnpack, false);
   counters.ns_irecv += now_ns() - t0;
   return MPI_SUCCESS;
 }
@@ -1158,6 +1168,7 @@ bool progress(bool full) {
     put_event(b->event);
     b->event = nullptr;
     b->complete = true;
+    if (b->scatter) --scattersInFlight;
     std::vector<Op *> ops;
     ops.swap(b->ops);
     for (Op *op : ops) op->gpu_done();
