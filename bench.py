@@ -234,6 +234,9 @@ def headline(args, mpi, torch, rank, world, pg, dev):
     value = total_alg / el_max / 1e9
     mpi.Type_free(t)
 
+    # the box's achievable HBM rate for the same bytes: a device-to-device
+    # copy of the packed size (read + write, SURVEY 8(d) "calibrated peak")
+    cal = calibrate_copy(torch, packed, dst, payload)
     launches = kt["packs"] + kt["unpacks"]
     avg_ms = (kt["pack_ms"] + kt["unpack_ms"]) / max(launches, 1)
     alg_launch = 2.0 * payload
@@ -274,16 +277,45 @@ def headline(args, mpi, torch, rank, world, pg, dev):
             "pack_avg_ms": round(kt["pack_ms"] / max(kt["packs"], 1), 4),
             "unpack_avg_ms": round(kt["unpack_ms"] / max(kt["unpacks"], 1), 4),
             "timed_launches": launches,
+            # calibration: the guide's achievable streaming rate, and this
+            # box's hipMemcpyAsync D2D of the same bytes (slower than the
+            # pack kernel itself, so not a ceiling)
+            "achievable_peak": HBM_ACHIEVABLE_GBS,
+            "frac_achievable": round(achieved / HBM_ACHIEVABLE_GBS, 4),
+            "d2d_copy_GBps": round(cal, 1),
+            "calibration": ("achievable_peak: MI355X_MICROARCH.md HBM section (~6.3 TB/s streaming); d2d_copy_GBps: "
+                            "torch copy_ (hipMemcpyAsync D2D) of the packed size, 10 launches, HIP events"),
         },
     }
     return rec
 
 
+HBM_ACHIEVABLE_GBS = 6300.0  # MI355X_MICROARCH.md: "8 TB/s peak (spec); ~6.3 TB/s achievable"
+
+
+def calibrate_copy(torch, a, scratch, n):
+    """GB/s (read + write) of a plain device-to-device copy of n bytes"""
+    b = scratch[:n]
+    for _ in range(2):
+        b.copy_(a)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(10):
+        b.copy_(a)
+    e1.record()
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / 10
+    return 2.0 * n / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+
+
 XGMI_LINK_GBS = 153.0  # per direction, per link (SURVEY 8(d))
 
 
-def halo(args, mpi, world):
-    """Config 4 through libtempi_apps.so's tempi_bench_halo (every rank)."""
+def halo(args, mpi, world, grid=None):
+    """Config 4 through libtempi_apps.so's tempi_bench_halo (every rank).
+    grid: the global edge (default --halo-grid, fixed total work); the
+    reference's own scripts weak-scale it instead (512, 645, 813, 1024 for 1,
+    2, 4, 8 ranks: scripts/summit/bench_halo_exchange.sh:27-45)."""
     import ctypes
 
     import tempi_amd
@@ -291,7 +323,7 @@ def halo(args, mpi, world):
     L = ctypes.CDLL(os.path.join(tempi_amd.LIBDIR, "libtempi_apps.so"), mode=ctypes.RTLD_GLOBAL)
     L.tempi_bench_halo.argtypes = [ctypes.c_int] * 9 + [ctypes.c_char_p, ctypes.c_int]
     buf = ctypes.create_string_buffer(4096)
-    g = args.halo_grid
+    g = grid or args.halo_grid
     rc = L.tempi_bench_halo(args.halo_iters, g, g, g, 8, 3, 0, 0, 0, buf, 4096)
     if rc != 0:
         raise SystemExit(f"halo exchange failed rc={rc}")
@@ -477,6 +509,10 @@ def main():
             h = halo(args, mpi, world)
             if rank == 0:
                 rec["halo"] = h
+            if world > 1:  # the reference scripts' weak scaling: 512 * N^(1/3) per edge
+                hw = halo(args, mpi, world, grid=int(round(args.halo_grid * world ** (1.0 / 3.0))))
+                if rank == 0:
+                    rec["halo_weak"] = hw
         if world > 1 and not args.no_p2p:
             pp = pingpong(args, world)
             a2 = alltoallv(args, world)
