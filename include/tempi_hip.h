@@ -62,7 +62,14 @@ typedef struct tempi_hip_batch_item {
   void *packed;
   void *first;
   tempi_hip_desc desc;
+  uint32_t flags; /* TEMPI_HIP_ITEM_*; 0 for ordinary items */
+  uint32_t reserved_;
 } tempi_hip_batch_item;
+/* unpack: `packed` is another process's memory mapped through an IPC handle
+   (possibly another GPU's), reused by its owner for later messages; the
+   kernel reads it with system-scope loads so that no line this GPU cached
+   from an earlier message in the same buffer is returned */
+#define TEMPI_HIP_ITEM_REMOTE 1u
 int tempi_hip_pack_batch(const tempi_hip_batch_item *items, int n, void *stream);
 int tempi_hip_unpack_batch(const tempi_hip_batch_item *items, int n, void *stream);
 

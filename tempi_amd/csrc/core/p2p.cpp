@@ -82,6 +82,7 @@ struct DirectShared {
 std::map<uint64_t, std::shared_ptr<DirectShared>> directShared; // sent, not yet matched
 uint64_t nextDirectToken = 1;
 bool directEnabled = true;
+bool ipcSystemLoads = true; // TEMPI_IPC_PLAIN_LOADS=1 turns off TEMPI_HIP_ITEM_REMOTE (A/B only)
 
 MPI_Comm ctrlComm = MPI_COMM_NULL; // private duplicate of MPI_COMM_WORLD for acks
 int tagUb = 32767;
@@ -817,7 +818,10 @@ struct IrecvOp : Op {
       }
       const char *peer = static_cast<const char *>(base) + d.offset;
       elems = size ? d.bytes / size : 0;
+      const size_t first = pendingUnpack.items.size();
       pendingUnpack.add_items(this, packer, const_cast<char *>(peer), origin, elems);
+      if (ipcSystemLoads) // the peer reuses this slab: never read a line cached from an earlier message
+        for (size_t i = first; i < pendingUnpack.items.size(); ++i) pendingUnpack.items[i].flags |= TEMPI_HIP_ITEM_REMOTE;
     } else {
       if (int64_t(n) > bytes) LOG_FATAL("message truncated: " << n << " B into " << bytes);
       elems = size ? n / size : 0;
@@ -959,6 +963,7 @@ void init() {
   gpu::choose_lanes(topology::ranks_on_node());
   gpuAwareLibrary = std::getenv("TEMPI_MPI_GPU_AWARE") != nullptr;
   directEnabled = std::getenv("TEMPI_NO_DIRECT") == nullptr;
+  ipcSystemLoads = std::getenv("TEMPI_IPC_PLAIN_LOADS") == nullptr;
   if (const char *s = std::getenv("TEMPI_EARLY_FLUSH")) earlyFlush = size_t(std::max(1, std::atoi(s)));
   firstFlush = std::min<size_t>(16, earlyFlush);
   if (const char *s = std::getenv("TEMPI_FIRST_FLUSH")) firstFlush = size_t(std::max(1, std::atoi(s)));

@@ -157,9 +157,53 @@ template <int ND> struct KArgs {
   // strided dimensions, INNERMOST FIRST
   uint32_t cnt[ND > 0 ? ND : 1];
   Magic mcnt[ND > 0 ? ND : 1];
+  uint32_t flags;  // TEMPI_HIP_ITEM_* of the item (sits in what was padding)
   int64_t stride[ND > 0 ? ND : 1];
   int64_t wrap[ND > 0 ? ND : 1]; // cnt[k] * stride[k]
 };
+
+// Packed bytes that live in another process's memory (an IPC-mapped slab,
+// possibly on another GPU: TEMPI_HIP_ITEM_REMOTE) are read with system-scope
+// loads (sc0 sc1). The slab is reused for later messages, and a plain load
+// could return a line this GPU's L2 kept from an earlier message in it. The
+// buffer form keeps the loads counted by hipcc; its base is the first active
+// lane's address (wave-uniform), which every call site keeps lowest.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t remote_rsrc(const void *p, uint32_t *off) {
+  const uint64_t a = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(uint32_t(a));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(uint32_t(a >> 32));
+  const uint64_t base = (uint64_t(hi) << 32) | lo;
+  *off = uint32_t(a - base);
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(base), 0, 0x7fffffff, 0x00020000);
+}
+constexpr int kSysScope = 1 | 16; // cache policy sc0 | sc1
+template <typename T> __device__ __forceinline__ T ld_remote(const T *p) {
+  uint32_t off;
+  const __amdgpu_buffer_rsrc_t r = remote_rsrc(p, &off);
+  T v;
+  if constexpr (sizeof(T) == 16) {
+    u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(r, int(off), 0, kSysScope);
+    __builtin_memcpy(&v, &x, 16);
+  } else if constexpr (sizeof(T) == 8) {
+    u32x2 x = __builtin_amdgcn_raw_buffer_load_b64(r, int(off), 0, kSysScope);
+    __builtin_memcpy(&v, &x, 8);
+  } else if constexpr (sizeof(T) == 4) {
+    uint32_t x = __builtin_amdgcn_raw_buffer_load_b32(r, int(off), 0, kSysScope);
+    __builtin_memcpy(&v, &x, 4);
+  } else if constexpr (sizeof(T) == 2) {
+    uint16_t x = __builtin_amdgcn_raw_buffer_load_b16(r, int(off), 0, kSysScope);
+    __builtin_memcpy(&v, &x, 2);
+  } else {
+    uint8_t x = __builtin_amdgcn_raw_buffer_load_b8(r, int(off), 0, kSysScope);
+    __builtin_memcpy(&v, &x, 1);
+  }
+  return v;
+}
+// a load of packed bytes on the unpack side
+template <typename T, int ND> __device__ __forceinline__ T ld_packed(const KArgs<ND> &a, const T *p, bool nt) {
+  if (a.flags & TEMPI_HIP_ITEM_REMOTE) return ld_remote(p);
+  return ld(p, nt);
+}
 
 // row index -> byte offset of the row, plus the odometer digits
 template <int ND>
@@ -226,7 +270,7 @@ __device__ void partial_chunk(uint32_t c, const KArgs<ND> &a) {
     if (PACK)
       *pk = *sp;
     else
-      *sp = *pk;
+      *sp = ld_packed(a, pk, false);
   }
 }
 
@@ -290,7 +334,7 @@ __device__ __forceinline__ void unpack_body(const KArgs<ND> &a, uint32_t blk, ui
       const uint32_t c = base + u * kBlock + threadIdx.x;
       const int64_t q0 = int64_t(c) * CW - a.head;
       full[u] = c < a.nchunks && q0 >= 0 && q0 + CW <= int64_t(a.nwords);
-      if (full[u]) buf[u].v = ld(reinterpret_cast<const uint4 *>(a.chunk0 + size_t(c) * 16), kNtPacked);
+      if (full[u]) buf[u].v = ld_packed(a, reinterpret_cast<const uint4 *>(a.chunk0 + size_t(c) * 16), kNtPacked);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -350,7 +394,7 @@ __device__ __forceinline__ void unpack_il_tile(const KArgs<ND> &a, uint32_t tile
     unpack_body<W, ND, 1>(a, tileIdx, ntiles);
     return;
   }
-  tile[threadIdx.x] = ld(reinterpret_cast<const uint4 *>(a.chunk0 + size_t(c0 + threadIdx.x) * 16), kNtPacked);
+  tile[threadIdx.x] = ld_packed(a, reinterpret_cast<const uint4 *>(a.chunk0 + size_t(c0 + threadIdx.x) * 16), kNtPacked);
   __syncthreads();
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const WT *src = reinterpret_cast<const WT *>(tile + wave * 64);
@@ -600,6 +644,10 @@ int word_width(uintptr_t packed, uintptr_t first, const Norm &n) {
   return int(g & (~g + 1));
 }
 
+// TEMPI_HIP_ITEM_* of the object make_args is describing (set around each
+// item by run_batch; 0 for the single-object entry points)
+thread_local uint32_t gItemFlags = 0;
+
 // descriptor + workgroup count of one object
 template <int W, int ND>
 void make_args(char *packed, char *first, const Norm &n, KArgs<ND> *out, uint32_t *blocks) {
@@ -610,6 +658,7 @@ void make_args(char *packed, char *first, const Norm &n, KArgs<ND> *out, uint32_
   constexpr int CW = 16 / W;
   a.chunk0 = packed - size_t(head) * W;
   a.strided = first;
+  a.flags = gItemFlags;
   a.nwords = uint32_t(nwords);
   a.head = head;
   a.nchunks = uint32_t((nwords + head + CW - 1) / CW);
@@ -644,6 +693,7 @@ int launch_nd(bool pack, char *packed, char *first, const Norm &n, hipStream_t s
 struct Job {
   char *packed, *first;
   Norm n;
+  uint32_t flags;
 };
 
 template <int W, int ND> int launch_batch_nd(bool pack, const std::vector<Job> &jobs, hipStream_t s) {
@@ -672,7 +722,9 @@ template <int W, int ND> int launch_batch_nd(bool pack, const std::vector<Job> &
   for (const Job &j : jobs) {
     KArgs<ND> a;
     uint32_t blocks;
+    gItemFlags = j.flags;
     make_args<W, ND>(j.packed, j.first, j.n, &a, &blocks);
+    gItemFlags = 0;
     if (il) blocks = (a.nchunks + kBlock - 1) / kBlock;
     if (!blocks) continue;
     if (uint64_t(total) + blocks >= (uint64_t(1) << 31))
@@ -843,11 +895,15 @@ int run_batch(bool pack, const tempi_hip_batch_item *items, int n, hipStream_t s
     Job j;
     j.packed = static_cast<char *>(items[i].packed);
     j.first = static_cast<char *>(items[i].first);
+    j.flags = pack ? 0u : items[i].flags; // (gathers read the strided side only)
     if (!normalise(&items[i].desc, &j.n)) return int(hipErrorInvalidValue);
     const int64_t bytes = norm_bytes(j.n);
     if (bytes == 0) continue;
     if (bytes >= kMaxLaunchBytes) { // too big for one 32-bit-indexed item
-      if (int e = launch_split(pack, j.packed, j.first, j.n, s)) return e;
+      gItemFlags = j.flags;
+      const int e = launch_split(pack, j.packed, j.first, j.n, s);
+      gItemFlags = 0;
+      if (e) return e;
       continue;
     }
     const int w = word_width(reinterpret_cast<uintptr_t>(j.packed), reinterpret_cast<uintptr_t>(j.first), j.n);

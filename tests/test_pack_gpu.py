@@ -284,14 +284,21 @@ class HipDesc(ctypes.Structure):
 
 
 class HipItem(ctypes.Structure):
-    _fields_ = [("packed", ctypes.c_void_p), ("first", ctypes.c_void_p), ("desc", HipDesc)]
+    _fields_ = [("packed", ctypes.c_void_p), ("first", ctypes.c_void_p), ("desc", HipDesc),
+                ("flags", ctypes.c_uint32), ("reserved_", ctypes.c_uint32)]
 
 
+ITEM_REMOTE = 1  # TEMPI_HIP_ITEM_REMOTE
+
+
+@pytest.mark.parametrize("remote", [False, True])
 @pytest.mark.parametrize("seed", range(6))
-def test_batched_kernel_c_abi(mpi, gpu, seed):
+def test_batched_kernel_c_abi(mpi, gpu, seed, remote):
     """tempi_hip_pack_batch / tempi_hip_unpack_batch (include/tempi_hip.h):
     up to 100 objects of mixed word width / rank / alignment in one call,
-    against oracle/typemap.c, and the scatter back restores every type map."""
+    against oracle/typemap.c, and the scatter back restores every type map.
+    remote: every other item carries TEMPI_HIP_ITEM_REMOTE, so its scatter
+    reads the packed bytes with system-scope buffer loads (the IPC path)."""
     torch = _torch()
     import tempi_amd
 
@@ -331,6 +338,7 @@ def test_batched_kernel_c_abi(mpi, gpu, seed):
         for j, (cn, st) in enumerate(c["dims"]):
             it.desc.counts[j] = cn
             it.desc.strides[j] = st
+        it.flags = ITEM_REMOTE if remote and k % 2 == 0 else 0
     torch.cuda.synchronize()
     assert H.tempi_hip_pack_batch(items, len(cases), None) == 0
     torch.cuda.synchronize()
