@@ -29,15 +29,22 @@ struct Counters {
   uint64_t progress_passes = 0, batches = 0, batched_items = 0;
 };
 
+extern Counters counters;
+extern bool kernelProfiling;
+// the ns_* host timers run only when asked for (TEMPI_PRINT_COUNTERS or
+// TEMPI_HOST_TIMING): a clock read is ~20 ns, several per message
+extern bool hostTiming;
+
 uint64_t now_ns();
+inline uint64_t tick() { return hostTiming ? now_ns() : 0; }
+inline void tock(uint64_t &acc, uint64_t t0) {
+  if (hostTiming) acc += now_ns() - t0;
+}
 struct ScopedNs {
   uint64_t &acc;
   uint64_t t0;
-  explicit ScopedNs(uint64_t &a) : acc(a), t0(now_ns()) {}
-  ~ScopedNs() { acc += now_ns() - t0; }
+  explicit ScopedNs(uint64_t &a) : acc(a), t0(tick()) {}
+  ~ScopedNs() { tock(acc, t0); }
 };
-
-extern Counters counters;
-extern bool kernelProfiling;
 
 } // namespace tempi

@@ -39,6 +39,7 @@ void coll_finalize();
 State state;
 Counters counters;
 bool kernelProfiling = false;
+bool hostTiming = false;
 
 int raise_error(MPI_Comm comm, int code) {
   MPI_Comm_call_errhandler(comm, code);
@@ -51,6 +52,7 @@ void init_after_mpi() {
   MPI_Comm_rank(MPI_COMM_WORLD, &state.worldRank);
   MPI_Comm_size(MPI_COMM_WORLD, &state.worldSize);
   logRank = state.worldRank;
+  hostTiming = std::getenv("TEMPI_PRINT_COUNTERS") || std::getenv("TEMPI_HOST_TIMING");
   gpu::init();
   types_init();
   state.active = true;

@@ -79,7 +79,7 @@ struct DirectShared {
   int device = 0;
   Op *sender = nullptr; // while the send is incomplete
 };
-std::map<uint64_t, std::shared_ptr<DirectShared>> directShared; // sent, not yet matched
+std::unordered_map<uint64_t, std::shared_ptr<DirectShared>> directShared; // sent, not yet matched
 uint64_t nextDirectToken = 1;
 bool directEnabled = true;
 bool ipcSystemLoads = true; // TEMPI_IPC_PLAIN_LOADS=1 turns off TEMPI_HIP_ITEM_REMOTE (A/B only)
@@ -587,7 +587,7 @@ struct IsendDirectOp : Op {
     // it: the request is released now and the descriptor outlives it in `sh`
     MPI_Request sreq;
     next.MPI_Isend(&sh->desc, int(sizeof sh->desc), MPI_PACKED, dest, tag, comm, &sreq);
-    MPI_Request_free(&sreq);
+    next.MPI_Request_free(&sreq);
     maybe_done();
   }
   ~IsendDirectOp() override {
@@ -942,11 +942,18 @@ uint32_t nextHandle = 1;
 std::unordered_map<uint32_t, std::unique_ptr<Op>> active;
 std::vector<uint32_t> detachedOps; // freed by the application, still running
 
+bool handlesWrapped = false; // once the counter has wrapped, skip handles still in use
+
 MPI_Request add(std::unique_ptr<Op> op) {
-  while (active.count(nextHandle) || nextHandle == 0) nextHandle = (nextHandle + 1) % kHandleSpace;
+  if (handlesWrapped)
+    while (active.count(nextHandle) || nextHandle == 0) nextHandle = (nextHandle + 1) % kHandleSpace;
   const uint32_t h = nextHandle;
   nextHandle = (nextHandle + 1) % kHandleSpace;
-  active[h] = std::move(op);
+  if (nextHandle == 0) {
+    nextHandle = 1;
+    handlesWrapped = true;
+  }
+  active.emplace(h, std::move(op));
   return MPI_Request(h);
 }
 
@@ -969,6 +976,8 @@ void init() {
   if (const char *s = std::getenv("TEMPI_FIRST_FLUSH")) firstFlush = size_t(std::max(1, std::atoi(s)));
   scattersInFlight = 0;
   directShared.clear();
+  directShared.reserve(512);
+  active.reserve(2048);
   systemPerformanceLoaded = import_system_performance(&systemPerformance);
   modelCache.clear();
   if (const char *s = std::getenv("TEMPI_IPC_MIN_BYTES")) ipcMinBytes = std::atoll(s);
@@ -1090,7 +1099,7 @@ int irecv(void *buf, int count, MPI_Datatype dt, int source, int tag, MPI_Comm c
   // start queued gathers (a burst of Isends shares this launch); the rest of
   // progress is left to the waits, so a burst of Irecvs stays O(1) each
   if (!pendingPack.empty()) flush_list(pendingPack, true);
-  uint64_t t0 = now_ns();
+  const uint64_t t0 = tick();
   counters.irecvs++;
   if (!rec->packer) {
     *req = add(std::make_unique<LibIrecvOp>(buf, count, dt, source, tag, comm));
@@ -1104,7 +1113,7 @@ int irecv(void *buf, int count, MPI_Datatype dt, int source, int tag, MPI_Comm c
   // messages' copies / unpacks once a launch's worth has queued up
   // (sooner while the GPU has no scatter work: the first batch starts early)
   if (pendingUnpack.size() >= (scattersInFlight ? earlyFlush : firstFlush)) flush_list(pendingUnpack, false);
-  counters.ns_irecv += now_ns() - t0;
+  tock(counters.ns_irecv, t0);
   return MPI_SUCCESS;
 }
 
@@ -1159,7 +1168,7 @@ bool progress(bool full) {
   }
   // 1. GPU events, in launch order (a later event of the same stream cannot
   //    complete before an earlier one)
-  uint64_t t0 = now_ns();
+  uint64_t t0 = tick();
   uint64_t blocked = 0; // streams (bit per device x lane) with an incomplete batch
   for (auto &b : batches) {
     const uint64_t bit = uint64_t(1) << ((b->device * gpu::kMaxLanes + b->lane) & 63);
@@ -1180,8 +1189,8 @@ bool progress(bool full) {
     moved = true;
   }
   while (!batches.empty() && batches.front()->complete) batches.pop_front();
-  counters.ns_events += now_ns() - t0;
-  t0 = now_ns();
+  tock(counters.ns_events, t0);
+  t0 = tick();
   // 2. every outstanding library request in one MPI_Testsome
   pollReqs.clear();
   pollOps.clear();
@@ -1241,7 +1250,7 @@ bool progress(bool full) {
       pendingAcks.pop_back();
     }
   }
-  counters.ns_testsome += now_ns() - t0;
+  tock(counters.ns_testsome, t0);
   // 3. unpacks of messages that arrived: launched together when the caller
   //    is about to wait for them (light passes from MPI_Isend / MPI_Irecv
   //    only queue them, so a burst of receives shares one launch)
