@@ -103,6 +103,30 @@ std::vector<std::unique_ptr<PendingAck>> pendingAcks; // stable addresses: Irecv
 // peer slabs mapped into this process: (world rank, slab id) -> base
 std::map<std::pair<int, uint64_t>, void *> ipcOpen;
 
+// A datatype handle that stays valid while an operation still needs it:
+// the application may MPI_Type_free its type right after MPI_Isend /
+// MPI_Irecv returns. Derived types are duplicated (the duplicate of a
+// committed type is committed); named types are returned as they are.
+bool named_type(MPI_Datatype t) {
+  int ni = 0, na = 0, nd = 0, comb = 0;
+  MPI_Type_get_envelope(t, &ni, &na, &nd, &comb);
+  return comb == MPI_COMBINER_NAMED;
+}
+MPI_Datatype hold_type(MPI_Datatype t) {
+  if (named_type(t)) return t;
+  MPI_Datatype d = MPI_DATATYPE_NULL;
+  MPI_Type_dup(t, &d);
+  return d;
+}
+void drop_type(MPI_Datatype t) {
+  if (t != MPI_DATATYPE_NULL && !named_type(t)) next.MPI_Type_free(&t);
+}
+
+// the status of a completed receive: `bytes` received (MPI_Get_count with
+// the receive's datatype then gives whole elements), without touching the
+// application's datatype handle, which may have been freed meanwhile
+void set_received(MPI_Status *s, int64_t bytes) { MPI_Status_set_elements_x(s, MPI_BYTE, MPI_Count(bytes)); }
+
 int64_t pack_size(int count, MPI_Datatype dt, MPI_Comm comm) {
   int s = 0;
   MPI_Pack_size(count, dt, comm, &s);
@@ -541,7 +565,7 @@ struct IsendOp : Op {
       s->MPI_SOURCE = MPI_ANY_SOURCE;
       s->MPI_TAG = MPI_ANY_TAG;
       s->MPI_ERROR = MPI_SUCCESS;
-      MPI_Status_set_elements(s, dt, 0);
+      MPI_Status_set_elements(s, MPI_BYTE, 0);
     }
   }
 };
@@ -616,7 +640,7 @@ struct IsendDirectOp : Op {
       s->MPI_SOURCE = MPI_ANY_SOURCE;
       s->MPI_TAG = MPI_ANY_TAG;
       s->MPI_ERROR = MPI_SUCCESS;
-      MPI_Status_set_elements(s, dt, 0);
+      MPI_Status_set_elements(s, MPI_BYTE, 0);
     }
   }
 };
@@ -840,7 +864,7 @@ struct IrecvOp : Op {
     if (s != MPI_STATUS_IGNORE) {
       *s = libStatus;
       s->MPI_ERROR = MPI_SUCCESS;
-      MPI_Status_set_elements(s, dt, int(elems));
+      set_received(s, elems * rec->desc.size);
     }
   }
 };
@@ -865,7 +889,7 @@ struct LibIsendOp : Op {
   void status(MPI_Status *s) const override {
     if (s != MPI_STATUS_IGNORE) {
       s->MPI_ERROR = MPI_SUCCESS;
-      MPI_Status_set_elements(s, dt, 0);
+      MPI_Status_set_elements(s, MPI_BYTE, 0);
     }
   }
 };
@@ -877,10 +901,11 @@ struct HostIsendOp : Op {
   MPI_Datatype dt;
   MPI_Comm comm;
   HostIsendOp(const void *b, int c, MPI_Datatype d, int de, int t, MPI_Comm cm)
-      : buf(b), count(c), dest(de), tag(t), dt(d), comm(cm) {
+      : buf(b), count(c), dest(de), tag(t), dt(hold_type(d)), comm(cm) {
     ready = true;
     gate_enter(gate_key(comm, dest), this);
   }
+  ~HostIsendOp() override { drop_type(dt); }
   void post() override {
     next.MPI_Isend(buf, count, dt, dest, tag, comm, &lib);
     watch(this);
@@ -889,7 +914,7 @@ struct HostIsendOp : Op {
   void status(MPI_Status *s) const override {
     if (s != MPI_STATUS_IGNORE) {
       s->MPI_ERROR = MPI_SUCCESS;
-      MPI_Status_set_elements(s, dt, 0);
+      MPI_Status_set_elements(s, MPI_BYTE, 0);
     }
   }
 };
@@ -902,7 +927,9 @@ struct LibIrecvOp : Op {
   MPI_Comm comm;
   MPI_Status libStatus{};
   int elems = 0;
-  LibIrecvOp(void *b, int c, MPI_Datatype d, int source, int tag, MPI_Comm cm) : user(b), count(c), dt(d), comm(cm) {
+  int received = 0; // bytes
+  LibIrecvOp(void *b, int c, MPI_Datatype d, int source, int tag, MPI_Comm cm)
+      : user(b), count(c), dt(hold_type(d)), comm(cm) {
     buf.resize(std::max<size_t>(size_t(std::max<int64_t>(pack_size(c, d, cm), 1)), kDescCap));
     next.MPI_Irecv(buf.data(), int(buf.size()), MPI_PACKED, source, tag, comm, &lib);
     watch(this);
@@ -919,15 +946,17 @@ struct LibIrecvOp : Op {
     }
     MPI_Type_size(dt, &size);
     elems = size ? n / size : 0;
+    received = elems * size;
     int pos = 0;
     tempi::unpack(buf.data(), n, &pos, user, elems, dt, comm);
     done = true;
   }
+  ~LibIrecvOp() override { drop_type(dt); }
   void status(MPI_Status *s) const override {
     if (s != MPI_STATUS_IGNORE) {
       *s = libStatus;
       s->MPI_ERROR = MPI_SUCCESS;
-      MPI_Status_set_elements(s, dt, elems);
+      set_received(s, received);
     }
   }
 };
@@ -1338,7 +1367,7 @@ int recv_host_ipc_aware(void *buf, int count, MPI_Datatype dt, int source, int t
   next.MPI_Unpack(src, nbytes, &pos, buf, elems, dt, comm);
   if (status != MPI_STATUS_IGNORE) {
     *status = st;
-    MPI_Status_set_elements(status, dt, elems);
+    set_received(status, int64_t(elems) * size);
   }
   return MPI_SUCCESS;
 }

@@ -268,6 +268,28 @@ class MPI:
         self._call("MPI_Wait", ctypes.byref(r), self.STATUS_IGNORE)
         return r.value
 
+    def _decode(self, st, t):
+        """(source, tag, count in elements of t) of an MPI_Status buffer"""
+        def at(name):
+            off = self.const(f"offsetof(MPI_Status,{name})")
+            return ctypes.c_int.from_buffer(st, off).value
+        n = ctypes.c_int(0)
+        self._call("MPI_Get_count", st, self.h(t), ctypes.byref(n))
+        return at("MPI_SOURCE"), at("MPI_TAG"), n.value
+
+    def Wait_status(self, req, t):
+        """MPI_Wait with a status: returns (request, (source, tag, count of t))"""
+        r, st = self.Request(req), self._status()
+        self._call("MPI_Wait", ctypes.byref(r), st)
+        return r.value, self._decode(st, t)
+
+    def Recv_status(self, buf, count, t, source, tag, comm=None):
+        """MPI_Recv with a status: (source, tag, count of t)"""
+        st = self._status()
+        self._call("MPI_Recv", ctypes.c_void_p(buf), count, self.h(t), source, tag,
+                   self.h(self.COMM_WORLD if comm is None else comm), st)
+        return self._decode(st, t)
+
     def Waitall(self, reqs):
         n = len(reqs)
         arr = (self.Request * max(n, 1))(*reqs)

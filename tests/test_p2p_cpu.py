@@ -28,6 +28,13 @@ def test_neighbor_collectives_host(ranks):
 
 
 @pytest.mark.parametrize("n", [1, 2])
+def test_receive_status_host(n):
+    """the status program on host buffers (library path end to end)"""
+    rc, out = mpi_launch.run(n, mpi_launch.py("status.py"), timeout=180)
+    assert rc == 0 and "RESULT errors=0" in out, out[-3000:]
+
+
+@pytest.mark.parametrize("n", [1, 2])
 def test_send_order_host(n):
     """the send-order program on host buffers (library path end to end)"""
     rc, out = mpi_launch.run(n, mpi_launch.py("order.py"), timeout=180)

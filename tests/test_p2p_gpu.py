@@ -107,6 +107,18 @@ def test_completion_family_device(gpu, method):
 
 
 @pytest.mark.parametrize("n,method", [(2, "AUTO"), (2, "ONESHOT"), (2, "IPC"), (2, "STAGED"), (1, "AUTO"),
+                                      (1, "NO_DIRECT")])
+def test_receive_status_and_freed_types(gpu, n, method):
+    """MPI_Status source / tag / MPI_Get_count of device receives (fewer
+    elements than allowed), with both datatypes freed before the wait"""
+    env = dict(METHODS.get(method, {}))
+    if method == "NO_DIRECT":
+        env["TEMPI_NO_DIRECT"] = "1"
+    rc, out = mpi_launch.run(n, mpi_launch.py("status.py", "--device"), env=env, timeout=240)
+    assert rc == 0 and "RESULT errors=0" in out, out[-3000:]
+
+
+@pytest.mark.parametrize("n,method", [(2, "AUTO"), (2, "ONESHOT"), (2, "IPC"), (2, "STAGED"), (1, "AUTO"),
                                       (1, "NO_DIRECT"), (2, "LANES")])
 def test_send_order_across_routes(gpu, n, method):
     """MPI non-overtaking: a gathered strided send, a host send, a
