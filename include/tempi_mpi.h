@@ -28,6 +28,7 @@
  *   MPI_Waitall      (not interposed: F8)            progress TEMPI requests
  *   MPI_Test         (not interposed: F8)            progress TEMPI requests
  *   MPI_Testall / _Testany / _Waitany / _Testsome / _Waitsome / MPI_Request_free
+ *   / MPI_Request_get_status / MPI_Cancel
  *                    (not interposed: F8)            understand TEMPI requests
  *   MPI_Alltoallv    src/alltoallv.cpp:14-68         device-buffer alltoallv
  *   MPI_Neighbor_alltoallw  src/neighbor_alltoallw.cpp:11-18 (-> internal/
@@ -84,6 +85,8 @@ int MPI_Testsome(int incount, MPI_Request array_of_requests[], int *outcount, in
 int MPI_Waitsome(int incount, MPI_Request array_of_requests[], int *outcount, int array_of_indices[],
                  MPI_Status array_of_statuses[]);
 int MPI_Request_free(MPI_Request *request);
+int MPI_Request_get_status(MPI_Request request, int *flag, MPI_Status *status);
+int MPI_Cancel(MPI_Request *request);
 int MPI_Alltoallv(const void *sendbuf, const int sendcounts[], const int sdispls[],
                   MPI_Datatype sendtype, void *recvbuf, const int recvcounts[], const int rdispls[],
                   MPI_Datatype recvtype, MPI_Comm comm);

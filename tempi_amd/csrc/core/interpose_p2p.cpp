@@ -260,3 +260,17 @@ TEMPI_EXPORT int MPI_Request_free(MPI_Request *request) {
   }
   return next.MPI_Request_free(request);
 }
+
+// MPI_Request_get_status and MPI_Cancel: not interposed by the reference (F8)
+TEMPI_EXPORT int MPI_Request_get_status(MPI_Request request, int *flag, MPI_Status *status) {
+  resolve_next();
+  if (state.active && p2p::is_tempi_request(request)) return p2p::get_status(request, flag, status);
+  if (state.active && p2p::busy()) p2p::progress();
+  return next.MPI_Request_get_status(request, flag, status);
+}
+
+TEMPI_EXPORT int MPI_Cancel(MPI_Request *request) {
+  resolve_next();
+  if (state.active && p2p::is_tempi_request(*request)) return p2p::cancel(*request);
+  return next.MPI_Cancel(request);
+}

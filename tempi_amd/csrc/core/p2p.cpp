@@ -279,6 +279,7 @@ struct Op {
   virtual void stalled() {}                    // waited on and still incomplete after a pass
   virtual void peer_done() {}                  // (direct sends) the receiver's copy ran
   virtual void post() {}                       // (sends) hand the message to the library
+  virtual void cancel() {}                     // MPI_Cancel (receives not yet matched)
   bool queued = false;                         // GPU work not launched yet
   bool ready = false;                          // (sends in a gate) post() may run
   bool posted = false;                         // (sends) post() has run
@@ -762,6 +763,8 @@ struct IrecvOp : Op {
   bool fallback = false; // waiting for the bytes the peer re-sends through the host
   int64_t elems = 0;
   std::shared_ptr<DirectShared> direct; // a same-process send being copied / unpacked
+  bool arrived = false;   // the library receive matched
+  bool cancelled = false; // MPI_Cancel took effect
 
   IrecvOp(const TypeRecord *r, char *o, int c, MPI_Datatype d, int source, int tag, MPI_Comm cm, int dev,
           int64_t b)
@@ -784,8 +787,23 @@ struct IrecvOp : Op {
     watch(this);
   }
 
+  void cancel() override {
+    if (!arrived && lib != MPI_REQUEST_NULL) next.MPI_Cancel(&lib);
+  }
   void lib_done(const MPI_Status &st) override { // arrived: queue its unpack
     const Packer &packer = *rec->packer;
+    if (!arrived) {
+      int c = 0;
+      MPI_Test_cancelled(&st, &c);
+      if (c) {
+        cancelled = done = true;
+        libStatus = st;
+        pinned_pool().put(hslab);
+        hslab = nullptr;
+        return;
+      }
+    }
+    arrived = true;
     if (fallback) { // the host copy of an IPC message we could not map
       elems = packer.desc().size ? desc.bytes / packer.desc().size : 0;
       pendingUnpack.add_items(this, packer, hslab->dev, origin, elems);
@@ -865,6 +883,7 @@ struct IrecvOp : Op {
       *s = libStatus;
       s->MPI_ERROR = MPI_SUCCESS;
       set_received(s, elems * rec->desc.size);
+      if (cancelled) MPI_Status_set_cancelled(s, 1);
     }
   }
 };
@@ -934,8 +953,18 @@ struct LibIrecvOp : Op {
     next.MPI_Irecv(buf.data(), int(buf.size()), MPI_PACKED, source, tag, comm, &lib);
     watch(this);
   }
+  bool cancelled = false;
+  void cancel() override {
+    if (lib != MPI_REQUEST_NULL) next.MPI_Cancel(&lib);
+  }
   void lib_done(const MPI_Status &st) override {
     libStatus = st;
+    int c = 0;
+    MPI_Test_cancelled(&st, &c);
+    if (c) {
+      cancelled = done = true;
+      return;
+    }
     int n = 0, size = 0;
     MPI_Get_count(&libStatus, MPI_PACKED, &n);
     if (is_direct(buf.data(), n) || is_ipc(buf.data(), n)) { // a TEMPI sender's descriptor
@@ -957,6 +986,7 @@ struct LibIrecvOp : Op {
       *s = libStatus;
       s->MPI_ERROR = MPI_SUCCESS;
       set_received(s, received);
+      if (cancelled) MPI_Status_set_cancelled(s, 1);
     }
   }
 };
@@ -1180,6 +1210,21 @@ void release(MPI_Request *req) {
     }
   }
   *req = MPI_REQUEST_NULL;
+}
+
+int get_status(MPI_Request r, int *flag, MPI_Status *status) {
+  auto it = active.find(uint32_t(r));
+  if (it == active.end()) return next.MPI_Request_get_status(r, flag, status);
+  progress();
+  *flag = it->second->done ? 1 : 0;
+  if (*flag) it->second->status(status);
+  return MPI_SUCCESS;
+}
+
+int cancel(MPI_Request r) {
+  auto it = active.find(uint32_t(r));
+  if (it != active.end()) it->second->cancel();
+  return MPI_SUCCESS;
 }
 
 bool progress(bool full) {

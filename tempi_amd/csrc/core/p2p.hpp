@@ -78,6 +78,13 @@ bool is_tempi_request(MPI_Request r);
 bool peek(MPI_Request r);
 // MPI_Request_free: the operation finishes in the background; *req = NULL
 void release(MPI_Request *req);
+// MPI_Request_get_status: complete? (status filled when it is; the request
+// stays until a wait / test / free)
+int get_status(MPI_Request r, int *flag, MPI_Status *status);
+// MPI_Cancel: a receive that nothing has matched yet is cancelled (its wait
+// then returns a status for which MPI_Test_cancelled is true); any other
+// operation completes normally, which MPI permits
+int cancel(MPI_Request r);
 // drive every TEMPI operation one step; returns true if anything moved.
 // full = false (from MPI_Isend / MPI_Irecv) leaves arrived messages' unpacks
 // queued so that a burst shares one launch; waits use full = true

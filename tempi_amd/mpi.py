@@ -283,6 +283,23 @@ class MPI:
         self._call("MPI_Wait", ctypes.byref(r), st)
         return r.value, self._decode(st, t)
 
+    def Cancel(self, req):
+        r = self.Request(req)
+        self._call("MPI_Cancel", ctypes.byref(r))
+
+    def Wait_cancelled(self, req):
+        """MPI_Wait, then MPI_Test_cancelled on its status"""
+        r, st, c = self.Request(req), self._status(), ctypes.c_int(0)
+        self._call("MPI_Wait", ctypes.byref(r), st)
+        self._call("MPI_Test_cancelled", st, ctypes.byref(c))
+        return r.value, bool(c.value)
+
+    def Request_get_status(self, req, t):
+        """(complete?, (source, tag, count of t) when complete); the request stays"""
+        st, flag = self._status(), ctypes.c_int(0)
+        self._call("MPI_Request_get_status", self.Request(req), ctypes.byref(flag), st)
+        return bool(flag.value), (self._decode(st, t) if flag.value else None)
+
     def Recv_status(self, buf, count, t, source, tag, comm=None):
         """MPI_Recv with a status: (source, tag, count of t)"""
         st = self._status()

@@ -92,6 +92,46 @@ for it, recipe in enumerate(RECIPES * 2):
         fail(f"{recipe}: received bytes differ ({'blocking' if blocking else 'Irecv'})")
     typezoo.free(mpi, probe_t, probe_temps, probe_basic)
 
+# MPI_Request_get_status leaves the request; MPI_Cancel of a receive nothing
+# will match (tag 999) completes it as cancelled
+recipe = RECIPES[0]
+tm = pyoracle.TypeMap(recipe)
+origin, buflen = tm.geometry(1)
+t, temps, basic = typezoo.build(mpi, recipe)
+s_host, s_dev = buf(buflen, 31 + rank)
+canvas, r_dev = buf(buflen, 32)
+rreq = mpi.Irecv(ptr(r_dev) + origin, 1, t, src_rank, 77)
+sreq = mpi.Isend(ptr(s_dev) + origin, 1, t, peer, 77)
+while True:
+    flag, st = mpi.Request_get_status(rreq, t)
+    if flag:
+        break
+if st != (src_rank, 77, 1):
+    fail(f"MPI_Request_get_status gave {st}, expected {(src_rank, 77, 1)}")
+_, (src_st, tag_st, n_st) = mpi.Wait_status(rreq, t)  # still a live request: the wait releases it
+if (src_st, tag_st, n_st) != (src_rank, 77, 1):
+    fail(f"wait after MPI_Request_get_status gave {(src_st, tag_st, n_st)}")
+mpi.Wait(sreq)
+exp = canvas.copy()
+tm.unpack(tm.pack(np.random.default_rng(31 + src_rank).integers(0, 256, buflen, dtype=np.uint8), origin, 1), exp,
+          origin, 1)
+if not np.array_equal(host(r_dev), exp):
+    fail("bytes after MPI_Request_get_status differ")
+for obj_recipe in RECIPES:  # strided (TEMPI receive) and irregular (library-packed receive)
+    ot, otemps, obasic = typezoo.build(mpi, obj_recipe)
+    otm = pyoracle.TypeMap(obj_recipe)
+    o_origin, o_len = otm.geometry(1)
+    canvas, r_dev = buf(o_len, 33)
+    creq = mpi.Irecv(ptr(r_dev) + o_origin, 1, ot, src_rank, 999)
+    mpi.Cancel(creq)
+    left, was_cancelled = mpi.Wait_cancelled(creq)
+    if not was_cancelled:
+        fail(f"{obj_recipe}: cancelled receive not reported as cancelled")
+    if not np.array_equal(host(r_dev), canvas):
+        fail(f"{obj_recipe}: a cancelled receive wrote its buffer")
+    typezoo.free(mpi, ot, otemps, obasic)
+typezoo.free(mpi, t, temps, basic)
+
 mpi.Finalize()
 print(f"RESULT errors={errors}", flush=True)
 sys.exit(1 if errors else 0)
