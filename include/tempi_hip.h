@@ -86,6 +86,8 @@ typedef struct tempi_hip_copy_item {
   const void *src_first;
   tempi_hip_desc dst;
   tempi_hip_desc src;
+  uint32_t flags; /* TEMPI_HIP_ITEM_REMOTE: src is another process's IPC-mapped memory */
+  uint32_t reserved_;
 } tempi_hip_copy_item;
 int tempi_hip_copy_supported(void *dst_first, const void *src_first,
                              const tempi_hip_desc *dst, const tempi_hip_desc *src);
@@ -152,6 +154,9 @@ int tempi_hip_memset_async(void *dst, int value, size_t n, void *stream);
 int tempi_hip_ipc_get_handle(void *handle_out, void *devptr);
 int tempi_hip_ipc_open_handle(void **devptr, const void *handle);
 int tempi_hip_ipc_close_handle(void *devptr);
+/* the device allocation holding p: its base, size and process-unique buffer
+   id (an allocation freed and replaced at the same address gets a new id) */
+int tempi_hip_mem_info(const void *p, void **base, size_t *size, uint64_t *buffer_id);
 
 const char *tempi_hip_error_string(int status);
 

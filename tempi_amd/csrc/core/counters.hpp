@@ -21,6 +21,7 @@ struct Counters {
   // had to be packed because their wait came before the matching receive
   uint64_t send_direct = 0, direct_fallbacks = 0;
   uint64_t neighbor_colls = 0; // neighbourhood collectives on device buffers
+  uint64_t send_ipc_copy = 0, copy_resends = 0; // IPC COPY sends; those answered through the host
   // kernel time of synchronous MPI_Pack / MPI_Unpack while profiling is on
   double pack_kernel_ms = 0, unpack_kernel_ms = 0;
   uint64_t pack_timed = 0, unpack_timed = 0;

@@ -62,6 +62,8 @@ TEMPI_EXPORT void tempi_get_counters(tempi_counters_t *o) {
   o->send_direct = c.send_direct;
   o->direct_fallbacks = c.direct_fallbacks;
   o->neighbor_colls = c.neighbor_colls;
+  o->send_ipc_copy = c.send_ipc_copy;
+  o->copy_resends = c.copy_resends;
 }
 
 TEMPI_EXPORT void tempi_reset_counters(void) { counters = Counters(); }

@@ -74,11 +74,13 @@ void finalize_before_mpi() {
   if (std::getenv("TEMPI_PRINT_COUNTERS")) {
     const Counters &c = counters;
     std::fprintf(stderr,
-                 "[tempi r%d] packs=%lu unpacks=%lu isends=%lu irecvs=%lu ipc=%lu oneshot=%lu staged=%lu direct=%lu/%lu "
+                 "[tempi r%d] packs=%lu unpacks=%lu isends=%lu irecvs=%lu ipc=%lu (copy %lu/%lu) oneshot=%lu staged=%lu "
+                 "direct=%lu/%lu "
                  "batches=%lu items=%lu passes=%lu | host ms: isend=%.2f irecv=%.2f flush=%.2f events=%.2f "
                  "testsome=%.2f wait=%.2f\n",
                  state.worldRank, (unsigned long)c.packs, (unsigned long)c.unpacks, (unsigned long)c.isends,
-                 (unsigned long)c.irecvs, (unsigned long)c.send_ipc, (unsigned long)c.send_oneshot,
+                 (unsigned long)c.irecvs, (unsigned long)c.send_ipc, (unsigned long)c.send_ipc_copy,
+                 (unsigned long)c.copy_resends, (unsigned long)c.send_oneshot,
                  (unsigned long)c.send_staged, (unsigned long)c.send_direct, (unsigned long)c.direct_fallbacks,
                  (unsigned long)c.batches, (unsigned long)c.batched_items,
                  (unsigned long)c.progress_passes, c.ns_isend * 1e-6, c.ns_irecv * 1e-6, c.ns_flush * 1e-6,

@@ -71,6 +71,34 @@ struct DirectDesc {
 };
 static_assert(sizeof(DirectDesc) == 160 && sizeof(DirectDesc) != sizeof(IpcDesc), "descriptor size");
 
+// IPC COPY (a large message between processes, wide rows): the descriptor
+// names the sender's own object through an IPC handle of its allocation, and
+// the receiver copies it strided -> strided straight out of the sender's
+// memory (tempi_hip_copy_batch, source read with system-scope loads). No
+// gather on the sender, no packed slab: the payload crosses xGMI once and
+// each HBM sees it once. The send completes when the receiver acknowledges
+// its copy (rendezvous), so only messages at least TEMPI_IPC_COPY_MIN_BYTES
+// take this route: as large as MPICH's own rendezvous messages, which no
+// correct program expects to be buffered. Narrow rows (< TEMPI_IPC_COPY_MIN_BLOCK)
+// are gathered on the sender instead: a 24-byte row read across xGMI costs a
+// whole remote line.
+constexpr uint64_t kMagicCopy = 0x54454d5049585043ull; // "TEMPIXPC"
+
+struct IpcCopyDesc {
+  uint64_t magic[2];
+  int64_t bytes;
+  int32_t senderWorld;
+  int32_t senderPid;
+  int32_t ackTag;
+  int32_t device;
+  uint64_t bufferId; // the sender allocation's id: the receiver's mapping cache key
+  uint64_t offset;   // of the object's first byte from the allocation base
+  uint64_t rawFirst; // the first byte, in the sender's address space
+  unsigned char handle[TEMPI_HIP_IPC_HANDLE_BYTES];
+  tempi_hip_desc desc; // the object's shape, element count folded in
+};
+static_assert(sizeof(IpcCopyDesc) == 224, "descriptor size");
+
 struct Op;
 struct DirectShared {
   DirectDesc desc{}; // the library's send buffer: alive until the receiver claims it
@@ -102,6 +130,18 @@ std::vector<std::unique_ptr<PendingAck>> pendingAcks; // stable addresses: Irecv
 
 // peer slabs mapped into this process: (world rank, slab id) -> base
 std::map<std::pair<int, uint64_t>, void *> ipcOpen;
+// peer allocations mapped for IPC COPY: (world rank, buffer id) -> base
+std::map<std::pair<int, uint64_t>, void *> ipcAllocOpen;
+// this process's allocations exported for IPC COPY: base -> (buffer id, handle)
+struct Export {
+  uint64_t id;
+  unsigned char handle[TEMPI_HIP_IPC_HANDLE_BYTES];
+};
+std::unordered_map<uintptr_t, Export> ipcExports;
+bool ipcCopyEnabled = true;             // TEMPI_NO_IPC_COPY
+int64_t ipcCopyMinBytes = 64 * 1024;    // TEMPI_IPC_COPY_MIN_BYTES
+int64_t ipcCopyMinBlock = 256;          // TEMPI_IPC_COPY_MIN_BLOCK
+uint32_t nextCopyTag = 0;
 
 // A datatype handle that stays valid while an operation still needs it:
 // the application may MPI_Type_free its type right after MPI_Isend /
@@ -222,12 +262,60 @@ void *peer_pointer(const IpcDesc &d) {
 
 // ack payload: 0 = pulled, release the slab; 1 = could not map it, send the
 // bytes through the host on (ctrlComm, ackTag)
-int ackCodes[2] = {0, 1};
+int ackCodes[3] = {0, 1, 2};
 
-void send_ack(const IpcDesc &d, int code = 0) {
+void send_ack(int world, int tag, int code) {
   MPI_Request r;
-  next.MPI_Isend(&ackCodes[code], 1, MPI_INT, d.senderWorld, d.ackTag, ctrlComm, &r);
-  MPI_Request_free(&r);
+  next.MPI_Isend(&ackCodes[code], 1, MPI_INT, world, tag, ctrlComm, &r);
+  next.MPI_Request_free(&r);
+}
+void send_ack(const IpcDesc &d, int code = 0) { send_ack(d.senderWorld, d.ackTag, code); }
+
+// IPC COPY acks: 0 = copied; 1 = cannot copy this shape, send the packed
+// bytes through the host on (ctrlComm, ackTag); 2 = the same, and the
+// sender's memory could not be mapped (no more IPC with that rank)
+enum { kCopyDone = 0, kCopyResend = 1, kCopyUnmapped = 2 };
+
+// the sender's allocation mapped into this process (its first byte), or
+// nullptr when it cannot be
+const char *peer_object(const IpcCopyDesc &d) {
+  if (d.senderPid == int32_t(getpid())) return reinterpret_cast<const char *>(d.rawFirst);
+  auto key = std::make_pair(int(d.senderWorld), d.bufferId);
+  auto it = ipcAllocOpen.find(key);
+  if (it == ipcAllocOpen.end()) {
+    void *p = nullptr;
+    static const bool injectFault = std::getenv("TEMPI_FAULT_IPC_OPEN") != nullptr;
+    const int e = injectFault ? 1 : tempi_hip_ipc_open_handle(&p, d.handle);
+    if (e != 0) {
+      LOG_WARN("cannot map rank " << d.senderWorld << "'s buffer: " << tempi_hip_error_string(e));
+      mark_ipc_broken(d.senderWorld);
+      return nullptr;
+    }
+    it = ipcAllocOpen.emplace(key, p).first;
+  }
+  return static_cast<const char *>(it->second) + d.offset;
+}
+
+// this process's allocation holding `first` exported for IPC COPY: fills the
+// descriptor's handle / buffer id / offset; false when it cannot be exported
+// (not hipMalloc memory, or the export fails)
+bool export_object(const void *first, IpcCopyDesc *d) {
+  void *base = nullptr;
+  size_t size = 0;
+  uint64_t id = 0;
+  if (tempi_hip_mem_info(first, &base, &size, &id) != 0 || !base) return false;
+  const uintptr_t b = reinterpret_cast<uintptr_t>(base);
+  auto it = ipcExports.find(b);
+  if (it == ipcExports.end() || it->second.id != id) { // new, or freed and replaced at the same address
+    Export x;
+    x.id = id;
+    if (tempi_hip_ipc_get_handle(x.handle, base) != 0) return false;
+    it = ipcExports.insert_or_assign(b, x).first;
+  }
+  d->bufferId = id;
+  d->offset = uint64_t(reinterpret_cast<uintptr_t>(first) - b);
+  std::memcpy(d->handle, it->second.handle, sizeof d->handle);
+  return true;
 }
 
 // ---------------------------------------------------------------- operations
@@ -482,6 +570,19 @@ void flush() {
   flush_list(pendingUnpack, false);
 }
 
+// Peer allocations stay mapped for reuse (keyed by buffer id). A peer that
+// keeps allocating new buffers would make that grow without bound and hold
+// its freed memory alive, so past kMaxAllocMaps every mapping is closed --
+// after the copies that may still read them have been launched and run.
+constexpr size_t kMaxAllocMaps = 256;
+void recycle_alloc_maps() {
+  if (ipcAllocOpen.size() < kMaxAllocMaps) return;
+  flush_list(pendingUnpack, false);
+  gpu::check(tempi_hip_device_synchronize(), "ipc mapping recycle");
+  for (auto &kv : ipcAllocOpen) tempi_hip_ipc_close_handle(kv.second);
+  ipcAllocOpen.clear();
+}
+
 struct IsendOp : Op {
   RecordRef rec;      // the type (kept alive: MPI_Type_free may come first)
   const char *origin; // GPU-visible
@@ -646,6 +747,62 @@ struct IsendDirectOp : Op {
   }
 };
 
+// IPC COPY sender: posts the descriptor, then waits for the receiver's ack
+// (its copy out of this process's memory has run). A NACK (the receiver
+// cannot copy this shape, or cannot map the memory) is answered by gathering
+// the object into pinned host memory here and sending those bytes on
+// (ctrlComm, ackTag), where the receiver has already posted for them.
+struct IsendCopyOp : Op {
+  RecordRef rec;
+  const char *origin; // GPU-visible
+  int count, dest, tag, peer;
+  MPI_Datatype dt;
+  MPI_Comm comm;
+  int64_t bytes;
+  IpcCopyDesc desc{};
+  int ack = -1;
+
+  IsendCopyOp(const TypeRecord *r, const char *o, int c, MPI_Datatype d, int de, int t, MPI_Comm cm, int dev,
+              int64_t b, int peerWorld, const IpcCopyDesc &filled)
+      : rec(r->ref()), origin(o), count(c), dest(de), tag(t), peer(peerWorld), dt(d), comm(cm), bytes(b),
+        desc(filled) {
+    device = dev;
+    post_or_queue(gate_key(comm, dest), this);
+  }
+  void post() override {
+    next.MPI_Irecv(&ack, 1, MPI_INT, peer, desc.ackTag, ctrlComm, &lib);
+    watch(this);
+    MPI_Request r; // the descriptor lives in this op until the ack, which follows its delivery
+    next.MPI_Isend(&desc, int(sizeof desc), MPI_PACKED, dest, tag, comm, &r);
+    next.MPI_Request_free(&r);
+  }
+  void lib_done(const MPI_Status &) override {
+    if (ack != kCopyDone) {
+      if (ack == kCopyUnmapped) mark_ipc_broken(peer);
+      counters.copy_resends++;
+      Slab *h = pinned_pool().get(size_t(std::max<int64_t>(bytes, 1)), device);
+      void *s = gpu::stream(device);
+      int cur = 0;
+      tempi_hip_get_device(&cur);
+      if (cur != device) tempi_hip_set_device(device);
+      gpu::check(rec->packer->pack_async(h->dev, origin, count, s), "ipc copy fallback gather");
+      gpu::check(tempi_hip_stream_synchronize(s), "ipc copy fallback sync");
+      if (cur != device) tempi_hip_set_device(cur);
+      next.MPI_Send(h->host, int(bytes), MPI_PACKED, peer, desc.ackTag, ctrlComm); // receive already posted
+      pinned_pool().put(h);
+    }
+    done = true;
+  }
+  void status(MPI_Status *s) const override {
+    if (s != MPI_STATUS_IGNORE) {
+      s->MPI_SOURCE = MPI_ANY_SOURCE;
+      s->MPI_TAG = MPI_ANY_TAG;
+      s->MPI_ERROR = MPI_SUCCESS;
+      MPI_Status_set_elements(s, MPI_BYTE, 0);
+    }
+  }
+};
+
 // the receiver side is done with a direct send's bytes
 void direct_finish(std::shared_ptr<DirectShared> &sh) {
   if (!sh) return;
@@ -692,6 +849,12 @@ bool is_direct(const void *msg, int n) {
   std::memcpy(m, msg, sizeof m);
   return m[0] == kMagicDirect && m[1] == kMagic1;
 }
+bool is_ipc_copy(const void *msg, int n) {
+  if (size_t(n) != sizeof(IpcCopyDesc)) return false;
+  uint64_t m[2];
+  std::memcpy(m, msg, sizeof m);
+  return m[0] == kMagicCopy && m[1] == kMagic1;
+}
 bool is_ipc(const void *msg, int n) {
   if (size_t(n) != sizeof(IpcDesc)) return false;
   uint64_t m[2];
@@ -713,6 +876,25 @@ void land_descriptor(const void *msg, int n, std::vector<char> &out) {
     pinned_pool().put(h);
     return;
   }
+  auto resend = [&](int world, int tag, int64_t bytes, int code) { // the sender gathers and sends the bytes
+    MPI_Request r;
+    next.MPI_Irecv(out.data(), int(bytes), MPI_PACKED, world, tag, ctrlComm, &r);
+    send_ack(world, tag, code);
+    for (;;) {
+      int flag = 0;
+      next.MPI_Test(&r, &flag, MPI_STATUS_IGNORE);
+      if (flag) break;
+      progress();
+    }
+  };
+  if (is_ipc_copy(msg, n)) { // a host receive: the sender gathers for it
+    IpcCopyDesc d;
+    std::memcpy(&d, msg, sizeof d);
+    out.resize(size_t(std::max<int64_t>(d.bytes, 1)));
+    resend(d.senderWorld, d.ackTag, d.bytes, kCopyResend);
+    out.resize(size_t(d.bytes));
+    return;
+  }
   IpcDesc d;
   std::memcpy(&d, msg, sizeof d);
   out.resize(size_t(std::max<int64_t>(d.bytes, 1)));
@@ -720,20 +902,12 @@ void land_descriptor(const void *msg, int n, std::vector<char> &out) {
     gpu::check(tempi_hip_memcpy(out.data(), static_cast<const char *>(base) + d.offset, size_t(d.bytes)), "ipc pull");
     send_ack(d);
   } else { // the sender re-sends through the host
-    MPI_Request r;
-    next.MPI_Irecv(out.data(), int(d.bytes), MPI_PACKED, d.senderWorld, d.ackTag, ctrlComm, &r);
-    send_ack(d, 1);
-    for (;;) {
-      int flag = 0;
-      next.MPI_Test(&r, &flag, MPI_STATUS_IGNORE);
-      if (flag) break;
-      progress();
-    }
+    resend(d.senderWorld, d.ackTag, d.bytes, 1);
   }
   out.resize(size_t(d.bytes));
 }
 
-constexpr size_t kDescCap = sizeof(DirectDesc) > sizeof(IpcDesc) ? sizeof(DirectDesc) : sizeof(IpcDesc);
+constexpr size_t kDescCap = std::max({sizeof(DirectDesc), sizeof(IpcDesc), sizeof(IpcCopyDesc)});
 
 int64_t desc_bytes(const tempi_hip_desc &d) {
   int64_t b = d.block;
@@ -765,6 +939,8 @@ struct IrecvOp : Op {
   std::shared_ptr<DirectShared> direct; // a same-process send being copied / unpacked
   bool arrived = false;   // the library receive matched
   bool cancelled = false; // MPI_Cancel took effect
+  bool xcopy = false;     // an IPC COPY out of the sender's memory: ack it when done
+  int copyWorld = -1, copyTag = 0;
 
   IrecvOp(const TypeRecord *r, char *o, int c, MPI_Datatype d, int source, int tag, MPI_Comm cm, int dev,
           int64_t b)
@@ -828,7 +1004,7 @@ struct IrecvOp : Op {
       if (direct->state == DirectShared::PENDING && sameDevice && elems * size == dd.bytes &&
           rec->flat(elems, &mine) && copy_ok(mine, dd.desc)) {
         direct->state = DirectShared::CLAIMED;
-        tempi_hip_copy_item c;
+        tempi_hip_copy_item c{};
         c.dst_first = first;
         c.src_first = reinterpret_cast<const void *>(dd.first);
         c.dst = mine;
@@ -843,6 +1019,38 @@ struct IrecvOp : Op {
         pendingUnpack.add_items(this, packer, hslab->dev, origin, elems);
       }
       pendingUnpack.queue(this);
+      return;
+    }
+    if (is_ipc_copy(hslab->host, n)) {
+      IpcCopyDesc xd;
+      std::memcpy(&xd, hslab->host, sizeof xd);
+      if (xd.bytes > bytes) LOG_FATAL("message truncated: " << xd.bytes << " B into " << bytes);
+      elems = size ? xd.bytes / size : 0;
+      const bool local = xd.senderPid == int32_t(getpid());
+      if (!local) recycle_alloc_maps();
+      const char *src = (local && xd.device != device) ? nullptr : peer_object(xd);
+      tempi_hip_desc mine;
+      if (src && elems * size == xd.bytes && rec->flat(elems, &mine) && copy_ok(mine, xd.desc)) {
+        xcopy = true;
+        copyWorld = xd.senderWorld;
+        copyTag = xd.ackTag;
+        tempi_hip_copy_item c{};
+        c.dst_first = origin + packer.desc().start;
+        c.src_first = src;
+        c.dst = mine;
+        c.src = xd.desc;
+        if (!local) c.flags = TEMPI_HIP_ITEM_REMOTE; // the sender's memory changes between messages
+        pendingUnpack.add_copy(this, c);
+        pendingUnpack.queue(this);
+        return;
+      }
+      // a shape the copy kernel does not take, or memory we cannot map: the
+      // sender gathers and sends the bytes through the host
+      fallback = true;
+      desc.bytes = xd.bytes;
+      next.MPI_Irecv(hslab->host, int(xd.bytes), MPI_PACKED, xd.senderWorld, xd.ackTag, ctrlComm, &lib);
+      watch(this);
+      send_ack(xd.senderWorld, xd.ackTag, (src || local) ? kCopyResend : kCopyUnmapped);
       return;
     }
     if (size_t(n) == sizeof(IpcDesc) && d.magic[0] == kMagic0 && d.magic[1] == kMagic1) {
@@ -873,6 +1081,7 @@ struct IrecvOp : Op {
   }
   void gpu_done() override {
     if (ipc) send_ack(desc);
+    if (xcopy) send_ack(copyWorld, copyTag, kCopyDone);
     direct_finish(direct);
     pinned_pool().put(hslab);
     hslab = nullptr;
@@ -967,7 +1176,7 @@ struct LibIrecvOp : Op {
     }
     int n = 0, size = 0;
     MPI_Get_count(&libStatus, MPI_PACKED, &n);
-    if (is_direct(buf.data(), n) || is_ipc(buf.data(), n)) { // a TEMPI sender's descriptor
+    if (is_direct(buf.data(), n) || is_ipc(buf.data(), n) || is_ipc_copy(buf.data(), n)) { // a TEMPI descriptor
       std::vector<char> bytes;
       land_descriptor(buf.data(), n, bytes);
       buf.swap(bytes);
@@ -1030,6 +1239,9 @@ void init() {
   gpuAwareLibrary = std::getenv("TEMPI_MPI_GPU_AWARE") != nullptr;
   directEnabled = std::getenv("TEMPI_NO_DIRECT") == nullptr;
   ipcSystemLoads = std::getenv("TEMPI_IPC_PLAIN_LOADS") == nullptr;
+  ipcCopyEnabled = std::getenv("TEMPI_NO_IPC_COPY") == nullptr;
+  if (const char *s = std::getenv("TEMPI_IPC_COPY_MIN_BYTES")) ipcCopyMinBytes = std::atoll(s);
+  if (const char *s = std::getenv("TEMPI_IPC_COPY_MIN_BLOCK")) ipcCopyMinBlock = std::atoll(s);
   if (const char *s = std::getenv("TEMPI_EARLY_FLUSH")) earlyFlush = size_t(std::max(1, std::atoi(s)));
   firstFlush = std::min<size_t>(16, earlyFlush);
   if (const char *s = std::getenv("TEMPI_FIRST_FLUSH")) firstFlush = size_t(std::max(1, std::atoi(s)));
@@ -1084,6 +1296,9 @@ void finalize() {
   eventPool.clear();
   for (auto &kv : ipcOpen) tempi_hip_ipc_close_handle(kv.second);
   ipcOpen.clear();
+  for (auto &kv : ipcAllocOpen) tempi_hip_ipc_close_handle(kv.second);
+  ipcAllocOpen.clear();
+  ipcExports.clear();
   if (ctrlComm != MPI_COMM_NULL) MPI_Comm_free(&ctrlComm);
   device_pool().release_all();
   pinned_pool().release_all();
@@ -1143,6 +1358,27 @@ int isend(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Co
   case Method::DEVICE: counters.send_device++; break;
   case Method::IPC: counters.send_ipc++; break;
   default: break;
+  }
+  // IPC COPY: a large message of wide rows is copied by the receiver straight
+  // out of this process's object (no gather, no slab)
+  if (m == Method::IPC && ipcCopyEnabled && bytes >= ipcCopyMinBytes && rec->flat(count, &flat) &&
+      flat.ndims <= 3 && flat.block >= ipcCopyMinBlock && bytes < (int64_t(1) << 31)) {
+    IpcCopyDesc d{};
+    d.magic[0] = kMagicCopy;
+    d.magic[1] = kMagic1;
+    d.bytes = bytes;
+    d.senderWorld = state.worldRank;
+    d.senderPid = int32_t(getpid());
+    d.device = p.device;
+    d.rawFirst = reinterpret_cast<uint64_t>(origin + rec->desc.start);
+    d.desc = flat;
+    const int half = std::max(1, tagUb / 2);
+    d.ackTag = half + int32_t(nextCopyTag++ % uint32_t(half)); // slab ids (the IPC acks) stay below
+    if (export_object(origin + rec->desc.start, &d)) {
+      counters.send_ipc_copy++;
+      *req = add(std::make_unique<IsendCopyOp>(rec, origin, count, dt, dest, tag, comm, p.device, bytes, destWorld, d));
+      return MPI_SUCCESS;
+    }
   }
   int cur = 0;
   tempi_hip_get_device(&cur);
@@ -1394,7 +1630,8 @@ int recv_host_ipc_aware(void *buf, int count, MPI_Datatype dt, int source, int t
   *handled = true;
   int n = 0;
   MPI_Get_count(&st, MPI_BYTE, &n);
-  if (size_t(n) != sizeof(IpcDesc) && size_t(n) != sizeof(DirectDesc)) return MPI_Mrecv(buf, count, dt, &msg, status);
+  if (size_t(n) != sizeof(IpcDesc) && size_t(n) != sizeof(DirectDesc) && size_t(n) != sizeof(IpcCopyDesc))
+    return MPI_Mrecv(buf, count, dt, &msg, status);
   alignas(16) char raw[kDescCap];
   MPI_Mrecv(raw, n, MPI_BYTE, &msg, &st);
   int size = 0;
@@ -1402,7 +1639,7 @@ int recv_host_ipc_aware(void *buf, int count, MPI_Datatype dt, int source, int t
   std::vector<char> packed;
   int nbytes = n;
   const char *src = raw;
-  if (is_direct(raw, n) || is_ipc(raw, n)) { // a TEMPI sender's descriptor: fetch what it names
+  if (is_direct(raw, n) || is_ipc(raw, n) || is_ipc_copy(raw, n)) { // a TEMPI descriptor: fetch what it names
     land_descriptor(raw, n, packed);
     src = packed.data();
     nbytes = int(packed.size());

@@ -963,7 +963,46 @@ struct CArgs {
   // instead of as a partial-sector write (a read-modify-write in DRAM)
   char *s2, *d2; // nullptr: not paired
   uint32_t nwords;
+  uint32_t flags; // TEMPI_HIP_ITEM_REMOTE: the source is another process's memory
 };
+
+// A system-scope (sc0 sc1) load through the flat global path, complete on
+// return: the source side of a copy may have any stride sign, so the
+// wave-uniform buffer base of ld_remote cannot be used. One load in flight
+// per lane is enough here: these reads cross xGMI, whose link rate, not the
+// latency, bounds them (256 CUs x 8 waves x 64 lanes x 8 B in flight / ~2 us
+// is well over a link's bandwidth).
+template <typename T> __device__ __forceinline__ T ld_sys(const T *p) {
+  T v;
+  if constexpr (sizeof(T) == 16) {
+    u32x4 x;
+    asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=v"(x) : "v"(p) : "memory");
+    __builtin_memcpy(&v, &x, 16);
+  } else if constexpr (sizeof(T) == 8) {
+    u32x2 x;
+    asm volatile("global_load_dwordx2 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=v"(x) : "v"(p) : "memory");
+    __builtin_memcpy(&v, &x, 8);
+  } else if constexpr (sizeof(T) == 4) {
+    uint32_t x;
+    asm volatile("global_load_dword %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=v"(x) : "v"(p) : "memory");
+    __builtin_memcpy(&v, &x, 4);
+  } else if constexpr (sizeof(T) == 2) {
+    uint32_t x;
+    asm volatile("global_load_ushort %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=v"(x) : "v"(p) : "memory");
+    const uint16_t h = uint16_t(x);
+    __builtin_memcpy(&v, &h, 2);
+  } else {
+    uint32_t x;
+    asm volatile("global_load_ubyte %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=v"(x) : "v"(p) : "memory");
+    const uint8_t b = uint8_t(x);
+    __builtin_memcpy(&v, &b, 1);
+  }
+  return v;
+}
+template <typename T> __device__ __forceinline__ T ld_src(const CArgs &a, const T *p, bool nt) {
+  if (a.flags & TEMPI_HIP_ITEM_REMOTE) return ld_sys(p);
+  return ld(p, nt);
+}
 
 template <int W> __device__ __forceinline__ int64_t side_offset(uint32_t q, const CSide &c) {
   uint32_t row = mdiv(q, c.mwpr);
@@ -995,8 +1034,8 @@ template <int W> __device__ __forceinline__ void copy_body(const CArgs &a, uint3
         so[j] = q < a.nwords ? side_offset<W>(q, a.s) : 0;
         dof[j] = q < a.nwords ? side_offset<W>(q, a.d) : 0;
         if (q < a.nwords) {
-          v[j] = ld(reinterpret_cast<const WT *>(a.s.first + so[j]), false);
-          v2[j] = ld(reinterpret_cast<const WT *>(a.s2 + so[j]), false);
+          v[j] = ld_src(a, reinterpret_cast<const WT *>(a.s.first + so[j]), false);
+          v2[j] = ld_src(a, reinterpret_cast<const WT *>(a.s2 + so[j]), false);
         }
       }
 #pragma unroll
@@ -1015,7 +1054,7 @@ template <int W> __device__ __forceinline__ void copy_body(const CArgs &a, uint3
 #pragma unroll
     for (int j = 0; j < CW; ++j) {
       const uint32_t q = base + uint32_t(j) * kBlock + threadIdx.x;
-      if (q < a.nwords) v[j] = ld(reinterpret_cast<const WT *>(a.s.first + side_offset<W>(q, a.s)), nt);
+      if (q < a.nwords) v[j] = ld_src(a, reinterpret_cast<const WT *>(a.s.first + side_offset<W>(q, a.s)), nt);
     }
 #pragma unroll
     for (int j = 0; j < CW; ++j) {
@@ -1090,6 +1129,7 @@ bool plan_copy(void *dst, const void *src, const tempi_hip_desc *dd, const tempi
   if (!make_side(const_cast<char *>(static_cast<const char *>(src)), ns, w, &job->a.s)) return false;
   if (!make_side(static_cast<char *>(dst), nd, w, &job->a.d)) return false;
   job->a.nwords = uint32_t(bytes / w);
+  job->a.flags = 0;
   job->a.s2 = job->a.d2 = nullptr;
   job->w = w;
   return true;
@@ -1116,7 +1156,7 @@ std::vector<CopyJob> pair_jobs(const std::vector<CopyJob> &in) {
     if (used[i]) continue;
     CopyJob j = in[i];
     for (size_t k = i + 1; k < in.size() && k < i + 64; ++k) {
-      if (used[k] || in[k].a.nwords != j.a.nwords || !same_shape(in[k].a.s, j.a.s) ||
+      if (used[k] || in[k].a.nwords != j.a.nwords || in[k].a.flags != j.a.flags || !same_shape(in[k].a.s, j.a.s) ||
           !same_shape(in[k].a.d, j.a.d))
         continue;
       j.a.s2 = in[k].a.s.first;
@@ -1182,6 +1222,7 @@ int tempi_hip_copy_batch(const tempi_hip_copy_item *items, int n, void *stream) 
     CopyJob j;
     if (!plan_copy(items[i].dst_first, items[i].src_first, &items[i].dst, &items[i].src, &j))
       return int(hipErrorInvalidValue);
+    j.a.flags = items[i].flags;
     if (j.a.nwords == 0) continue;
     const int wi = j.w == 1 ? 0 : j.w == 2 ? 1 : j.w == 4 ? 2 : j.w == 8 ? 3 : 4;
     groups[wi].push_back(j);

@@ -156,6 +156,26 @@ int tempi_hip_ipc_open_handle(void **devptr, const void *handle) {
 }
 int tempi_hip_ipc_close_handle(void *devptr) { RET(hipIpcCloseMemHandle(devptr)); }
 
+int tempi_hip_mem_info(const void *p, void **base, size_t *size, uint64_t *buffer_id) {
+  hipDeviceptr_t b = nullptr;
+  size_t n = 0;
+  hipError_t e = hipMemGetAddressRange(&b, &n, const_cast<void *>(p));
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    RET(e);
+  }
+  unsigned long long id = 0;
+  e = hipPointerGetAttribute(&id, HIP_POINTER_ATTRIBUTE_BUFFER_ID, const_cast<void *>(p));
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    RET(e);
+  }
+  *base = b;
+  *size = n;
+  *buffer_id = uint64_t(id);
+  return 0;
+}
+
 const char *tempi_hip_error_string(int status) {
   return hipGetErrorString(static_cast<hipError_t>(status));
 }

@@ -23,7 +23,10 @@ pytestmark = pytest.mark.gpu
 
 class CopyItem(ctypes.Structure):
     _fields_ = [("dst_first", ctypes.c_void_p), ("src_first", ctypes.c_void_p), ("dst", HipDesc),
-                ("src", HipDesc)]
+                ("src", HipDesc), ("flags", ctypes.c_uint32), ("reserved_", ctypes.c_uint32)]
+
+
+ITEM_REMOTE = 1  # TEMPI_HIP_ITEM_REMOTE
 
 
 def _hip():
@@ -64,12 +67,14 @@ def _reshape(rng, size):
     return f"vector({nb},{bl},{2 * bl},byte)", 1
 
 
+@pytest.mark.parametrize("remote", [False, True])
 @pytest.mark.parametrize("seed", range(8))
-def test_copy_kernel_c_abi(mpi, gpu, seed):
+def test_copy_kernel_c_abi(mpi, gpu, seed, remote):
     """tempi_hip_copy_batch: 1-60 (src, dst) pairs of equal size -- same shape
     at other offsets (the halo case), or a different shape entirely -- mixed
     word widths and ranks in one call; the canvas outside each dst type map
-    stays untouched."""
+    stays untouched. remote: two items in three carry TEMPI_HIP_ITEM_REMOTE
+    (source read with system-scope loads, the IPC-copy route)."""
     import torch
 
     H = _hip()
@@ -104,6 +109,7 @@ def test_copy_kernel_c_abi(mpi, gpu, seed):
         it.src_first = src.data_ptr() + so + sshift + sd["start"]
         it.dst_first = dst.data_ptr() + do + dshift + dd["start"]
         it.src, it.dst = sdesc, ddesc
+        it.flags = ITEM_REMOTE if remote and i % 3 != 0 else 0
         ok = H.tempi_hip_copy_supported(it.dst_first, it.src_first, ctypes.byref(it.dst), ctypes.byref(it.src))
         if not ok:
             continue

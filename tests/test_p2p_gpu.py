@@ -20,6 +20,8 @@ METHODS = {
     "DEVICE": {"TEMPI_DATATYPE_DEVICE": "1"},  # no GPU-aware MPI here: IPC intra-node
     # IPC whose peer mapping fails (fault injection): NACK -> host re-send
     "IPC_FAULT": {"TEMPI_DATATYPE_IPC": "1", "TEMPI_FAULT_IPC_OPEN": "1"},
+    # IPC COPY for every size and row width (the receiver copies out of the sender's object)
+    "XCOPY": {"TEMPI_DATATYPE_IPC": "1", "TEMPI_IPC_COPY_MIN_BYTES": "1", "TEMPI_IPC_COPY_MIN_BLOCK": "1"},
 }
 
 
@@ -59,7 +61,13 @@ def test_pingpong_nd(gpu, method, total, block):
     # multi-lane configuration of one rank per GPU (scatters on lanes 1-3)
     (2, "40", {"TEMPI_STREAMS": "4"}, []), (4, "64 64 16", {"TEMPI_STREAMS": "3"}, []),
     (4, "32", {"TEMPI_STREAMS": "3"}, ["--neighbor"]), (2, "40", {"TEMPI_STREAMS": "3", "TEMPI_NO_DIRECT": "1"}, []),
-    (1, "48", {"TEMPI_STREAMS": "1"}, [])])
+    (1, "48", {"TEMPI_STREAMS": "1"}, []),
+    # IPC COPY: wide rows only (the default row limit), every row, with lanes, unmappable
+    (2, "40", {"TEMPI_IPC_COPY_MIN_BYTES": "1"}, []),
+    (4, "64 64 16", {"TEMPI_IPC_COPY_MIN_BYTES": "1", "TEMPI_IPC_COPY_MIN_BLOCK": "1"}, []),
+    (2, "40", {"TEMPI_IPC_COPY_MIN_BYTES": "1", "TEMPI_IPC_COPY_MIN_BLOCK": "1", "TEMPI_STREAMS": "3"}, []),
+    (2, "40", {"TEMPI_IPC_COPY_MIN_BYTES": "1", "TEMPI_FAULT_IPC_OPEN": "1"}, []),
+    (4, "32", {"TEMPI_IPC_COPY_MIN_BYTES": "1", "TEMPI_IPC_COPY_MIN_BLOCK": "1"}, ["--neighbor"])])
 def test_halo_exchange_content(gpu, ranks, grid, env, extra):
     rc, out = mpi_launch.run(ranks, [os.path.join(LIB, "halo_exchange"), "2"] + grid.split() + ["--quants", "2", "--check"] + extra,
                              env=env, timeout=300)
@@ -98,7 +106,7 @@ def test_alltoallv_sparse_app(gpu, ranks, scale, density):
     assert rc == 0 and r["checked"] and r["errors"] == 0, out[-3000:]
 
 
-@pytest.mark.parametrize("method", ["AUTO", "ONESHOT", "IPC", "STAGED"])
+@pytest.mark.parametrize("method", ["AUTO", "ONESHOT", "IPC", "STAGED", "XCOPY"])
 def test_completion_family_device(gpu, method):
     """TEMPI device requests mixed with library requests through
     MPI_Testall / Testany / Waitany / Testsome / Waitsome / Request_free"""
@@ -106,8 +114,21 @@ def test_completion_family_device(gpu, method):
     assert rc == 0 and "RESULT errors=0" in out, out[-3000:]
 
 
+@pytest.mark.parametrize("env", [METHODS["XCOPY"], dict(METHODS["XCOPY"], TEMPI_FAULT_IPC_OPEN="1"),
+                                 dict(METHODS["XCOPY"], TEMPI_STREAMS="3")], ids=["copy", "unmapped", "lanes"])
+def test_ipc_copy_receivers(gpu, env):
+    """IPC COPY against every receiver: same and other strided shapes (copy
+    kernel), a receive type too deep for it and a host receive (the sender
+    gathers and re-sends through the host), a blocking receive, and one send
+    buffer rewritten and re-sent (no stale bytes through the peer mapping)"""
+    rc, out = mpi_launch.run(2, mpi_launch.py("xcopy.py"), env=env, timeout=120)
+    assert rc == 0 and "RESULT errors=0" in out, out[-3000:]
+    if "TEMPI_FAULT_IPC_OPEN" not in env:
+        assert "rank 0 counters ipc_copy=8 resends=2" in out, out[-3000:]
+
+
 @pytest.mark.parametrize("n,method", [(2, "AUTO"), (2, "ONESHOT"), (2, "IPC"), (2, "STAGED"), (1, "AUTO"),
-                                      (1, "NO_DIRECT")])
+                                      (1, "NO_DIRECT"), (2, "XCOPY")])
 def test_receive_status_and_freed_types(gpu, n, method):
     """MPI_Status source / tag / MPI_Get_count of device receives (fewer
     elements than allowed), with both datatypes freed before the wait"""
@@ -119,7 +140,7 @@ def test_receive_status_and_freed_types(gpu, n, method):
 
 
 @pytest.mark.parametrize("n,method", [(2, "AUTO"), (2, "ONESHOT"), (2, "IPC"), (2, "STAGED"), (1, "AUTO"),
-                                      (1, "NO_DIRECT"), (2, "LANES")])
+                                      (1, "NO_DIRECT"), (2, "LANES"), (2, "XCOPY")])
 def test_send_order_across_routes(gpu, n, method):
     """MPI non-overtaking: a gathered strided send, a host send, a
     library-packed irregular send and another strided send to one peer with
