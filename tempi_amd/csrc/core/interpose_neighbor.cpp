@@ -33,6 +33,7 @@
 #include "counters.hpp"
 #include "gpu.hpp"
 #include "next_mpi.hpp"
+#include "p2p.hpp"
 #include "state.hpp"
 #include "type_cache.hpp"
 
@@ -110,15 +111,41 @@ int isir(const void *sendbuf, const int *scounts, const MPI_Aint *sdispls, const
   const int tag = 0x4E41; // "NA": alone on the private communicator
   std::vector<MPI_Request> reqs;
   reqs.reserve(in.size() + out.size());
+  // Self edges: the k-th edge to this rank meets the k-th edge from it (edge
+  // order, as message matching would pair them). Each such pair whose blocks
+  // are device objects is one strided -> strided copy queued right here, with
+  // no library messages; the rest go as messages, still in edge order.
+  std::vector<char> doneIn(in.size(), 0), doneOut(out.size(), 0);
+  int me = 0;
+  next.MPI_Comm_rank(c, &me);
+  {
+    std::vector<size_t> selfIn, selfOut;
+    for (size_t j = 0; j < in.size(); ++j)
+      if (in[j] == me) selfIn.push_back(j);
+    for (size_t i = 0; i < out.size(); ++i)
+      if (out[i] == me) selfOut.push_back(i);
+    bool any = false;
+    for (size_t k = 0; k < selfIn.size() && k < selfOut.size(); ++k) {
+      const size_t i = selfOut[k], j = selfIn[k];
+      MPI_Request r;
+      if (p2p::local_copy(static_cast<const char *>(sendbuf) + sdispls[i], scounts[i], stypes[i],
+                          static_cast<char *>(recvbuf) + rdispls[j], rcounts[j], rtypes[j], &r)) {
+        reqs.push_back(r);
+        doneOut[i] = doneIn[j] = 1;
+        any = true;
+      }
+    }
+    if (any) p2p::start_queued(); // the copies run while the messages are posted
+  }
   for (size_t i = 0; i < in.size(); ++i) {
-    if (in[i] == MPI_PROC_NULL) continue;
+    if (in[i] == MPI_PROC_NULL || doneIn[i]) continue;
     MPI_Request r;
     const int rc = MPI_Irecv(static_cast<char *>(recvbuf) + rdispls[i], rcounts[i], rtypes[i], in[i], tag, c, &r);
     if (rc != MPI_SUCCESS) return rc;
     reqs.push_back(r);
   }
   for (size_t i = 0; i < out.size(); ++i) {
-    if (out[i] == MPI_PROC_NULL) continue;
+    if (out[i] == MPI_PROC_NULL || doneOut[i]) continue;
     MPI_Request r;
     const int rc =
         MPI_Isend(static_cast<const char *>(sendbuf) + sdispls[i], scounts[i], stypes[i], out[i], tag, c, &r);

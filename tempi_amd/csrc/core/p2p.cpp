@@ -1200,6 +1200,27 @@ struct LibIrecvOp : Op {
   }
 };
 
+// a self edge of a collective: the copy alone (see p2p::local_copy)
+struct LocalCopyOp : Op {
+  RecordRef srec, rrec;
+  int64_t bytes;
+  LocalCopyOp(const TypeRecord *s, const TypeRecord *r, int dev, int64_t b, const tempi_hip_copy_item &c)
+      : srec(s->ref()), rrec(r->ref()), bytes(b) {
+    device = dev;
+    pendingUnpack.add_copy(this, c);
+    pendingUnpack.queue(this);
+  }
+  void gpu_done() override { done = true; }
+  void status(MPI_Status *s) const override {
+    if (s != MPI_STATUS_IGNORE) {
+      s->MPI_SOURCE = state.worldRank;
+      s->MPI_TAG = MPI_ANY_TAG;
+      s->MPI_ERROR = MPI_SUCCESS;
+      set_received(s, bytes);
+    }
+  }
+};
+
 // ------------------------------------------------------------- request table
 
 // TEMPI request handles live in [1, 2^26): the top bits of an MPICH handle
@@ -1410,6 +1431,32 @@ int irecv(void *buf, int count, MPI_Datatype dt, int source, int tag, MPI_Comm c
   if (pendingUnpack.size() >= (scattersInFlight ? earlyFlush : firstFlush)) flush_list(pendingUnpack, false);
   tock(counters.ns_irecv, t0);
   return MPI_SUCCESS;
+}
+
+bool local_copy(const void *sbuf, int scount, MPI_Datatype stype, void *rbuf, int rcount, MPI_Datatype rtype,
+                MPI_Request *req) {
+  if (!directEnabled) return false;
+  Route sr, rr;
+  if (!handles(sbuf, scount, stype, 0, &sr) || !handles(rbuf, rcount, rtype, 0, &rr)) return false;
+  if (!sr.rec->packer || !rr.rec->packer || !sr.rec->desc.valid || !rr.rec->desc.valid) return false;
+  if (sr.ptr.device != rr.ptr.device) return false;
+  const int64_t bytes = sr.rec->desc.size * int64_t(scount);
+  if (bytes != rr.rec->desc.size * int64_t(rcount) || bytes <= 0) return false;
+  tempi_hip_desc sflat, rflat;
+  if (!sr.rec->flat(scount, &sflat) || !rr.rec->flat(rcount, &rflat) || !copy_ok(rflat, sflat)) return false;
+  tempi_hip_copy_item c{};
+  c.src_first = sr.ptr.dptr;
+  c.dst_first = rr.ptr.dptr;
+  c.src = sflat;
+  c.dst = rflat;
+  counters.send_direct++;
+  *req = add(std::make_unique<LocalCopyOp>(sr.rec, rr.rec, rr.ptr.device, bytes, c));
+  return true;
+}
+
+void start_queued() {
+  if (!pendingPack.empty()) flush_list(pendingPack, true);
+  if (!pendingUnpack.empty()) flush_list(pendingUnpack, false);
 }
 
 bool send_gated(MPI_Comm comm, int dest) { return gate_busy(gate_key(comm, dest)); }

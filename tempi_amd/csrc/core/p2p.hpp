@@ -69,6 +69,16 @@ int irecv(void *buf, int count, MPI_Datatype dt, int source, int tag, MPI_Comm c
 // TEMPI send to (comm, dest) is still gathering, a library send there would
 // overtake it. send_gated() says so; isend_host() then queues the host send
 // behind it (a TEMPI request) and drain_sends() waits until it has left.
+// A message from this process to itself whose receive is known at the same
+// time (a neighbourhood collective's self edge): one strided -> strided copy
+// queued on the GPU, no library messages. False (nothing queued) when it
+// cannot be one copy: host memory, unequal sizes, shapes the copy kernel does
+// not take, different devices, TEMPI_NO_DIRECT. start_queued() launches what
+// is queued.
+bool local_copy(const void *sbuf, int scount, MPI_Datatype stype, void *rbuf, int rcount, MPI_Datatype rtype,
+                MPI_Request *req);
+void start_queued();
+
 bool send_gated(MPI_Comm comm, int dest);
 int isend_host(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Comm comm, MPI_Request *req);
 void drain_sends(MPI_Comm comm, int dest);
