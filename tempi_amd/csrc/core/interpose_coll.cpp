@@ -96,8 +96,20 @@ int isir(const void *sendbuf, const int *scounts, const int *sdispls, MPI_Dataty
     }
   const int tag = 0x3A2A;
   std::vector<MPI_Request> reqs;
+  // this rank's own block: one queued copy when both sides are device
+  // objects (no library messages), else a message like the others
+  bool selfDone = false;
+  if (scounts[rank] > 0 && rcounts[rank] > 0) {
+    MPI_Request r;
+    if (p2p::local_copy(static_cast<const char *>(sendbuf) + int64_t(sdispls[rank]) * sext, scounts[rank], stype,
+                        static_cast<char *>(recvbuf) + int64_t(rdispls[rank]) * rext, rcounts[rank], rtype, &r)) {
+      reqs.push_back(r);
+      selfDone = true;
+      p2p::start_queued();
+    }
+  }
   for (int p : order)
-    if (rcounts[p] > 0) {
+    if (rcounts[p] > 0 && !(selfDone && p == rank)) {
       MPI_Request r;
       char *b = static_cast<char *>(recvbuf) + int64_t(rdispls[p]) * rext;
       p2p::Route route;
@@ -108,7 +120,7 @@ int isir(const void *sendbuf, const int *scounts, const int *sdispls, MPI_Dataty
       reqs.push_back(r);
     }
   for (int p : order)
-    if (scounts[p] > 0) {
+    if (scounts[p] > 0 && !(selfDone && p == rank)) {
       MPI_Request r;
       const char *b = static_cast<const char *>(sendbuf) + int64_t(sdispls[p]) * sext;
       const int force = topology::colocated(comm, p) ? local : remote;
