@@ -322,10 +322,10 @@ bool export_object(const void *first, IpcCopyDesc *d) {
 //
 // Every operation is a small state machine with at most one GPU event and at
 // most one library request outstanding. progress() polls GPU events in
-// creation order and stops at the first one that is not complete (all TEMPI
-// work of a device runs on one in-order stream, so later events cannot be
-// complete either), then tests every outstanding library request with a
-// single MPI_Testsome. A pass therefore costs O(newly completed) HIP queries
+// creation order, skipping the rest of a stream (device x lane) once one of
+// its events is incomplete (each lane is an in-order stream, so its later
+// events cannot be complete either), then tests every outstanding library
+// request with a single MPI_Testsome. A pass therefore costs O(newly completed) HIP queries
 // plus one library call, instead of one query and one MPI_Test per operation
 // (the reference's try_progress wakes every operation: async_operation.cpp:
 // 501-513).
