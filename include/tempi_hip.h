@@ -101,6 +101,9 @@ int tempi_hip_word_width(const void *packed, const void *first,
 
 /* devices */
 int tempi_hip_device_count(int *n);
+/* a 16-byte identity of the physical GPU (the same in every process that
+   sees it, whatever its ordinal there) */
+int tempi_hip_device_uuid(int device, unsigned char uuid[16]);
 int tempi_hip_get_device(int *dev);
 int tempi_hip_set_device(int dev);
 int tempi_hip_device_synchronize(void);

@@ -53,6 +53,21 @@ void finalize() {
   }
 }
 
+uint32_t identity(int device) {
+  static std::vector<uint32_t> ids;
+  std::lock_guard<std::mutex> g(mtx);
+  if (device < 0 || device >= nDevices) return 0;
+  if (ids.size() < size_t(nDevices)) ids.assign(size_t(nDevices), 0);
+  if (!ids[size_t(device)]) {
+    unsigned char u[16] = {0};
+    tempi_hip_device_uuid(device, u);
+    uint32_t h = 2166136261u;
+    for (unsigned char c : u) h = (h ^ c) * 16777619u;
+    ids[size_t(device)] = h ? h : 1;
+  }
+  return ids[size_t(device)];
+}
+
 Ptr classify(const void *p) {
   Ptr r;
   if (!nDevices || !p) return r;

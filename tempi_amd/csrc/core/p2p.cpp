@@ -42,7 +42,7 @@ struct IpcDesc {
   int32_t senderWorld;
   int32_t senderPid;
   int32_t ackTag;
-  int32_t pad;
+  uint32_t gpu;    // gpu::identity of the slab's GPU
   uint64_t rawPtr; // valid inside the sender's own process
   unsigned char handle[TEMPI_HIP_IPC_HANDLE_BYTES];
 };
@@ -96,8 +96,10 @@ struct IpcCopyDesc {
   uint64_t rawFirst; // the first byte, in the sender's address space
   unsigned char handle[TEMPI_HIP_IPC_HANDLE_BYTES];
   tempi_hip_desc desc; // the object's shape, element count folded in
+  uint32_t gpu;        // gpu::identity of the object's GPU
+  uint32_t pad;
 };
-static_assert(sizeof(IpcCopyDesc) == 224, "descriptor size");
+static_assert(sizeof(IpcCopyDesc) == 232, "descriptor size");
 
 struct Op;
 struct DirectShared {
@@ -292,6 +294,7 @@ const char *peer_object(const IpcCopyDesc &d) {
       return nullptr;
     }
     it = ipcAllocOpen.emplace(key, p).first;
+    LOG_DEBUG("ipc copy map: rank " << d.senderWorld << " id " << d.bufferId << " -> " << p);
   }
   return static_cast<const char *>(it->second) + d.offset;
 }
@@ -311,6 +314,9 @@ bool export_object(const void *first, IpcCopyDesc *d) {
     x.id = id;
     if (tempi_hip_ipc_get_handle(x.handle, base) != 0) return false;
     it = ipcExports.insert_or_assign(b, x).first;
+    LOG_DEBUG("ipc copy export: base " << base << " size " << size << " id " << id);
+  } else {
+    LOG_DEBUG("ipc copy export reused: base " << base << " size " << size << " id " << id);
   }
   d->bufferId = id;
   d->offset = uint64_t(reinterpret_cast<uintptr_t>(first) - b);
@@ -641,6 +647,7 @@ struct IsendOp : Op {
       desc.senderPid = int32_t(getpid());
       desc.ackTag = int32_t(dslab->id % uint32_t(tagUb));
       desc.rawPtr = reinterpret_cast<uint64_t>(dslab->dev);
+      desc.gpu = gpu::identity(device);
       std::memcpy(desc.handle, slab_ipc_handle(dslab), sizeof desc.handle);
       // the slab is reused once the receiver acknowledges (private comm)
       const int peer = topology::world_rank(comm, dest);
@@ -762,12 +769,23 @@ struct IsendCopyOp : Op {
   IpcCopyDesc desc{};
   int ack = -1;
 
+  uint64_t key;
+
   IsendCopyOp(const TypeRecord *r, const char *o, int c, MPI_Datatype d, int de, int t, MPI_Comm cm, int dev,
               int64_t b, int peerWorld, const IpcCopyDesc &filled)
       : rec(r->ref()), origin(o), count(c), dest(de), tag(t), peer(peerWorld), dt(d), comm(cm), bytes(b),
-        desc(filled) {
+        desc(filled), key(gate_key(cm, de)) {
     device = dev;
-    post_or_queue(gate_key(comm, dest), this);
+    // The application's last writes to the object may still sit in this
+    // GPU's L2, invisible to a reader on another GPU. The descriptor leaves
+    // only after a batch event (a system-scope release: the L2 is written
+    // back) has completed -- an empty batch on lane 0, queued like a gather.
+    gate_enter(key, this);
+    pendingPack.queue(this);
+  }
+  void gpu_done() override {
+    ready = true;
+    gate_advance(key);
   }
   void post() override {
     next.MPI_Irecv(&ack, 1, MPI_INT, peer, desc.ackTag, ctrlComm, &lib);
@@ -1039,7 +1057,11 @@ struct IrecvOp : Op {
         c.src_first = src;
         c.dst = mine;
         c.src = xd.desc;
-        if (!local) c.flags = TEMPI_HIP_ITEM_REMOTE; // the sender's memory changes between messages
+        // another GPU's memory, reused by its owner between messages: read it
+        // with system-scope loads. (Memory of this same GPU is read through
+        // its own L2, which holds the sender's latest writes: measured, the
+        // system-scope loads could return stale bytes there.)
+        if (!local && ipcSystemLoads && xd.gpu != gpu::identity(device)) c.flags = TEMPI_HIP_ITEM_REMOTE;
         pendingUnpack.add_copy(this, c);
         pendingUnpack.queue(this);
         return;
@@ -1070,7 +1092,7 @@ struct IrecvOp : Op {
       elems = size ? d.bytes / size : 0;
       const size_t first = pendingUnpack.items.size();
       pendingUnpack.add_items(this, packer, const_cast<char *>(peer), origin, elems);
-      if (ipcSystemLoads) // the peer reuses this slab: never read a line cached from an earlier message
+      if (ipcSystemLoads && d.gpu != gpu::identity(device)) // another GPU's slab, reused between messages
         for (size_t i = first; i < pendingUnpack.items.size(); ++i) pendingUnpack.items[i].flags |= TEMPI_HIP_ITEM_REMOTE;
     } else {
       if (int64_t(n) > bytes) LOG_FATAL("message truncated: " << n << " B into " << bytes);
@@ -1393,6 +1415,7 @@ int isend(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Co
     d.device = p.device;
     d.rawFirst = reinterpret_cast<uint64_t>(origin + rec->desc.start);
     d.desc = flat;
+    d.gpu = gpu::identity(p.device);
     const int half = std::max(1, tagUb / 2);
     d.ackTag = half + int32_t(nextCopyTag++ % uint32_t(half)); // slab ids (the IPC acks) stay below
     if (export_object(origin + rec->desc.start, &d)) {

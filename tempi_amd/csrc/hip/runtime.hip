@@ -13,6 +13,7 @@
 
 #include "tempi_hip.h"
 
+#include <algorithm>
 #include <cstring>
 
 #define RET(expr) return int(expr)
@@ -28,6 +29,22 @@ int tempi_hip_device_count(int *n) {
   return int(e);
 }
 int tempi_hip_get_device(int *dev) { RET(hipGetDevice(dev)); }
+int tempi_hip_device_uuid(int device, unsigned char uuid[16]) {
+  hipUUID u;
+  std::memset(&u, 0, sizeof u);
+  hipError_t e = hipDeviceGetUuid(&u, device);
+  if (e != hipSuccess || std::all_of(u.bytes, u.bytes + 16, [](char c) { return c == 0; })) {
+    (void)hipGetLastError();
+    char bus[64] = {0}; // no UUID: the PCI bus id, zero padded
+    e = hipDeviceGetPCIBusId(bus, int(sizeof bus), device);
+    if (e != hipSuccess) RET(e);
+    std::memset(uuid, 0, 16);
+    for (int i = 0; bus[i] && i < 64; ++i) uuid[i % 16] ^= static_cast<unsigned char>(bus[i]);
+    return 0;
+  }
+  std::memcpy(uuid, u.bytes, 16);
+  return 0;
+}
 int tempi_hip_set_device(int dev) { RET(hipSetDevice(dev)); }
 int tempi_hip_device_synchronize(void) { RET(hipDeviceSynchronize()); }
 

@@ -10,6 +10,9 @@ every kind of receiver. Rank 0 sends, rank 1 receives, for each case:
             INTEGRATION.md)
   blocking  a blocking device MPI_Recv
   reuse     the same send buffer rewritten and sent again (no stale bytes)
+  realloc   the send buffer freed back to HIP and a new one allocated (maybe
+            at the same address) before each send: the receiver must map the
+            new allocation, not reuse the old mapping
 Every received byte is checked against the oracle; counters are printed."""
 import os
 import sys
@@ -40,6 +43,7 @@ CASES = [
     ("host", SEND, SEND, 1),
     ("blocking", SEND, SEND, 1),
     ("reuse", SEND, SEND, 3),
+    ("realloc", SEND, SEND, 3),
 ]
 
 
@@ -63,6 +67,11 @@ for ci, (name, _, rrecipe, reps) in enumerate(CASES):
         seed = 1000 * ci + rep
         src = np.random.default_rng(seed).integers(0, 256, slen, dtype=np.uint8)
         if rank == 0:
+            if name == "realloc":
+                del sbuf
+                torch.cuda.synchronize()
+                torch.cuda.empty_cache()  # the block goes back to hipFree
+                sbuf = torch.zeros(slen, dtype=torch.uint8, device="cuda")
             sbuf.copy_(torch.from_numpy(src))
             torch.cuda.synchronize()
             mpi.Wait(mpi.Isend(sbuf.data_ptr() + so, 1, st, 1, 50 + ci))

@@ -16,7 +16,7 @@ import pytest
 
 from oracle import pyoracle
 from tests import typezoo
-from tests.test_pack_gpu import HipDesc, _random_recipe
+from tests.test_pack_gpu import HipDesc, _random_recipe, release_l2
 
 pytestmark = pytest.mark.gpu
 
@@ -120,6 +120,8 @@ def test_copy_kernel_c_abi(mpi, gpu, seed, remote):
         pytest.skip("no supported pair drawn")
     items = (CopyItem * len(cases))(*[c[0] for c in cases])
     torch.cuda.synchronize()
+    if remote:
+        release_l2(H)
     assert H.tempi_hip_copy_batch(items, len(cases), None) == 0
     torch.cuda.synchronize()
     for it, src, dst, exp, sr, dr in cases:

@@ -291,6 +291,21 @@ class HipItem(ctypes.Structure):
 ITEM_REMOTE = 1  # TEMPI_HIP_ITEM_REMOTE
 
 
+def release_l2(H):
+    """a HIP event recorded and waited for: its system-scope release writes
+    the L2 back, as the transport's batch event does before an IPC reader on
+    another GPU is told (TEMPI_HIP_ITEM_REMOTE loads bypass this GPU's L2)"""
+    H.tempi_hip_event_create.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int]
+    H.tempi_hip_event_record.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    H.tempi_hip_event_synchronize.argtypes = [ctypes.c_void_p]
+    H.tempi_hip_event_destroy.argtypes = [ctypes.c_void_p]
+    ev = ctypes.c_void_p()
+    assert H.tempi_hip_event_create(ctypes.byref(ev), 0) == 0
+    assert H.tempi_hip_event_record(ev, None) == 0
+    assert H.tempi_hip_event_synchronize(ev) == 0
+    H.tempi_hip_event_destroy(ev)
+
+
 @pytest.mark.parametrize("remote", [False, True])
 @pytest.mark.parametrize("seed", range(6))
 def test_batched_kernel_c_abi(mpi, gpu, seed, remote):
@@ -348,6 +363,8 @@ def test_batched_kernel_c_abi(mpi, gpu, seed, remote):
     for c in cases:
         c["src"].zero_()
     torch.cuda.synchronize()
+    if remote:
+        release_l2(H)
     assert H.tempi_hip_unpack_batch(items, len(cases), None) == 0
     torch.cuda.synchronize()
     for c in cases:
