@@ -30,6 +30,8 @@
  *   MPI_Testall / _Testany / _Waitany / _Testsome / _Waitsome / MPI_Request_free
  *   / MPI_Request_get_status / MPI_Cancel
  *                    (not interposed: F8)            understand TEMPI requests
+ *   MPI_Sendrecv     (not interposed)                Irecv + Isend through TEMPI
+ *                                                    when either side is a device object
  *   MPI_Alltoallv    src/alltoallv.cpp:14-68         device-buffer alltoallv
  *   MPI_Neighbor_alltoallw  src/neighbor_alltoallw.cpp:11-18 (-> internal/
  *                    neighbor_alltoallw.cpp:19-77)   per-edge Isend/Irecv when
@@ -87,6 +89,8 @@ int MPI_Waitsome(int incount, MPI_Request array_of_requests[], int *outcount, in
 int MPI_Request_free(MPI_Request *request);
 int MPI_Request_get_status(MPI_Request request, int *flag, MPI_Status *status);
 int MPI_Cancel(MPI_Request *request);
+int MPI_Sendrecv(const void *sendbuf, int sendcount, MPI_Datatype sendtype, int dest, int sendtag, void *recvbuf,
+                 int recvcount, MPI_Datatype recvtype, int source, int recvtag, MPI_Comm comm, MPI_Status *status);
 int MPI_Alltoallv(const void *sendbuf, const int sendcounts[], const int sdispls[],
                   MPI_Datatype sendtype, void *recvbuf, const int recvcounts[], const int rdispls[],
                   MPI_Datatype recvtype, MPI_Comm comm);

@@ -274,3 +274,30 @@ TEMPI_EXPORT int MPI_Cancel(MPI_Request *request) {
   if (state.active && p2p::is_tempi_request(*request)) return p2p::cancel(*request);
   return next.MPI_Cancel(request);
 }
+
+// MPI_Sendrecv: not interposed by the reference, so a device-buffer exchange
+// would reach a library that cannot read GPU memory. When either side is a
+// TEMPI object it is an MPI_Irecv + MPI_Isend through the interposed entry
+// points and two waits (receive first, so a message to this same rank
+// matches at once).
+TEMPI_EXPORT int MPI_Sendrecv(const void *sendbuf, int sendcount, MPI_Datatype sendtype, int dest, int sendtag,
+                              void *recvbuf, int recvcount, MPI_Datatype recvtype, int source, int recvtag,
+                              MPI_Comm comm, MPI_Status *status) {
+  resolve_next();
+  p2p::Route sr, rr;
+  const bool mine = state.active && (p2p::handles(sendbuf, sendcount, sendtype, dest, &sr) ||
+                                     p2p::handles(recvbuf, recvcount, recvtype, source, &rr));
+  if (!mine) {
+    if (state.active && p2p::send_gated(comm, dest)) p2p::drain_sends(comm, dest); // keep send order
+    return next.MPI_Sendrecv(sendbuf, sendcount, sendtype, dest, sendtag, recvbuf, recvcount, recvtype, source,
+                             recvtag, comm, status);
+  }
+  MPI_Request r = MPI_REQUEST_NULL, s = MPI_REQUEST_NULL;
+  int rc = MPI_Irecv(recvbuf, recvcount, recvtype, source, recvtag, comm, &r);
+  if (rc != MPI_SUCCESS) return rc;
+  rc = MPI_Isend(sendbuf, sendcount, sendtype, dest, sendtag, comm, &s);
+  if (rc != MPI_SUCCESS) return rc;
+  rc = MPI_Wait(&r, status);
+  const int rc2 = MPI_Wait(&s, MPI_STATUS_IGNORE);
+  return rc != MPI_SUCCESS ? rc : rc2;
+}

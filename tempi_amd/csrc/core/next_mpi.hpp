@@ -34,6 +34,7 @@
   X(MPI_Request_free)                                                          \
   X(MPI_Request_get_status)                                                    \
   X(MPI_Cancel)                                                                \
+  X(MPI_Sendrecv)                                                              \
   X(MPI_Alltoallv)                                                             \
   X(MPI_Neighbor_alltoallv)                                                    \
   X(MPI_Neighbor_alltoallw)                                                    \

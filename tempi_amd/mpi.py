@@ -283,6 +283,13 @@ class MPI:
         self._call("MPI_Wait", ctypes.byref(r), st)
         return r.value, self._decode(st, t)
 
+    def Sendrecv(self, sbuf, scount, st, dest, stag, rbuf, rcount, rt, source, rtag, comm=None):
+        """MPI_Sendrecv; returns (source, tag, count of rt) of the receive"""
+        status = self._status()
+        self._call("MPI_Sendrecv", ctypes.c_void_p(sbuf), scount, self.h(st), dest, stag, ctypes.c_void_p(rbuf),
+                   rcount, self.h(rt), source, rtag, self.h(self.COMM_WORLD if comm is None else comm), status)
+        return self._decode(status, rt)
+
     def Cancel(self, req):
         r = self.Request(req)
         self._call("MPI_Cancel", ctypes.byref(r))

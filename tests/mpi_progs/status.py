@@ -92,6 +92,24 @@ for it, recipe in enumerate(RECIPES * 2):
         fail(f"{recipe}: received bytes differ ({'blocking' if blocking else 'Irecv'})")
     typezoo.free(mpi, probe_t, probe_temps, probe_basic)
 
+# MPI_Sendrecv around the ring (device objects go through TEMPI), with its
+# status: source, tag, and MPI_Get_count (fewer elements than allowed)
+recipe = RECIPES[0]
+tm = pyoracle.TypeMap(recipe)
+origin, buflen = tm.geometry(3)
+t, temps, basic = typezoo.build(mpi, recipe)
+s_host, s_dev = buf(buflen, 51 + rank)
+canvas, r_dev = buf(buflen, 52)
+got = mpi.Sendrecv(ptr(s_dev) + origin, 2, t, peer, 60 + rank, ptr(r_dev) + origin, 3, t, src_rank, mpi.ANY_TAG)
+if got != (src_rank, 60 + src_rank, 2):
+    fail(f"MPI_Sendrecv status {got}, expected {(src_rank, 60 + src_rank, 2)}")
+exp = canvas.copy()
+tm.unpack(tm.pack(np.random.default_rng(51 + src_rank).integers(0, 256, buflen, dtype=np.uint8), origin, 2), exp,
+          origin, 2)
+if not np.array_equal(host(r_dev), exp):
+    fail("MPI_Sendrecv bytes differ")
+typezoo.free(mpi, t, temps, basic)
+
 # MPI_Request_get_status leaves the request; MPI_Cancel of a receive nothing
 # will match (tag 999) completes it as cancelled
 recipe = RECIPES[0]
