@@ -77,9 +77,10 @@ static_assert(sizeof(DirectDesc) == 160 && sizeof(DirectDesc) != sizeof(IpcDesc)
 // memory (tempi_hip_copy_batch, source read with system-scope loads). No
 // gather on the sender, no packed slab: the payload crosses xGMI once and
 // each HBM sees it once. The send completes when the receiver acknowledges
-// its copy (rendezvous), so only messages at least TEMPI_IPC_COPY_MIN_BYTES
-// take this route: as large as MPICH's own rendezvous messages, which no
-// correct program expects to be buffered. Narrow rows (< TEMPI_IPC_COPY_MIN_BLOCK)
+// its copy (rendezvous), so only messages of at least TEMPI_IPC_COPY_MIN_BYTES
+// take this route: larger than MPICH's eager limit, i.e. messages the library
+// itself would not buffer either (a program waiting on such a send before
+// posting the matching receive deadlocks with MPICH alone too). Narrow rows (< TEMPI_IPC_COPY_MIN_BLOCK)
 // are gathered on the sender instead: a 24-byte row read across xGMI costs a
 // whole remote line.
 constexpr uint64_t kMagicCopy = 0x54454d5049585043ull; // "TEMPIXPC"
@@ -141,7 +142,9 @@ struct Export {
 };
 std::unordered_map<uintptr_t, Export> ipcExports;
 bool ipcCopyEnabled = true;             // TEMPI_NO_IPC_COPY
-int64_t ipcCopyMinBytes = 64 * 1024;    // TEMPI_IPC_COPY_MIN_BYTES
+// above MPICH's own eager limit (MPIR_CVAR_CH3_EAGER_MAX_MSG_SIZE, 128 KiB):
+// a program that works with the library's rendezvous works with this one
+int64_t ipcCopyMinBytes = 128 * 1024 + 1; // TEMPI_IPC_COPY_MIN_BYTES
 int64_t ipcCopyMinBlock = 256;          // TEMPI_IPC_COPY_MIN_BLOCK
 uint32_t nextCopyTag = 0;
 
