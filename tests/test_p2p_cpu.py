@@ -48,6 +48,35 @@ def test_completion_family_host():
     assert rc == 0 and "RESULT errors=0" in out, out[-3000:]
 
 
+def _torchrun(script, n):
+    import os
+    import socket
+    import subprocess
+    import sys
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.join(mpi_launch.ROOT, "tests", "mpi_progs", script)]
+    env = dict(os.environ)
+    for k in list(env):
+        if k.startswith("PMI_"):
+            env.pop(k)
+    return subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=240, env=env,
+                          start_new_session=True)
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_bench_plumbing_under_torchrun(n):
+    """bench.py's dist_setup / barrier / max-over-ranks timing reductions on
+    gloo, and an MPI exchange between the torch-launched ranks it wires up"""
+    r = _torchrun("torchrun_bench.py", n)
+    assert r.returncode == 0 and r.stdout.count("RESULT ok") == n, r.stdout[-3000:]
+
+
 def test_mpi_under_torchrun():
     """bench.py's multi-GPU launch is torch.distributed.run, not mpiexec: the
     ranks are wired into one MPI job by tempi_amd.pmi (PMI-1 server)."""
