@@ -152,3 +152,14 @@ def test_send_order_across_routes(gpu, n, method):
         env["TEMPI_STREAMS"] = "3"
     rc, out = mpi_launch.run(n, mpi_launch.py("order.py", "--device"), env=env, timeout=240)
     assert rc == 0 and "RESULT errors=0" in out, out[-3000:]
+
+
+@pytest.mark.parametrize("n,seed,env", [(1, 7, {}), (2, 7, {}), (3, 11, {}), (4, 5, {}),
+                                        (3, 13, {"TEMPI_STREAMS": "3"}), (2, 17, {"TEMPI_NO_IPC_COPY": "1"}),
+                                        (2, 19, {"TEMPI_NO_DIRECT": "1"})])
+def test_transport_fuzz(gpu, n, seed, env):
+    """random mixes of every route (direct, IPC slab, IPC COPY, ONESHOT,
+    library-packed, host) between all pairs incl. self, tags reused so MPI
+    order matters, random posting interleavings; every byte checked"""
+    rc, out = mpi_launch.run(n, mpi_launch.py("fuzz.py", "5", str(seed)), env=env, timeout=200)
+    assert rc == 0 and "RESULT errors=0" in out, out[-3000:]
