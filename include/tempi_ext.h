@@ -42,6 +42,7 @@ typedef struct tempi_counters_t {
   uint64_t neighbor_colls; /* MPI_Neighbor_alltoall{v,w} taken by TEMPI */
   uint64_t send_ipc_copy;  /* IPC sends the receiver copied out of the sender's object */
   uint64_t copy_resends;   /* IPC COPY sends answered through the host instead */
+  uint64_t ipc_maps_replaced; /* peer mappings closed because the peer freed and replaced that allocation */
 } tempi_counters_t;
 void tempi_get_counters(tempi_counters_t *out);
 void tempi_reset_counters(void);

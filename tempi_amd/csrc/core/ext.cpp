@@ -64,6 +64,7 @@ TEMPI_EXPORT void tempi_get_counters(tempi_counters_t *o) {
   o->neighbor_colls = c.neighbor_colls;
   o->send_ipc_copy = c.send_ipc_copy;
   o->copy_resends = c.copy_resends;
+  o->ipc_maps_replaced = c.ipc_maps_replaced;
 }
 
 TEMPI_EXPORT void tempi_reset_counters(void) { counters = Counters(); }

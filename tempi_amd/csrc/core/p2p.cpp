@@ -133,8 +133,13 @@ std::vector<std::unique_ptr<PendingAck>> pendingAcks; // stable addresses: Irecv
 
 // peer slabs mapped into this process: (world rank, slab id) -> base
 std::map<std::pair<int, uint64_t>, void *> ipcOpen;
-// peer allocations mapped for IPC COPY: (world rank, buffer id) -> base
-std::map<std::pair<int, uint64_t>, void *> ipcAllocOpen;
+// peer allocations mapped for IPC COPY: (world rank, buffer id) -> mapping
+struct AllocMap {
+  void *base;                // the mapping in this process
+  uint64_t senderBase;       // the allocation's base in the sender's address space
+  unsigned char handle[TEMPI_HIP_IPC_HANDLE_BYTES];
+};
+std::map<std::pair<int, uint64_t>, AllocMap> ipcAllocOpen;
 // this process's allocations exported for IPC COPY: base -> (buffer id, handle)
 struct Export {
   uint64_t id;
@@ -281,6 +286,33 @@ void send_ack(const IpcDesc &d, int code = 0) { send_ack(d.senderWorld, d.ackTag
 // sender's memory could not be mapped (no more IPC with that rank)
 enum { kCopyDone = 0, kCopyResend = 1, kCopyUnmapped = 2 };
 
+// A new allocation of a sender at the base of one we hold mapped, or with the
+// same handle bytes, means that sender freed the old one (its sends from it
+// have completed, so no copy of ours still reads it). Close those mappings
+// first: the runtime may hand back its cached import for identical handle
+// bytes -- the freed allocation's pages, not the new one's.
+void forget_freed_allocs(const IpcCopyDesc &d) {
+  const uint64_t senderBase = d.rawFirst - d.offset;
+  bool synced = false;
+  for (auto it = ipcAllocOpen.begin(); it != ipcAllocOpen.end();) {
+    const AllocMap &m = it->second;
+    if (it->first.first == int(d.senderWorld) &&
+        (m.senderBase == senderBase || std::memcmp(m.handle, d.handle, sizeof m.handle) == 0)) {
+      if (!synced) {
+        gpu::check(tempi_hip_device_synchronize(), "ipc mapping replace");
+        synced = true;
+      }
+      LOG_DEBUG("ipc copy unmap: rank " << d.senderWorld << " id " << it->first.second << " (replaced by id "
+                                        << d.bufferId << ")");
+      tempi_hip_ipc_close_handle(m.base);
+      counters.ipc_maps_replaced++;
+      it = ipcAllocOpen.erase(it);
+    } else {
+      ++it;
+    }
+  }
+}
+
 // the sender's allocation mapped into this process (its first byte), or
 // nullptr when it cannot be
 const char *peer_object(const IpcCopyDesc &d) {
@@ -288,6 +320,7 @@ const char *peer_object(const IpcCopyDesc &d) {
   auto key = std::make_pair(int(d.senderWorld), d.bufferId);
   auto it = ipcAllocOpen.find(key);
   if (it == ipcAllocOpen.end()) {
+    forget_freed_allocs(d);
     void *p = nullptr;
     static const bool injectFault = std::getenv("TEMPI_FAULT_IPC_OPEN") != nullptr;
     const int e = injectFault ? 1 : tempi_hip_ipc_open_handle(&p, d.handle);
@@ -296,10 +329,14 @@ const char *peer_object(const IpcCopyDesc &d) {
       mark_ipc_broken(d.senderWorld);
       return nullptr;
     }
-    it = ipcAllocOpen.emplace(key, p).first;
+    AllocMap m;
+    m.base = p;
+    m.senderBase = d.rawFirst - d.offset;
+    std::memcpy(m.handle, d.handle, sizeof m.handle);
+    it = ipcAllocOpen.emplace(key, m).first;
     LOG_DEBUG("ipc copy map: rank " << d.senderWorld << " id " << d.bufferId << " -> " << p);
   }
-  return static_cast<const char *>(it->second) + d.offset;
+  return static_cast<const char *>(it->second.base) + d.offset;
 }
 
 // this process's allocation holding `first` exported for IPC COPY: fills the
@@ -588,7 +625,7 @@ void recycle_alloc_maps() {
   if (ipcAllocOpen.size() < kMaxAllocMaps) return;
   flush_list(pendingUnpack, false);
   gpu::check(tempi_hip_device_synchronize(), "ipc mapping recycle");
-  for (auto &kv : ipcAllocOpen) tempi_hip_ipc_close_handle(kv.second);
+  for (auto &kv : ipcAllocOpen) tempi_hip_ipc_close_handle(kv.second.base);
   ipcAllocOpen.clear();
 }
 
@@ -1342,7 +1379,7 @@ void finalize() {
   eventPool.clear();
   for (auto &kv : ipcOpen) tempi_hip_ipc_close_handle(kv.second);
   ipcOpen.clear();
-  for (auto &kv : ipcAllocOpen) tempi_hip_ipc_close_handle(kv.second);
+  for (auto &kv : ipcAllocOpen) tempi_hip_ipc_close_handle(kv.second.base);
   ipcAllocOpen.clear();
   ipcExports.clear();
   if (ctrlComm != MPI_COMM_NULL) MPI_Comm_free(&ctrlComm);

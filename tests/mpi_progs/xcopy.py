@@ -43,7 +43,7 @@ CASES = [
     ("host", SEND, SEND, 1),
     ("blocking", SEND, SEND, 1),
     ("reuse", SEND, SEND, 3),
-    ("realloc", SEND, SEND, 3),
+    ("realloc", SEND, SEND, 8),
 ]
 
 
@@ -63,6 +63,7 @@ for ci, (name, _, rrecipe, reps) in enumerate(CASES):
         raise SystemExit(f"case {name}: sizes differ ({rtm.size} vs {stm.size})")
     ro, rlen = rtm.geometry(1)
     rt, rtemps, rbasic = typezoo.build(mpi, rrecipe)
+    prev = None
     for rep in range(reps):
         seed = 1000 * ci + rep
         src = np.random.default_rng(seed).integers(0, 256, slen, dtype=np.uint8)
@@ -92,11 +93,14 @@ for ci, (name, _, rrecipe, reps) in enumerate(CASES):
                 torch.cuda.synchronize()
                 got = dbuf.cpu().numpy()
             if not np.array_equal(got, exp):
-                fail(f"case {name} rep {rep}: received bytes differ")
+                stale = prev is not None and np.array_equal(rtm.pack(got, ro, 1), prev)
+                fail(f"case {name} rep {rep}: received bytes differ" + (" (the previous message's)" if stale else ""))
+            prev = stm.pack(src, so, 1)
     typezoo.free(mpi, rt, rtemps, rbasic)
 typezoo.free(mpi, st, stemps, sbasic)
 c = mpi.counters()
-print(f"rank {rank} counters ipc_copy={c['send_ipc_copy']} resends={c['copy_resends']} ipc={c['send_ipc']}",
+print(f"rank {rank} counters ipc_copy={c['send_ipc_copy']} resends={c['copy_resends']} ipc={c['send_ipc']} "
+      f"replaced={c['ipc_maps_replaced']}",
       flush=True)
 mpi.Finalize()
 print(f"RESULT errors={errors}", flush=True)

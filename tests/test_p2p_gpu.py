@@ -124,7 +124,7 @@ def test_ipc_copy_receivers(gpu, env):
     rc, out = mpi_launch.run(2, mpi_launch.py("xcopy.py"), env=env, timeout=120)
     assert rc == 0 and "RESULT errors=0" in out, out[-3000:]
     if "TEMPI_FAULT_IPC_OPEN" not in env:
-        assert "rank 0 counters ipc_copy=11 resends=2" in out, out[-3000:]
+        assert "rank 0 counters ipc_copy=16 resends=2" in out, out[-3000:]
 
 
 @pytest.mark.parametrize("n,method", [(2, "AUTO"), (2, "ONESHOT"), (2, "IPC"), (2, "STAGED"), (1, "AUTO"),
