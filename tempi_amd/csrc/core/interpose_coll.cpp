@@ -96,6 +96,7 @@ int isir(const void *sendbuf, const int *scounts, const int *sdispls, MPI_Dataty
     }
   const int tag = 0x3A2A;
   std::vector<MPI_Request> reqs;
+  p2p::CollectiveScope scope; // every receive is posted before any wait
   // this rank's own block: one queued copy when both sides are device
   // objects (no library messages), else a message like the others
   bool selfDone = false;

@@ -144,6 +144,7 @@ int isir(const void *sendbuf, const int *scounts, const MPI_Aint *sdispls, const
     if (rc != MPI_SUCCESS) return rc;
     reqs.push_back(r);
   }
+  p2p::CollectiveScope scope; // every receive above is posted: rendezvous sends cannot deadlock
   for (size_t i = 0; i < out.size(); ++i) {
     if (out[i] == MPI_PROC_NULL || doneOut[i]) continue;
     MPI_Request r;

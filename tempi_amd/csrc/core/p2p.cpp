@@ -147,6 +147,10 @@ struct Export {
 };
 std::unordered_map<uintptr_t, Export> ipcExports;
 bool ipcCopyEnabled = true;             // TEMPI_NO_IPC_COPY
+// Inside a collective every receive is posted before any send is waited on,
+// so a rendezvous send cannot deadlock there: IPC COPY takes messages of any
+// size (TEMPI_NO_COLL_COPY keeps the point-to-point threshold)
+bool collCopyEnabled = true;
 // above MPICH's own eager limit (MPIR_CVAR_CH3_EAGER_MAX_MSG_SIZE, 128 KiB):
 // a program that works with the library's rendezvous works with this one
 int64_t ipcCopyMinBytes = 128 * 1024 + 1; // TEMPI_IPC_COPY_MIN_BYTES
@@ -1317,12 +1321,15 @@ std::vector<MPI_Status> pollSt;
 
 } // namespace
 
+int collectiveDepth = 0;
+
 void init() {
   gpu::choose_lanes(topology::ranks_on_node());
   gpuAwareLibrary = std::getenv("TEMPI_MPI_GPU_AWARE") != nullptr;
   directEnabled = std::getenv("TEMPI_NO_DIRECT") == nullptr;
   ipcSystemLoads = std::getenv("TEMPI_IPC_PLAIN_LOADS") == nullptr;
   ipcCopyEnabled = std::getenv("TEMPI_NO_IPC_COPY") == nullptr;
+  collCopyEnabled = std::getenv("TEMPI_NO_COLL_COPY") == nullptr;
   if (const char *s = std::getenv("TEMPI_IPC_COPY_MIN_BYTES")) ipcCopyMinBytes = std::atoll(s);
   if (const char *s = std::getenv("TEMPI_IPC_COPY_MIN_BLOCK")) ipcCopyMinBlock = std::atoll(s);
   if (const char *s = std::getenv("TEMPI_EARLY_FLUSH")) earlyFlush = size_t(std::max(1, std::atoi(s)));
@@ -1444,7 +1451,8 @@ int isend(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Co
   }
   // IPC COPY: a large message of wide rows is copied by the receiver straight
   // out of this process's object (no gather, no slab)
-  if (m == Method::IPC && ipcCopyEnabled && bytes >= ipcCopyMinBytes && rec->flat(count, &flat) &&
+  const int64_t copyMin = (collectiveDepth > 0 && collCopyEnabled) ? 1 : ipcCopyMinBytes;
+  if (m == Method::IPC && ipcCopyEnabled && bytes >= copyMin && rec->flat(count, &flat) &&
       flat.ndims <= 3 && flat.block >= ipcCopyMinBlock && bytes < (int64_t(1) << 31)) {
     IpcCopyDesc d{};
     d.magic[0] = kMagicCopy;

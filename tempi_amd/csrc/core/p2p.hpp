@@ -56,6 +56,17 @@ struct Route {
 // true when TEMPI handles this send / receive (otherwise: library)
 bool handles(const void *buf, int count, MPI_Datatype dt, int peer, Route *route);
 
+// Collectives (MPI_Alltoallv, neighbourhood) post every receive before they
+// wait on any send; while one is in this scope IPC COPY (a rendezvous: the
+// send completes when the receiver has copied) is used at every message size
+extern int collectiveDepth;
+struct CollectiveScope {
+  CollectiveScope() { ++collectiveDepth; }
+  ~CollectiveScope() { --collectiveDepth; }
+  CollectiveScope(const CollectiveScope &) = delete;
+  CollectiveScope &operator=(const CollectiveScope &) = delete;
+};
+
 // force: -1 = choose by TEMPI_DATATYPE_* / AUTO; else a forced method
 // (0 ONESHOT, 1 STAGED, 2 DEVICE, 3 IPC)
 // blocking = true (MPI_Send) never takes the DIRECT route, whose completion
