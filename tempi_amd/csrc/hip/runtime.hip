@@ -134,8 +134,14 @@ int tempi_hip_event_elapsed_ms(float *ms, void *start, void *stop) {
 int tempi_hip_malloc(void **p, size_t n) { RET(hipMalloc(p, n ? n : 1)); }
 int tempi_hip_free(void *p) { RET(hipFree(p)); }
 
+// Pinned slabs are written by kernels and read by the host MPI, or written by
+// the host and read by kernels, and then reused for the next message. They are
+// allocated coherent (fine-grained): without hipHostMallocCoherent, HIP's
+// default (HIP_HOST_COHERENT=0) is coarse-grained host memory, whose lines a
+// kernel may find in L2 from the slab's previous message.
 int tempi_hip_host_alloc(void **host, void **dev, size_t n) {
-  hipError_t e = hipHostMalloc(host, n ? n : 1, hipHostMallocMapped | hipHostMallocPortable);
+  hipError_t e =
+      hipHostMalloc(host, n ? n : 1, hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent);
   if (e != hipSuccess) RET(e);
   RET(hipHostGetDevicePointer(dev, *host, 0));
 }

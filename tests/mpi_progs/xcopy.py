@@ -94,7 +94,14 @@ for ci, (name, _, rrecipe, reps) in enumerate(CASES):
                 got = dbuf.cpu().numpy()
             if not np.array_equal(got, exp):
                 stale = prev is not None and np.array_equal(rtm.pack(got, ro, 1), prev)
-                fail(f"case {name} rep {rep}: received bytes differ" + (" (the previous message's)" if stale else ""))
+                diff = np.flatnonzero(got != exp)
+                gp, ep = rtm.pack(got, ro, 1), rtm.pack(exp, ro, 1)
+                pd = np.flatnonzero(gp != ep)
+                zeros = int(np.count_nonzero(gp[pd] == 0))
+                unwritten = int(np.count_nonzero(gp[pd] == rtm.pack(canvas, ro, 1)[pd]))
+                fail(f"case {name} rep {rep}: received bytes differ" + (" (the previous message's)" if stale else "")
+                     + f" [{diff.size} bytes, {pd.size} of the payload at packed offsets {pd[:1].tolist()}..{pd[-1:].tolist()}"
+                     f": {zeros} zero, {unwritten} still the canvas; outside the payload {diff.size - pd.size}]")
             prev = stm.pack(src, so, 1)
     typezoo.free(mpi, rt, rtemps, rbasic)
 typezoo.free(mpi, st, stemps, sbasic)
