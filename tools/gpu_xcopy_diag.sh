@@ -7,7 +7,7 @@ cd "$(dirname "$0")/.."
 O=gpurun_out
 mkdir -p $O
 rm -f $O/xdiag.log
-for rep in 1 2 3 4; do
+for rep in $(seq 1 ${REPS:-4}); do
   for v in "TEMPI_FAULT_IPC_OPEN=1" "TEMPI_X=1"; do
     echo "== rep $rep $v" >> $O/xdiag.log
     env TEMPI_DATATYPE_IPC=1 TEMPI_IPC_COPY_MIN_BLOCK=1 TEMPI_IPC_COPY_MIN_BYTES=1 $v HYDRA_LAUNCHER=fork \
