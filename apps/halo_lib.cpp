@@ -295,17 +295,28 @@ tempi_bench_halo(int nIters, int gx, int gy, int gz, int nQuants, int radius, in
   MPI_Allreduce(MPI_IN_PLACE, &maxLinkAll, 1, MPI_DOUBLE, MPI_MAX, MPI_COMM_WORLD);
   double totalBytes = bytesPerIter;
   MPI_Allreduce(MPI_IN_PLACE, &totalBytes, 1, MPI_DOUBLE, MPI_SUM, MPI_COMM_WORLD);
+  // the SURVEY 8(d) aggregate-xGMI form: bytes that leave a rank, over the
+  // directed (sender, receiver) GPU pairs that carry any
+  double remote[2] = {0, 0}; // bytes to other ranks, directed links used
+  for (double b : peerBytes)
+    if (b > 0) {
+      remote[0] += b;
+      remote[1] += 1;
+    }
+  MPI_Allreduce(MPI_IN_PLACE, remote, 2, MPI_DOUBLE, MPI_SUM, MPI_COMM_WORLD);
   const double tIter = trimean(times);
   if (rank == 0 && json && jsonCap > 0) {
     std::snprintf(json, size_t(jsonCap), "{\"ranks\": %d, \"global\": [%d, %d, %d], \"dims\": [%d, %d, %d], \"lcr\": [%d, %d, %d], "
                 "\"quants\": %d, \"radius\": %d, \"iters\": %d, \"us_per_iter\": %.2f, \"us_min\": %.2f, "
                 "\"payload_bytes_per_iter_per_rank0\": %.0f, \"total_bytes_per_iter\": %.0f, "
                 "\"max_peer_bytes_per_iter\": %.0f, \"aggregate_GBps\": %.2f, \"busiest_link_GBps\": %.2f, "
+                "\"remote_bytes_per_iter\": %.0f, \"links_used\": %.0f, "
                 "\"checked\": %s, \"errors\": %lld, \"api\": \"%s\", \"rank0_us_per_iter\": {\"isend\": %.1f, "
                 "\"irecv\": %.1f, \"wait\": %.1f}}\n",
                 size, global.x, global.y, global.z, dims.x, dims.y, dims.z, lcr.x, lcr.y, lcr.z, nQuants, radius,
                 nIters, tIter * 1e6, *std::min_element(times.begin(), times.end()) * 1e6, bytesPerIter, totalBytes,
-                maxLinkAll, totalBytes / tIter / 1e9, maxLinkAll / tIter / 1e9, check ? "true" : "false", errors,
+                maxLinkAll, totalBytes / tIter / 1e9, maxLinkAll / tIter / 1e9, remote[0], remote[1],
+                check ? "true" : "false", errors,
                 neighbor ? "MPI_Neighbor_alltoallw" : "MPI_Isend/MPI_Irecv/MPI_Wait",
                 tIsend / nIters * 1e6, tIrecv / nIters * 1e6, tWait / nIters * 1e6);
   }

@@ -398,6 +398,13 @@ def halo(args, mpi, world, grid=None):
         out["roofline"] = {"bound": "xgmi", "busiest_link_GBps": round(r["busiest_link_GBps"], 2),
                            "link_peak_GBps": XGMI_LINK_GBS, "frac": round(r["busiest_link_GBps"] / XGMI_LINK_GBS, 4),
                            "lower_bound_us": round(lb * 1e6, 1)}
+        links = r.get("links_used") or 0
+        if links:
+            # sum of peer bytes / t / (directed links used x link peak)
+            agg = r["remote_bytes_per_iter"] / t / 1e9
+            out["roofline"].update({"remote_bytes_per_iter": int(r["remote_bytes_per_iter"]),
+                                    "links_used": int(links), "aggregate_xgmi_GBps": round(agg, 1),
+                                    "aggregate_frac": round(agg / (links * XGMI_LINK_GBS), 4)})
     return out
 
 
