@@ -147,7 +147,7 @@ struct Export {
 };
 std::unordered_map<uintptr_t, Export> ipcExports;
 bool ipcCopyEnabled = true;             // TEMPI_NO_IPC_COPY
-// Inside a collective every receive is posted before any send is waited on,
+// Inside MPI_Alltoallv every receive is posted before any send is waited on,
 // so a rendezvous send cannot deadlock there: IPC COPY takes messages of any
 // size (TEMPI_NO_COLL_COPY keeps the point-to-point threshold)
 bool collCopyEnabled = true;

@@ -56,8 +56,8 @@ struct Route {
 // true when TEMPI handles this send / receive (otherwise: library)
 bool handles(const void *buf, int count, MPI_Datatype dt, int peer, Route *route);
 
-// Collectives (MPI_Alltoallv, neighbourhood) post every receive before they
-// wait on any send; while one is in this scope IPC COPY (a rendezvous: the
+// A collective that posts every receive before it waits on any send
+// (MPI_Alltoallv) opens this scope; inside it IPC COPY (a rendezvous: the
 // send completes when the receiver has copied) is used at every message size
 extern int collectiveDepth;
 struct CollectiveScope {
