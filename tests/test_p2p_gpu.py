@@ -97,7 +97,8 @@ def test_neighbor_collectives_device(gpu, ranks, env):
     assert rc == 0 and "RESULT errors=0" in out, out[-3000:]
 
 
-@pytest.mark.parametrize("ranks,scale,density", [(2, 100000, 1.0), (3, 1000, 0.5), (4, 10, 1.0), (4, 100000, 0.25)])
+@pytest.mark.parametrize("ranks,scale,density", [(2, 100000, 1.0), (3, 1000, 0.5), (4, 10, 1.0), (4, 100000, 0.25),
+                                                    (2, 1000000, 1.0), (3, 10000, 1.0)])
 def test_alltoallv_sparse_app(gpu, ranks, scale, density):
     """config 5 app: the reference's random sparse matrices, every byte checked"""
     rc, out = mpi_launch.run(ranks, [os.path.join(LIB, "alltoallv_sparse"), "3", "--scale", str(scale), "--density",
