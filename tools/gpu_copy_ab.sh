@@ -2,6 +2,9 @@
 # Copy-kernel A/B on one box: mixed-width launches (TEMPI_COPY_MIXED) against
 # per-width launches over the halo regions (hbench), interleaved 3x; then the
 # direct-copy GPU tests and the 1-rank halo with the shipped library.
+# Variants (built on the CPU first): cur = tools/build_variants.sh; nomix = the same
+# hipcc line with -DTEMPI_COPY_MIXED=0 on the mixed-launch build this A/B measured
+# (reverted).
 set -o pipefail
 cd "$(dirname "$0")/.."
 O=gpurun_out

@@ -1,6 +1,9 @@
 #!/bin/bash
 # Unpack A/B on one box: TEMPI_UNPACK_TOUCH (load the destination line of
 # sub-sector rows before the scatter writes it) against the shipped kernel.
+# Variants (built on the CPU first): cur = tools/build_variants.sh; touch = the same
+# hipcc line with -DTEMPI_UNPACK_TOUCH=1 on the build this A/B measured
+# (reverted).
 set -o pipefail
 cd "$(dirname "$0")/.."
 O=gpurun_out
