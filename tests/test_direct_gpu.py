@@ -310,3 +310,68 @@ def test_self_any_source_any_tag_and_type_freed_in_flight(mpi, gpu):
     assert mpi.Waitall([r, s]) == [mpi.REQUEST_NULL] * 2
     torch.cuda.synchronize()
     assert np.array_equal(dst.cpu().numpy(), exp)
+
+
+def _halo_desc(block, counts, strides):
+    d = HipDesc()
+    d.block = block
+    d.ndims = len(counts)
+    for j, (cn, st) in enumerate(zip(counts, strides)):
+        d.counts[j] = cn
+        d.strides[j] = st
+    return d
+
+
+@pytest.mark.parametrize("remote", [False, True])
+@pytest.mark.parametrize("l,nq", [(16, 1), (37, 3), (64, 5)])
+def test_copy_paired_halo_faces(mpi, gpu, l, nq, remote):
+    """The paired copy route (pack_kernels.hip CArgs::s2, pair_jobs): the +-x
+    faces of each quantity of a radius-3 periodic halo, where the sector one
+    item writes ([0,24) of a row) is the sector its partner reads ([24,48)),
+    plus the y faces (16-byte words, another launch) and one extra x face on
+    its own buffer that is left unpaired. Bit-exact against numpy's slicing of
+    the same halo (the 1-rank case of bench-halo-exchange,
+    /root/reference/bin/bench_halo_exchange.cpp:679-704 decomposition)."""
+    import torch
+
+    H = _hip()
+    r, q = 3, 8
+    width = (l + 2 * r) * q
+    pitch = (width + 511) // 512 * 512
+    ysz = zsz = l + 2 * r
+    plane = pitch * ysz
+    rng = np.random.default_rng(l * 31 + nq)
+    hosts = [rng.integers(0, 256, plane * zsz, dtype=np.uint8) for _ in range(nq + 1)]
+    devs = [torch.from_numpy(h).to(gpu) for h in hosts]
+    exps = [h.reshape(zsz, ysz, pitch).copy() for h in hosts]
+    items = []
+
+    def add(k, s3, d3, e3):
+        # s3 / d3: (z, y, x-cell) origins; e3: extents in cells
+        src = devs[k].data_ptr() + s3[0] * plane + s3[1] * pitch + s3[2] * q
+        dst = devs[k].data_ptr() + d3[0] * plane + d3[1] * pitch + d3[2] * q
+        desc = _halo_desc(e3[2] * q, [e3[0], e3[1]], [plane, pitch])
+        it = CopyItem()
+        it.src_first, it.dst_first, it.src, it.dst = src, dst, desc, desc
+        it.flags = ITEM_REMOTE if remote else 0
+        items.append(it)
+        h = hosts[k].reshape(zsz, ysz, pitch)
+        xs, xd, n = s3[2] * q, d3[2] * q, e3[2] * q
+        exps[k][d3[0]:d3[0] + e3[0], d3[1]:d3[1] + e3[1], xd:xd + n] = \
+            h[s3[0]:s3[0] + e3[0], s3[1]:s3[1] + e3[1], xs:xs + n]
+
+    for k in range(nq):
+        add(k, (r, r, r), (r, r, l + r), (l, l, r))  # -x face -> +x halo
+        add(k, (r, r, l), (r, r, 0), (l, l, r))      # +x face -> -x halo (its partner)
+        add(k, (r, r, r), (r, l + r, r), (l, r, l))  # -y face -> +y halo
+        add(k, (r, l, r), (r, 0, r), (l, r, l))      # +y face -> -y halo
+    add(nq, (r, r, r), (r, r, l + r), (l, l, r))     # unpaired
+    torch.cuda.synchronize()
+    if remote:
+        release_l2(H)
+    arr = (CopyItem * len(items))(*items)
+    assert H.tempi_hip_copy_batch(arr, len(items), None) == 0
+    torch.cuda.synchronize()
+    for k in range(nq + 1):
+        got = devs[k].cpu().numpy().reshape(zsz, ysz, pitch)
+        assert np.array_equal(got, exps[k]), f"quantity {k}"
