@@ -24,8 +24,8 @@
 //    Montgomery) for words-per-row and every dimension count; offsets are
 //    64-bit (extents of several GiB are fine; the reference's are 32-bit, F6).
 //    One decode per chunk, then an odometer step per row change.
-//  * Grid: 256-thread workgroups (4 waves), one 16-byte chunk per lane for
-//    16-byte words (a 1 GiB pack is 262144 workgroups: the dispatcher keeps
+//  * Grid: 128-thread workgroups (2 waves), one 16-byte chunk per lane for
+//    16-byte words (a 1 GiB pack is 524288 workgroups: the dispatcher keeps
 //    every CU full and no lane loops), two chunks per lane for 8-byte words;
 //    grid-stride only beyond 2^20 workgroups. Packed-side accesses are nontemporal, and so are strided-side
 //    ones when the word is 16 bytes: every byte is touched once. Measured on
@@ -85,7 +85,12 @@ template <> struct Word<16> { typedef uint4 T; };
 #define TEMPI_MAX_BLOCKS (1 << 20)
 #endif
 #ifndef TEMPI_BLOCK
-#define TEMPI_BLOCK 256
+// 128-lane workgroups for the packers: against 256 on one box
+// (tools/gpu_block_ab.sh, profiles/r01/block_ab_s9.jsonl) the 512-byte-row
+// headline packs 6 223-6 288 vs 6 022-6 068 GB/s and unpacks 6 235-6 309 vs
+// 6 075-6 092, 64-byte rows unpack 5 712 vs 4 685-4 887; 512 and 1024 are no
+// better than 256. The copy kernels keep 256 (kCopyBlock)
+#define TEMPI_BLOCK 128
 #endif
 #ifndef TEMPI_NT
 // 0: plain; 1: nontemporal packed side; 2: nontemporal both sides;
@@ -376,7 +381,7 @@ __global__ __launch_bounds__(kBlock) void unpack_kernel(const KArgs<ND> a) {
 // For 1- and 2-byte words the chunk-per-lane scatter has every store
 // instruction of a wave touch 64 different rows, 16/W rows apart, so each
 // cache line of the strided side is written by 16/W separate instructions.
-// Here the workgroup's 4 KiB of packed input is staged in LDS (one 16-byte
+// Here the workgroup's kBlock x 16 bytes of packed input is staged in LDS (one 16-byte
 // load per lane), and store instruction j of a wave writes the 64 CONSECUTIVE
 // words j*64 .. j*64+63 of the wave's 1 KiB: neighbouring rows, so one
 // instruction covers a line and every line is written once. Tiles holding the
@@ -458,7 +463,7 @@ template <int W, int ND> __global__ __launch_bounds__(kBlock) void unpack_il_ker
 // s <= kDenseRatio * b): every 64-byte DRAM sector of the strided side holds
 // payload, so reading the whole window costs no more HBM traffic than reading
 // the rows, but the per-word path spends one 1/2/4-byte load instruction per
-// row. Here a workgroup's 4 KiB of packed output covers rows [rl, rh] of one
+// row. Here a workgroup's kBlock x 16 bytes of packed output covers rows [rl, rh] of one
 // inner segment, whose window the workgroup streams into LDS
 // with 16-byte coalesced loads (<= 16 KiB + s); each lane then gathers its 16 output bytes
 // from LDS (ds_read_u8) and writes them with one 16-byte store -- the "LDS
@@ -697,7 +702,7 @@ struct Job {
 };
 
 template <int W, int ND> int launch_batch_nd(bool pack, const std::vector<Job> &jobs, hipStream_t s) {
-  const bool il = il_width(pack, W); // il kernels: one 4 KiB tile per workgroup
+  const bool il = il_width(pack, W); // il kernels: one kBlock x 16-byte tile per workgroup
   BatchArgs<ND> b;
   b.nitems = 0;
   uint32_t total = 0;
@@ -943,6 +948,13 @@ int run_batch(bool pack, const tempi_hip_batch_item *items, int n, hipStream_t s
 // have count 1, stride 0); anything deeper is reported unsupported and the
 // caller packs + unpacks through a slab instead.
 constexpr int kCopyND = 3;
+// The copy kernels keep 256-lane workgroups: on the halo regions 128 measured
+// 2-5 % slower (tools/gpu_block_ab.sh), while the single-object packers gain
+// from 128 (see TEMPI_BLOCK)
+#ifndef TEMPI_COPY_BLOCK
+#define TEMPI_COPY_BLOCK 256
+#endif
+constexpr int kCopyBlock = TEMPI_COPY_BLOCK;
 
 struct CSide {
   char *first;
@@ -1023,14 +1035,14 @@ template <int W> __device__ __forceinline__ void copy_body(const CArgs &a, uint3
   typedef typename Word<W>::T WT;
   constexpr int CW = 16 / W * TEMPI_COPY_U;
   constexpr bool nt = W == 16;
-  const uint32_t tile = uint32_t(kBlock) * CW;
+  const uint32_t tile = uint32_t(kCopyBlock) * CW;
   if (a.s2) {
     for (uint32_t base = blk * tile; base < a.nwords; base += nblk * tile) {
       WT v[CW], v2[CW];
       int64_t so[CW], dof[CW];
 #pragma unroll
       for (int j = 0; j < CW; ++j) {
-        const uint32_t q = base + uint32_t(j) * kBlock + threadIdx.x;
+        const uint32_t q = base + uint32_t(j) * kCopyBlock + threadIdx.x;
         so[j] = q < a.nwords ? side_offset<W>(q, a.s) : 0;
         dof[j] = q < a.nwords ? side_offset<W>(q, a.d) : 0;
         if (q < a.nwords) {
@@ -1040,7 +1052,7 @@ template <int W> __device__ __forceinline__ void copy_body(const CArgs &a, uint3
       }
 #pragma unroll
       for (int j = 0; j < CW; ++j) {
-        const uint32_t q = base + uint32_t(j) * kBlock + threadIdx.x;
+        const uint32_t q = base + uint32_t(j) * kCopyBlock + threadIdx.x;
         if (q < a.nwords) {
           st(reinterpret_cast<WT *>(a.d.first + dof[j]), v[j], false);
           st(reinterpret_cast<WT *>(a.d2 + dof[j]), v2[j], false);
@@ -1053,18 +1065,18 @@ template <int W> __device__ __forceinline__ void copy_body(const CArgs &a, uint3
     WT v[CW];
 #pragma unroll
     for (int j = 0; j < CW; ++j) {
-      const uint32_t q = base + uint32_t(j) * kBlock + threadIdx.x;
+      const uint32_t q = base + uint32_t(j) * kCopyBlock + threadIdx.x;
       if (q < a.nwords) v[j] = ld_src(a, reinterpret_cast<const WT *>(a.s.first + side_offset<W>(q, a.s)), nt);
     }
 #pragma unroll
     for (int j = 0; j < CW; ++j) {
-      const uint32_t q = base + uint32_t(j) * kBlock + threadIdx.x;
+      const uint32_t q = base + uint32_t(j) * kCopyBlock + threadIdx.x;
       if (q < a.nwords) st(reinterpret_cast<WT *>(a.d.first + side_offset<W>(q, a.d)), v[j], nt);
     }
   }
 }
 
-template <int W> __global__ __launch_bounds__(kBlock) void copy_kernel(const CArgs a) {
+template <int W> __global__ __launch_bounds__(kCopyBlock) void copy_kernel(const CArgs a) {
   copy_body<W>(a, blockIdx.x, gridDim.x);
 }
 
@@ -1075,7 +1087,7 @@ struct CBatchArgs {
   CArgs item[kCopyMax];
 };
 
-template <int W> __global__ __launch_bounds__(kBlock) void copy_batch_kernel(const CBatchArgs b) {
+template <int W> __global__ __launch_bounds__(kCopyBlock) void copy_batch_kernel(const CBatchArgs b) {
   uint32_t lo = 0, hi = b.nitems;
   while (hi - lo > 1) {
     const uint32_t mid = (lo + hi) >> 1;
@@ -1170,7 +1182,7 @@ std::vector<CopyJob> pair_jobs(const std::vector<CopyJob> &in) {
 }
 
 uint32_t copy_blocks(const CopyJob &j) {
-  const uint64_t tile = uint64_t(kBlock) * (16 / j.w) * TEMPI_COPY_U;
+  const uint64_t tile = uint64_t(kCopyBlock) * (16 / j.w) * TEMPI_COPY_U;
   uint64_t b = (uint64_t(j.a.nwords) + tile - 1) / tile;
   if (b > TEMPI_MAX_BLOCKS) b = TEMPI_MAX_BLOCKS;
   return uint32_t(b);
@@ -1184,9 +1196,9 @@ template <int W> int launch_copy_group(const std::vector<CopyJob> &jobs, hipStre
     if (!b.nitems) return 0;
     b.first[b.nitems] = total;
     if (b.nitems == 1)
-      hipLaunchKernelGGL(copy_kernel<W>, dim3(total), dim3(kBlock), 0, s, b.item[0]);
+      hipLaunchKernelGGL(copy_kernel<W>, dim3(total), dim3(kCopyBlock), 0, s, b.item[0]);
     else
-      hipLaunchKernelGGL(copy_batch_kernel<W>, dim3(total), dim3(kBlock), 0, s, b);
+      hipLaunchKernelGGL(copy_batch_kernel<W>, dim3(total), dim3(kCopyBlock), 0, s, b);
     b.nitems = 0;
     total = 0;
     return int(hipGetLastError());
