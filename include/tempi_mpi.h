@@ -32,6 +32,14 @@
  *                    (not interposed: F8)            understand TEMPI requests
  *   MPI_Sendrecv     (not interposed)                Irecv + Isend through TEMPI
  *                                                    when either side is a device object
+ *   MPI_Probe / MPI_Iprobe / MPI_Mprobe / MPI_Improbe / MPI_Mrecv / MPI_Imrecv
+ *                    (not interposed: the reference's senders always send
+ *                    the packed bytes, sender.cpp:109,161)
+ *                                                    a co-located device send that
+ *                                                    travels as a descriptor is probed
+ *                                                    with its payload size and received
+ *                                                    as its payload, into host or device
+ *                                                    memory
  *   MPI_Alltoallv    src/alltoallv.cpp:14-68         device-buffer alltoallv
  *   MPI_Neighbor_alltoallw  src/neighbor_alltoallw.cpp:11-18 (-> internal/
  *                    neighbor_alltoallw.cpp:19-77)   per-edge Isend/Irecv when
@@ -46,9 +54,10 @@
  *   MPI_Comm_free    src/comm_free.cpp:13-19         drop per-handle caches
  *
  * Error behaviour: return codes of the library pass through unchanged. Where
- * TEMPI itself detects an error (a pack that does not fit in outsize) it
- * raises MPI_ERR_TRUNCATE on the communicator's error handler and returns it
- * (the reference silently overruns). GPU runtime failures abort with a
+ * TEMPI itself detects an error (a pack that does not fit in outsize, a
+ * message larger than the receive that TEMPI carried) it raises
+ * MPI_ERR_TRUNCATE on the communicator's error handler and returns it, with
+ * the status's MPI_ERROR set (the reference silently overruns). GPU runtime failures abort with a
  * message, as the reference does (/root/reference/include/cuda_runtime.hpp:13-20).
  */
 #ifndef TEMPI_MPI_H
@@ -91,6 +100,12 @@ int MPI_Request_get_status(MPI_Request request, int *flag, MPI_Status *status);
 int MPI_Cancel(MPI_Request *request);
 int MPI_Sendrecv(const void *sendbuf, int sendcount, MPI_Datatype sendtype, int dest, int sendtag, void *recvbuf,
                  int recvcount, MPI_Datatype recvtype, int source, int recvtag, MPI_Comm comm, MPI_Status *status);
+int MPI_Probe(int source, int tag, MPI_Comm comm, MPI_Status *status);
+int MPI_Iprobe(int source, int tag, MPI_Comm comm, int *flag, MPI_Status *status);
+int MPI_Mprobe(int source, int tag, MPI_Comm comm, MPI_Message *message, MPI_Status *status);
+int MPI_Improbe(int source, int tag, MPI_Comm comm, int *flag, MPI_Message *message, MPI_Status *status);
+int MPI_Mrecv(void *buf, int count, MPI_Datatype datatype, MPI_Message *message, MPI_Status *status);
+int MPI_Imrecv(void *buf, int count, MPI_Datatype datatype, MPI_Message *message, MPI_Request *request);
 int MPI_Alltoallv(const void *sendbuf, const int sendcounts[], const int sdispls[],
                   MPI_Datatype sendtype, void *recvbuf, const int recvcounts[], const int rdispls[],
                   MPI_Datatype recvtype, MPI_Comm comm);

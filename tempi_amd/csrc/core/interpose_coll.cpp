@@ -116,6 +116,8 @@ int isir(const void *sendbuf, const int *scounts, const int *sdispls, MPI_Dataty
       p2p::Route route;
       if (p2p::handles(b, rcounts[p], rtype, p, &route))
         p2p::irecv(b, rcounts[p], rtype, p, tag, comm, &r, route);
+      else if (p2p::host_recv_aware(p, comm)) // a host block a peer's device send may reach as a descriptor
+        p2p::irecv_host(b, rcounts[p], rtype, p, tag, comm, &r);
       else
         next.MPI_Irecv(b, rcounts[p], rtype, p, tag, comm, &r);
       reqs.push_back(r);
@@ -200,12 +202,11 @@ TEMPI_EXPORT int MPI_Alltoallv(const void *sendbuf, const int sendcounts[], cons
   int n = 0, rank = 0;
   MPI_Comm_size(comm, &n);
   MPI_Comm_rank(comm, &rank);
-  int64_t lo, hi;
-  const bool sdev = span(sendcounts, sdispls, n, sendtype, &lo, &hi) &&
-                    gpu::classify(static_cast<const char *>(sendbuf) + lo).device_accessible;
-  const bool rdev = span(recvcounts, rdispls, n, recvtype, &lo, &hi) &&
-                    gpu::classify(static_cast<char *>(recvbuf) + lo).device_accessible;
-  if (!sdev && !rdev) return lib();
+  // Every rank takes TEMPI's route, whatever memory its own blocks are in:
+  // a rank whose buffers are all on the host still exchanges with ranks
+  // whose buffers are not, so the choice must be the same everywhere (the
+  // library's alltoallv on `comm` cannot match TEMPI's messages on the
+  // private duplicate). Only conditions every rank shares lead to the library.
   if (!type_lookup(sendtype) || !type_lookup(recvtype)) return lib(); // uncommitted: let MPI complain
   const MPI_Comm c = private_comm(comm);
   int rc;

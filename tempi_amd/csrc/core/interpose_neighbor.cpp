@@ -91,19 +91,9 @@ bool neighbours(MPI_Comm comm, std::vector<int> &in, std::vector<int> &out) {
   return false;
 }
 
-// true when some non-empty block lives in GPU-accessible memory
-bool any_device(const void *buf, const int *counts, const MPI_Aint *displs, const MPI_Datatype *types, size_t n) {
-  for (size_t i = 0; i < n; ++i) {
-    if (counts[i] <= 0) continue;
-    MPI_Aint tlb = 0, text = 0;
-    MPI_Type_get_true_extent(types[i], &tlb, &text);
-    if (gpu::classify(static_cast<const char *>(buf) + displs[i] + tlb).device_accessible) return true;
-  }
-  return false;
-}
-
 // one Isend / Irecv per edge through the interposed entry points (device
-// blocks -> TEMPI transport, host blocks -> library), receives first
+// blocks -> TEMPI transport, host blocks -> library sends and
+// descriptor-aware receives), receives first
 int isir(const void *sendbuf, const int *scounts, const MPI_Aint *sdispls, const MPI_Datatype *stypes,
          void *recvbuf, const int *rcounts, const MPI_Aint *rdispls, const MPI_Datatype *rtypes, MPI_Comm comm,
          const std::vector<int> &in, const std::vector<int> &out) {
@@ -172,10 +162,10 @@ TEMPI_EXPORT int MPI_Neighbor_alltoallw(const void *sendbuf, const int sendcount
                                        recvtypes, comm);
   };
   std::vector<int> in, out;
+  // every rank takes the per-edge route, whatever memory its own blocks are
+  // in: its neighbours' device blocks travel on the private duplicate, which
+  // the library's own algorithm on `comm` would never match
   if (!state.active || !gpu::available() || !neighbours(comm, in, out)) return lib();
-  if (!any_device(sendbuf, sendcounts, sdispls, sendtypes, out.size()) &&
-      !any_device(recvbuf, recvcounts, rdispls, recvtypes, in.size()))
-    return lib(); // host memory only: the library's own algorithm
   counters.neighbor_colls++;
   return isir(sendbuf, sendcounts, sdispls, sendtypes, recvbuf, recvcounts, rdispls, recvtypes, comm, in, out);
 }
@@ -198,10 +188,7 @@ TEMPI_EXPORT int MPI_Neighbor_alltoallv(const void *sendbuf, const int sendcount
   for (size_t i = 0; i < out.size(); ++i) sd[i] = MPI_Aint(sdispls[i]) * sext;
   for (size_t i = 0; i < in.size(); ++i) rd[i] = MPI_Aint(rdispls[i]) * rext;
   std::vector<MPI_Datatype> st(out.size(), sendtype), rt(in.size(), recvtype);
-  if (!any_device(sendbuf, sendcounts, sd.data(), st.data(), out.size()) &&
-      !any_device(recvbuf, recvcounts, rd.data(), rt.data(), in.size()))
-    return lib();
-  counters.neighbor_colls++;
+  counters.neighbor_colls++; // (every rank takes this route: see MPI_Neighbor_alltoallw)
   return isir(sendbuf, sendcounts, sd.data(), st.data(), recvbuf, recvcounts, rd.data(), rt.data(), comm, in, out);
 }
 

@@ -74,6 +74,8 @@ TEMPI_EXPORT int MPI_Irecv(void *buf, int count, MPI_Datatype datatype, int sour
   if (p2p::handles(buf, count, datatype, source, &route))
     return p2p::irecv(buf, count, datatype, source, tag, comm, request, route);
   if (state.active) p2p::progress(false);
+  // a host buffer: a co-located TEMPI device send may arrive as a descriptor
+  if (p2p::host_recv_aware(source, comm)) return p2p::irecv_host(buf, count, datatype, source, tag, comm, request);
   counters.lib_recvs++;
   return next.MPI_Irecv(buf, count, datatype, source, tag, comm, request);
 }
@@ -285,8 +287,11 @@ TEMPI_EXPORT int MPI_Sendrecv(const void *sendbuf, int sendcount, MPI_Datatype s
                               MPI_Comm comm, MPI_Status *status) {
   resolve_next();
   p2p::Route sr, rr;
+  // TEMPI's when either side is a device object, or when the host receive
+  // could meet a descriptor
   const bool mine = state.active && (p2p::handles(sendbuf, sendcount, sendtype, dest, &sr) ||
-                                     p2p::handles(recvbuf, recvcount, recvtype, source, &rr));
+                                     p2p::handles(recvbuf, recvcount, recvtype, source, &rr) ||
+                                     p2p::host_recv_aware(source, comm));
   if (!mine) {
     if (state.active && p2p::send_gated(comm, dest)) p2p::drain_sends(comm, dest); // keep send order
     return next.MPI_Sendrecv(sendbuf, sendcount, sendtype, dest, sendtag, recvbuf, recvcount, recvtype, source,
@@ -300,4 +305,42 @@ TEMPI_EXPORT int MPI_Sendrecv(const void *sendbuf, int sendcount, MPI_Datatype s
   rc = MPI_Wait(&r, status);
   const int rc2 = MPI_Wait(&s, MPI_STATUS_IGNORE);
   return rc != MPI_SUCCESS ? rc : rc2;
+}
+
+// The probe family and matched receives: not interposed by the reference,
+// whose senders always send the packed bytes. Here a co-located device send
+// may travel as a descriptor, so a probe reports the payload's size and a
+// matched receive lands the payload (p2p.hpp).
+TEMPI_EXPORT int MPI_Probe(int source, int tag, MPI_Comm comm, MPI_Status *status) {
+  resolve_next();
+  return p2p::probe(source, tag, comm, nullptr, status);
+}
+
+TEMPI_EXPORT int MPI_Iprobe(int source, int tag, MPI_Comm comm, int *flag, MPI_Status *status) {
+  resolve_next();
+  return p2p::probe(source, tag, comm, flag, status);
+}
+
+TEMPI_EXPORT int MPI_Mprobe(int source, int tag, MPI_Comm comm, MPI_Message *message, MPI_Status *status) {
+  resolve_next();
+  return p2p::mprobe(source, tag, comm, nullptr, message, status);
+}
+
+TEMPI_EXPORT int MPI_Improbe(int source, int tag, MPI_Comm comm, int *flag, MPI_Message *message,
+                             MPI_Status *status) {
+  resolve_next();
+  return p2p::mprobe(source, tag, comm, flag, message, status);
+}
+
+TEMPI_EXPORT int MPI_Mrecv(void *buf, int count, MPI_Datatype datatype, MPI_Message *message, MPI_Status *status) {
+  resolve_next();
+  if (!state.active) return next.MPI_Mrecv(buf, count, datatype, message, status);
+  return p2p::mrecv(buf, count, datatype, message, status);
+}
+
+TEMPI_EXPORT int MPI_Imrecv(void *buf, int count, MPI_Datatype datatype, MPI_Message *message,
+                            MPI_Request *request) {
+  resolve_next();
+  if (!state.active) return next.MPI_Imrecv(buf, count, datatype, message, request);
+  return p2p::imrecv(buf, count, datatype, message, request);
 }

@@ -35,6 +35,12 @@
   X(MPI_Request_get_status)                                                    \
   X(MPI_Cancel)                                                                \
   X(MPI_Sendrecv)                                                              \
+  X(MPI_Probe)                                                                 \
+  X(MPI_Iprobe)                                                                \
+  X(MPI_Mprobe)                                                                \
+  X(MPI_Improbe)                                                               \
+  X(MPI_Mrecv)                                                                 \
+  X(MPI_Imrecv)                                                                \
   X(MPI_Alltoallv)                                                             \
   X(MPI_Neighbor_alltoallv)                                                    \
   X(MPI_Neighbor_alltoallw)                                                    \

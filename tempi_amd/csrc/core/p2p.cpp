@@ -13,6 +13,7 @@
 #include "type_cache.hpp"
 
 #include <chrono>
+#include <cstddef>
 #include <cstdlib>
 #include <cstring>
 #include <algorithm>
@@ -426,6 +427,8 @@ struct Op {
   bool watched = false;                        // in libWatch
   bool detached = false;                       // MPI_Request_free'd: dropped when done
   bool done = false;
+  int err = MPI_SUCCESS;                       // completed with this error (MPI_ERR_TRUNCATE, ...)
+  MPI_Comm errComm = MPI_COMM_NULL;            // whose error handler the wait raises it on
 };
 
 // ops with a library request outstanding (tested together by progress()).
@@ -689,7 +692,8 @@ struct IsendOp : Op {
       desc.bytes = bytes;
       desc.senderWorld = state.worldRank;
       desc.senderPid = int32_t(getpid());
-      desc.ackTag = int32_t(dslab->id % uint32_t(tagUb));
+      // slab acks take [0, tagUb/2); IPC COPY acks the upper half
+      desc.ackTag = int32_t(dslab->id % uint32_t(std::max(1, tagUb / 2)));
       desc.rawPtr = reinterpret_cast<uint64_t>(dslab->dev);
       desc.gpu = gpu::identity(device);
       std::memcpy(desc.handle, slab_ipc_handle(dslab), sizeof desc.handle);
@@ -985,6 +989,69 @@ bool copy_ok(const tempi_hip_desc &dst, const tempi_hip_desc &src) {
   return dst.ndims <= 3 && src.ndims <= 3 && b == desc_bytes(dst) && b < (int64_t(1) << 31);
 }
 
+// A message a probe had to receive to look at it (it has a descriptor's
+// size): it stays matchable, in arrival order, until a receive or probe takes
+// it, or an MPI_Mprobe handle claims it.
+struct Probed {
+  MPI_Comm comm = MPI_COMM_NULL;
+  MPI_Status st{};         // source and tag as the library reported them
+  std::vector<char> bytes; // the message as received (MPI_BYTE)
+  int64_t payload = 0;     // what the application receives (a descriptor's payload size)
+};
+std::deque<std::unique_ptr<Probed>> probed;
+std::unordered_map<uint32_t, std::unique_ptr<Probed>> probedMsgs; // MPI_Mprobe handles
+uint32_t nextMsgHandle = 1;
+
+bool probed_matches(const Probed &p, int source, int tag, MPI_Comm comm) {
+  return p.comm == comm && (source == MPI_ANY_SOURCE || source == p.st.MPI_SOURCE) &&
+         (tag == MPI_ANY_TAG || tag == p.st.MPI_TAG);
+}
+
+// the earliest kept message a receive (source, tag, comm) matches, taken out
+std::unique_ptr<Probed> take_probed(int source, int tag, MPI_Comm comm) {
+  if (probed.empty()) return nullptr;
+  for (auto it = probed.begin(); it != probed.end(); ++it)
+    if (probed_matches(**it, source, tag, comm)) {
+      std::unique_ptr<Probed> p = std::move(*it);
+      probed.erase(it);
+      return p;
+    }
+  return nullptr;
+}
+
+bool is_descriptor(const void *msg, int n) { return is_direct(msg, n) || is_ipc(msg, n) || is_ipc_copy(msg, n); }
+
+int64_t descriptor_payload(const void *msg, int n) {
+  int64_t b = n;
+  if (is_direct(msg, n)) std::memcpy(&b, static_cast<const char *>(msg) + offsetof(DirectDesc, bytes), sizeof b);
+  if (is_ipc(msg, n)) std::memcpy(&b, static_cast<const char *>(msg) + offsetof(IpcDesc, bytes), sizeof b);
+  if (is_ipc_copy(msg, n)) std::memcpy(&b, static_cast<const char *>(msg) + offsetof(IpcCopyDesc, bytes), sizeof b);
+  return b;
+}
+
+// A message that reached host memory (`msg`, n bytes: a descriptor or the
+// packed bytes themselves) delivered into the application's host receive
+// (buf, count, dt): the descriptor's bytes are fetched first, then unpacked.
+// Returns MPI_SUCCESS or MPI_ERR_TRUNCATE (nothing written); *received =
+// bytes delivered.
+int land_host(const char *msg, int n, void *buf, int count, MPI_Datatype dt, MPI_Comm comm, int64_t *received) {
+  std::vector<char> fetched;
+  if (is_descriptor(msg, n)) {
+    land_descriptor(msg, n, fetched); // releases the sender whatever happens next
+    msg = fetched.data();
+    n = int(fetched.size());
+  }
+  int size = 0;
+  MPI_Type_size(dt, &size);
+  *received = 0;
+  if (int64_t(n) > int64_t(size) * count) return MPI_ERR_TRUNCATE;
+  const int elems = size ? n / size : 0;
+  int pos = 0;
+  if (elems) next.MPI_Unpack(msg, n, &pos, buf, elems, dt, comm);
+  *received = int64_t(elems) * size;
+  return MPI_SUCCESS;
+}
+
 struct IrecvOp : Op {
   RecordRef rec;
   char *origin; // GPU-visible
@@ -1004,16 +1071,27 @@ struct IrecvOp : Op {
   bool xcopy = false;     // an IPC COPY out of the sender's memory: ack it when done
   int copyWorld = -1, copyTag = 0;
 
+  // msg: receive this library message (MPI_Mrecv); pre: a message a probe
+  // already received (it is delivered at once)
   IrecvOp(const TypeRecord *r, char *o, int c, MPI_Datatype d, int source, int tag, MPI_Comm cm, int dev,
-          int64_t b)
+          int64_t b, MPI_Message *msg = nullptr, std::unique_ptr<Probed> pre = nullptr)
       : rec(r->ref()), origin(o), count(c), dt(d), comm(cm), bytes(b) {
     device = dev;
+    errComm = cm;
     const size_t cap = std::max<size_t>(size_t(bytes), kDescCap);
     hslab = pinned_pool().get(cap, device);
-    next.MPI_Irecv(hslab->host, int(cap), MPI_PACKED, source, tag, comm, &lib);
+    if (pre) {
+      std::memcpy(hslab->host, pre->bytes.data(), std::min(cap, pre->bytes.size()));
+      lib_done(pre->st);
+      return;
+    }
+    if (msg)
+      next.MPI_Imrecv(hslab->host, int(cap), MPI_PACKED, msg, &lib);
+    else
+      next.MPI_Irecv(hslab->host, int(cap), MPI_PACKED, source, tag, comm, &lib);
     // a message from this same process is matched as the receive is posted:
     // take it now, so its copy can start while the caller posts more
-    if (source >= 0 && topology::world_rank(comm, source) == state.worldRank) {
+    if (!msg && source >= 0 && topology::world_rank(comm, source) == state.worldRank) {
       int flag = 0;
       MPI_Status st;
       next.MPI_Test(&lib, &flag, &st);
@@ -1028,6 +1106,17 @@ struct IrecvOp : Op {
   void cancel() override {
     if (!arrived && lib != MPI_REQUEST_NULL) next.MPI_Cancel(&lib);
   }
+  // the message is larger than the receive allows: the wait returns
+  // MPI_ERR_TRUNCATE (on the communicator's error handler); nothing is
+  // written, and the sender has already been released
+  void truncate(int64_t got) {
+    LOG_DEBUG("message truncated: " << got << " B into " << bytes);
+    err = MPI_ERR_TRUNCATE;
+    elems = 0;
+    pinned_pool().put(hslab);
+    hslab = nullptr;
+    done = true;
+  }
   void lib_done(const MPI_Status &st) override { // arrived: queue its unpack
     const Packer &packer = *rec->packer;
     if (!arrived) {
@@ -1038,6 +1127,14 @@ struct IrecvOp : Op {
         libStatus = st;
         pinned_pool().put(hslab);
         hslab = nullptr;
+        return;
+      }
+      if (st.MPI_ERROR != MPI_SUCCESS) { // the library's own error (e.g. its truncation)
+        libStatus = st;
+        err = st.MPI_ERROR;
+        pinned_pool().put(hslab);
+        hslab = nullptr;
+        done = true;
         return;
       }
     }
@@ -1058,7 +1155,10 @@ struct IrecvOp : Op {
       DirectDesc dd;
       std::memcpy(&dd, hslab->host, sizeof dd);
       direct = claim_direct(dd);
-      if (dd.bytes > bytes) LOG_FATAL("message truncated: " << dd.bytes << " B into " << bytes);
+      if (dd.bytes > bytes) {
+        direct_finish(direct);
+        return truncate(dd.bytes);
+      }
       elems = size ? dd.bytes / size : 0;
       const bool sameDevice = direct->device == device;
       tempi_hip_desc mine;
@@ -1086,7 +1186,10 @@ struct IrecvOp : Op {
     if (is_ipc_copy(hslab->host, n)) {
       IpcCopyDesc xd;
       std::memcpy(&xd, hslab->host, sizeof xd);
-      if (xd.bytes > bytes) LOG_FATAL("message truncated: " << xd.bytes << " B into " << bytes);
+      if (xd.bytes > bytes) {
+        send_ack(xd.senderWorld, xd.ackTag, kCopyDone);
+        return truncate(xd.bytes);
+      }
       elems = size ? xd.bytes / size : 0;
       const bool local = xd.senderPid == int32_t(getpid());
       if (!local) recycle_alloc_maps();
@@ -1122,7 +1225,10 @@ struct IrecvOp : Op {
     if (size_t(n) == sizeof(IpcDesc) && d.magic[0] == kMagic0 && d.magic[1] == kMagic1) {
       ipc = true;
       desc = d;
-      if (d.bytes > bytes) LOG_FATAL("message truncated: " << d.bytes << " B into " << bytes);
+      if (d.bytes > bytes) {
+        send_ack(d);
+        return truncate(d.bytes);
+      }
       void *base = peer_pointer(d);
       if (!base) { // cannot map the sender's slab: ask for the bytes via the host
         ipc = false;
@@ -1139,7 +1245,7 @@ struct IrecvOp : Op {
       if (ipcSystemLoads && d.gpu != gpu::identity(device)) // another GPU's slab, reused between messages
         for (size_t i = first; i < pendingUnpack.items.size(); ++i) pendingUnpack.items[i].flags |= TEMPI_HIP_ITEM_REMOTE;
     } else {
-      if (int64_t(n) > bytes) LOG_FATAL("message truncated: " << n << " B into " << bytes);
+      if (int64_t(n) > bytes) return truncate(n);
       elems = size ? n / size : 0;
       pendingUnpack.add_items(this, packer, hslab->dev, origin, elems);
     }
@@ -1156,7 +1262,7 @@ struct IrecvOp : Op {
   void status(MPI_Status *s) const override {
     if (s != MPI_STATUS_IGNORE) {
       *s = libStatus;
-      s->MPI_ERROR = MPI_SUCCESS;
+      s->MPI_ERROR = err;
       set_received(s, elems * rec->desc.size);
       if (cancelled) MPI_Status_set_cancelled(s, 1);
     }
@@ -1220,12 +1326,24 @@ struct LibIrecvOp : Op {
   MPI_Datatype dt;
   MPI_Comm comm;
   MPI_Status libStatus{};
+  int64_t cap = 0; // packed bytes the receive allows
   int elems = 0;
   int received = 0; // bytes
-  LibIrecvOp(void *b, int c, MPI_Datatype d, int source, int tag, MPI_Comm cm)
+  LibIrecvOp(void *b, int c, MPI_Datatype d, int source, int tag, MPI_Comm cm, MPI_Message *msg = nullptr,
+             std::unique_ptr<Probed> pre = nullptr)
       : user(b), count(c), dt(hold_type(d)), comm(cm) {
-    buf.resize(std::max<size_t>(size_t(std::max<int64_t>(pack_size(c, d, cm), 1)), kDescCap));
-    next.MPI_Irecv(buf.data(), int(buf.size()), MPI_PACKED, source, tag, comm, &lib);
+    errComm = cm;
+    cap = pack_size(c, d, cm);
+    buf.resize(std::max<size_t>(size_t(std::max<int64_t>(cap, 1)), kDescCap));
+    if (pre) {
+      std::memcpy(buf.data(), pre->bytes.data(), std::min(buf.size(), pre->bytes.size()));
+      lib_done(pre->st);
+      return;
+    }
+    if (msg)
+      next.MPI_Imrecv(buf.data(), int(buf.size()), MPI_PACKED, msg, &lib);
+    else
+      next.MPI_Irecv(buf.data(), int(buf.size()), MPI_PACKED, source, tag, comm, &lib);
     watch(this);
   }
   bool cancelled = false;
@@ -1240,13 +1358,23 @@ struct LibIrecvOp : Op {
       cancelled = done = true;
       return;
     }
+    if (st.MPI_ERROR != MPI_SUCCESS) { // the library's own error (e.g. its truncation)
+      err = st.MPI_ERROR;
+      done = true;
+      return;
+    }
     int n = 0, size = 0;
     MPI_Get_count(&libStatus, MPI_PACKED, &n);
-    if (is_direct(buf.data(), n) || is_ipc(buf.data(), n) || is_ipc_copy(buf.data(), n)) { // a TEMPI descriptor
+    if (is_descriptor(buf.data(), n)) { // a TEMPI descriptor
       std::vector<char> bytes;
       land_descriptor(buf.data(), n, bytes);
       buf.swap(bytes);
       n = int(buf.size());
+    }
+    if (int64_t(n) > cap) { // larger than the receive allows: nothing written
+      err = MPI_ERR_TRUNCATE;
+      done = true;
+      return;
     }
     MPI_Type_size(dt, &size);
     elems = size ? n / size : 0;
@@ -1259,7 +1387,100 @@ struct LibIrecvOp : Op {
   void status(MPI_Status *s) const override {
     if (s != MPI_STATUS_IGNORE) {
       *s = libStatus;
-      s->MPI_ERROR = MPI_SUCCESS;
+      s->MPI_ERROR = err;
+      set_received(s, received);
+      if (cancelled) MPI_Status_set_cancelled(s, 1);
+    }
+  }
+};
+
+// A receive into host memory (p2p::irecv_host) that a co-located TEMPI send
+// may reach with a descriptor. Contiguous receives of at least kDescCap bytes
+// are posted in place with the buffer's first kDescCap bytes saved: a
+// descriptor that lands there is recognised (size + magic), the saved bytes
+// are put back and what it names is fetched and copied in. Other receives
+// land in a staging buffer as MPI_PACKED and are unpacked from it.
+struct HostIrecvOp : Op {
+  void *user;
+  int count;
+  MPI_Datatype dt = MPI_DATATYPE_NULL; // held for staged receives (unpacked with it)
+  MPI_Comm comm;
+  int64_t cap = 0; // bytes the receive allows
+  bool inPlace = false;
+  std::vector<char> stage;
+  alignas(16) char saved[kDescCap];
+  MPI_Status libStatus{};
+  int64_t received = 0;
+  bool cancelled = false;
+
+  HostIrecvOp(void *b, int c, MPI_Datatype d, int source, int tag, MPI_Comm cm, std::unique_ptr<Probed> pre)
+      : user(b), count(c), comm(cm) {
+    errComm = cm;
+    int size = 0;
+    MPI_Type_size(d, &size);
+    cap = int64_t(size) * c;
+    MPI_Aint lb = 0, ext = 0, tlb = 0, text = 0;
+    MPI_Type_get_extent(d, &lb, &ext);
+    MPI_Type_get_true_extent(d, &tlb, &text);
+    inPlace = !pre && tlb == 0 && text == size && (c == 1 || ext == size) && cap >= int64_t(kDescCap);
+    if (inPlace) {
+      std::memcpy(saved, b, kDescCap);
+      next.MPI_Irecv(b, c, d, source, tag, cm, &lib);
+      watch(this);
+      return;
+    }
+    dt = hold_type(d);
+    if (pre) {
+      libStatus = pre->st;
+      deliver(pre->bytes.data(), int(pre->bytes.size()));
+      return;
+    }
+    stage.resize(std::max({size_t(std::max<int64_t>(cap, 1)), size_t(pack_size(c, d, cm)), kDescCap}));
+    next.MPI_Irecv(stage.data(), int(stage.size()), MPI_PACKED, source, tag, cm, &lib);
+    watch(this);
+  }
+  ~HostIrecvOp() override { drop_type(dt); }
+  void cancel() override {
+    if (lib != MPI_REQUEST_NULL) next.MPI_Cancel(&lib);
+  }
+  void deliver(const char *msg, int n) {
+    err = land_host(msg, n, user, count, dt, comm, &received);
+    done = true;
+  }
+  void lib_done(const MPI_Status &st) override {
+    libStatus = st;
+    int c = 0;
+    MPI_Test_cancelled(&st, &c);
+    if (c || st.MPI_ERROR != MPI_SUCCESS) {
+      cancelled = c;
+      err = c ? MPI_SUCCESS : st.MPI_ERROR;
+      done = true;
+      return;
+    }
+    int n = 0;
+    MPI_Get_count(&st, MPI_BYTE, &n);
+    if (!inPlace) return deliver(stage.data(), n);
+    received = n;
+    if (is_descriptor(user, n)) {
+      alignas(16) char raw[kDescCap];
+      std::memcpy(raw, user, size_t(n));
+      std::memcpy(user, saved, size_t(n)); // the application's bytes under the descriptor
+      std::vector<char> fetched;
+      land_descriptor(raw, n, fetched);
+      received = 0;
+      if (int64_t(fetched.size()) > cap) {
+        err = MPI_ERR_TRUNCATE;
+      } else {
+        std::memcpy(user, fetched.data(), fetched.size());
+        received = int64_t(fetched.size());
+      }
+    }
+    done = true;
+  }
+  void status(MPI_Status *s) const override {
+    if (s != MPI_STATUS_IGNORE) {
+      *s = libStatus;
+      s->MPI_ERROR = err;
       set_received(s, received);
       if (cancelled) MPI_Status_set_cancelled(s, 1);
     }
@@ -1488,14 +1709,16 @@ int irecv(void *buf, int count, MPI_Datatype dt, int source, int tag, MPI_Comm c
   if (!pendingPack.empty()) flush_list(pendingPack, true);
   const uint64_t t0 = tick();
   counters.irecvs++;
+  std::unique_ptr<Probed> pre = take_probed(source, tag, comm); // a probe already received it
   if (!rec->packer) {
-    *req = add(std::make_unique<LibIrecvOp>(buf, count, dt, source, tag, comm));
+    *req = add(std::make_unique<LibIrecvOp>(buf, count, dt, source, tag, comm, nullptr, std::move(pre)));
     return MPI_SUCCESS;
   }
   const gpu::Ptr &p = route.ptr;
   const int64_t bytes = packed_bytes(rec, count, dt, comm);
   char *origin = static_cast<char *>(p.dptr) - rec->desc.start;
-  *req = add(std::make_unique<IrecvOp>(rec, origin, count, dt, source, tag, comm, p.device, bytes));
+  *req = add(std::make_unique<IrecvOp>(rec, origin, count, dt, source, tag, comm, p.device, bytes, nullptr,
+                                       std::move(pre)));
   // keep the GPU busy while the caller is still posting: launch arrived
   // messages' copies / unpacks once a launch's worth has queued up
   // (sooner while the GPU has no scatter work: the first batch starts early)
@@ -1638,8 +1861,10 @@ bool progress(bool full) {
     pollIdx.resize(size_t(n));
     pollSt.resize(size_t(n));
     int outcount = 0;
-    next.MPI_Testsome(n, pollReqs.data(), &outcount, pollIdx.data(), pollSt.data());
+    const int trc = next.MPI_Testsome(n, pollReqs.data(), &outcount, pollIdx.data(), pollSt.data());
     if (outcount == MPI_UNDEFINED) outcount = 0;
+    if (trc != MPI_ERR_IN_STATUS) // the statuses' MPI_ERROR fields are set only with this code
+      for (int k = 0; k < outcount; ++k) pollSt[size_t(k)].MPI_ERROR = MPI_SUCCESS;
     std::vector<size_t> ackedSlots;
     for (int k = 0; k < outcount; ++k) {
       const size_t i = size_t(pollIdx[size_t(k)]);
@@ -1701,6 +1926,15 @@ bool progress(bool full) {
 
 bool busy() { return !active.empty() || !pendingAcks.empty(); }
 
+namespace {
+// a completed operation's error, raised on its communicator's handler (as
+// the library does for its own requests) and returned
+int finish_error(int err, MPI_Comm comm) {
+  if (err == MPI_SUCCESS) return MPI_SUCCESS;
+  return raise_error(comm == MPI_COMM_NULL ? MPI_COMM_WORLD : comm, err);
+}
+} // namespace
+
 int wait(MPI_Request *req, MPI_Status *status) {
   const uint32_t h = uint32_t(*req);
   auto it = active.find(h);
@@ -1712,9 +1946,11 @@ int wait(MPI_Request *req, MPI_Status *status) {
     if (!op->done) op->stalled();
   }
   it->second->status(status);
+  const int err = op->err;
+  const MPI_Comm ec = op->errComm;
   active.erase(it);
   *req = MPI_REQUEST_NULL;
-  return MPI_SUCCESS;
+  return finish_error(err, ec);
 }
 
 int test(MPI_Request *req, int *flag, MPI_Status *status) {
@@ -1726,8 +1962,11 @@ int test(MPI_Request *req, int *flag, MPI_Status *status) {
   *flag = it->second->done ? 1 : 0;
   if (*flag) {
     it->second->status(status);
+    const int err = it->second->err;
+    const MPI_Comm ec = it->second->errComm;
     active.erase(it);
     *req = MPI_REQUEST_NULL;
+    return finish_error(err, ec);
   }
   return MPI_SUCCESS;
 }
@@ -1736,40 +1975,214 @@ int recv_host_ipc_aware(void *buf, int count, MPI_Datatype dt, int source, int t
                         MPI_Status *status, bool *handled) {
   *handled = false;
   if (!state.active || !gpu::available() || source == MPI_PROC_NULL) return MPI_SUCCESS;
+  *handled = true;
+  auto land = [&](const char *msg, int n, MPI_Status st) {
+    int64_t got = 0;
+    const int e = land_host(msg, n, buf, count, dt, comm, &got);
+    if (status != MPI_STATUS_IGNORE) {
+      *status = st;
+      status->MPI_ERROR = e;
+      set_received(status, got);
+    }
+    return e == MPI_SUCCESS ? MPI_SUCCESS : raise_error(comm, e);
+  };
+  if (std::unique_ptr<Probed> p = take_probed(source, tag, comm)) // a probe already received it
+    return land(p->bytes.data(), int(p->bytes.size()), p->st);
   MPI_Message msg;
   MPI_Status st;
   // keep TEMPI operations moving while we wait for the message
   for (;;) {
     int flag = 0;
-    MPI_Improbe(source, tag, comm, &flag, &msg, &st);
+    const int rc = next.MPI_Improbe(source, tag, comm, &flag, &msg, &st);
+    if (rc != MPI_SUCCESS) return rc;
     if (flag) break;
     progress();
   }
-  *handled = true;
   int n = 0;
   MPI_Get_count(&st, MPI_BYTE, &n);
   if (size_t(n) != sizeof(IpcDesc) && size_t(n) != sizeof(DirectDesc) && size_t(n) != sizeof(IpcCopyDesc))
-    return MPI_Mrecv(buf, count, dt, &msg, status);
+    return next.MPI_Mrecv(buf, count, dt, &msg, status);
   alignas(16) char raw[kDescCap];
-  MPI_Mrecv(raw, n, MPI_BYTE, &msg, &st);
-  int size = 0;
-  MPI_Type_size(dt, &size);
-  std::vector<char> packed;
-  int nbytes = n;
-  const char *src = raw;
-  if (is_direct(raw, n) || is_ipc(raw, n) || is_ipc_copy(raw, n)) { // a TEMPI descriptor: fetch what it names
-    land_descriptor(raw, n, packed);
-    src = packed.data();
-    nbytes = int(packed.size());
-  }
-  const int elems = size ? nbytes / size : 0;
-  int pos = 0;
-  next.MPI_Unpack(src, nbytes, &pos, buf, elems, dt, comm);
-  if (status != MPI_STATUS_IGNORE) {
-    *status = st;
-    set_received(status, int64_t(elems) * size);
-  }
+  next.MPI_Mrecv(raw, n, MPI_BYTE, &msg, &st);
+  return land(raw, n, st);
+}
+
+bool host_recv_aware(int source, MPI_Comm comm) {
+  if (!state.active || !gpu::available() || source == MPI_PROC_NULL) return false;
+  if (std::getenv("TEMPI_NO_HOST_RECV") != nullptr) return false; // A/B only: host receives straight to the library
+  return source == MPI_ANY_SOURCE || topology::colocated(comm, source);
+}
+
+int irecv_host(void *buf, int count, MPI_Datatype dt, int source, int tag, MPI_Comm comm, MPI_Request *req) {
+  counters.lib_recvs++;
+  *req = add(std::make_unique<HostIrecvOp>(buf, count, dt, source, tag, comm, take_probed(source, tag, comm)));
   return MPI_SUCCESS;
+}
+
+namespace {
+bool descriptor_sized(int n) {
+  return size_t(n) == sizeof(IpcDesc) || size_t(n) == sizeof(DirectDesc) || size_t(n) == sizeof(IpcCopyDesc);
+}
+
+// receive a library message of a descriptor's size to look at it
+std::unique_ptr<Probed> receive_probed(MPI_Message *m, int n, MPI_Comm comm) {
+  auto p = std::make_unique<Probed>();
+  p->comm = comm;
+  p->bytes.resize(size_t(n));
+  next.MPI_Mrecv(p->bytes.data(), n, MPI_BYTE, m, &p->st);
+  p->st.MPI_ERROR = MPI_SUCCESS;
+  p->payload = descriptor_payload(p->bytes.data(), n);
+  return p;
+}
+
+void report(const Probed &p, MPI_Status *status) {
+  if (status == MPI_STATUS_IGNORE) return;
+  *status = p.st;
+  set_received(status, p.payload);
+}
+} // namespace
+
+int probe(int source, int tag, MPI_Comm comm, int *flag, MPI_Status *status) {
+  if (source == MPI_PROC_NULL || !state.active)
+    return flag ? next.MPI_Iprobe(source, tag, comm, flag, status) : next.MPI_Probe(source, tag, comm, status);
+  if (flag && busy()) progress(false);
+  for (;;) {
+    for (const auto &p : probed)
+      if (probed_matches(*p, source, tag, comm)) {
+        report(*p, status);
+        if (flag) *flag = 1;
+        return MPI_SUCCESS;
+      }
+    int f = 0;
+    MPI_Status st;
+    int rc;
+    if (!flag && !busy()) { // nothing of TEMPI's to keep moving: the library may block
+      rc = next.MPI_Probe(source, tag, comm, &st);
+      f = 1;
+    } else {
+      rc = next.MPI_Iprobe(source, tag, comm, &f, &st);
+    }
+    if (rc != MPI_SUCCESS) return rc;
+    if (f) {
+      int n = 0;
+      MPI_Get_count(&st, MPI_BYTE, &n);
+      if (!descriptor_sized(n)) {
+        if (status != MPI_STATUS_IGNORE) *status = st;
+        if (flag) *flag = 1;
+        return MPI_SUCCESS;
+      }
+      // The earliest message from that source with that tag is the one just
+      // probed (the library keeps one sender's messages in order, and any
+      // earlier one would have matched the probe first): take it out to look
+      // at it, and keep it for the receive that will match it.
+      MPI_Message m = MPI_MESSAGE_NULL;
+      int g = 0;
+      MPI_Status st2;
+      next.MPI_Improbe(st.MPI_SOURCE, st.MPI_TAG, comm, &g, &m, &st2);
+      if (!g) LOG_FATAL("a probed message could not be matched");
+      probed.push_back(receive_probed(&m, n, comm));
+      continue;
+    }
+    if (flag) {
+      *flag = 0;
+      return MPI_SUCCESS;
+    }
+    progress();
+  }
+}
+
+int mprobe(int source, int tag, MPI_Comm comm, int *flag, MPI_Message *msg, MPI_Status *status) {
+  if (source == MPI_PROC_NULL || !state.active)
+    return flag ? next.MPI_Improbe(source, tag, comm, flag, msg, status) : next.MPI_Mprobe(source, tag, comm, msg, status);
+  if (flag && busy()) progress(false);
+  auto claim = [&](std::unique_ptr<Probed> p) { // a TEMPI message handle, outside the library's handle space
+    report(*p, status);
+    while (probedMsgs.count(nextMsgHandle) || nextMsgHandle == 0) nextMsgHandle = (nextMsgHandle + 1) % kHandleSpace;
+    const uint32_t h = nextMsgHandle;
+    nextMsgHandle = (nextMsgHandle + 1) % kHandleSpace;
+    probedMsgs.emplace(h, std::move(p));
+    *msg = MPI_Message(h);
+    if (flag) *flag = 1;
+    return MPI_SUCCESS;
+  };
+  for (;;) {
+    if (std::unique_ptr<Probed> p = take_probed(source, tag, comm)) return claim(std::move(p));
+    int f = 0;
+    MPI_Status st;
+    MPI_Message m = MPI_MESSAGE_NULL;
+    int rc;
+    if (!flag && !busy()) {
+      rc = next.MPI_Mprobe(source, tag, comm, &m, &st);
+      f = 1;
+    } else {
+      rc = next.MPI_Improbe(source, tag, comm, &f, &m, &st);
+    }
+    if (rc != MPI_SUCCESS) return rc;
+    if (f) {
+      int n = 0;
+      MPI_Get_count(&st, MPI_BYTE, &n);
+      if (!descriptor_sized(n)) { // the library's message, as it is
+        *msg = m;
+        if (status != MPI_STATUS_IGNORE) *status = st;
+        if (flag) *flag = 1;
+        return MPI_SUCCESS;
+      }
+      return claim(receive_probed(&m, n, comm));
+    }
+    if (flag) {
+      *flag = 0;
+      return MPI_SUCCESS;
+    }
+    progress();
+  }
+}
+
+int imrecv(void *buf, int count, MPI_Datatype dt, MPI_Message *msg, MPI_Request *req) {
+  Route route;
+  auto it = probedMsgs.find(uint32_t(*msg));
+  if (it == probedMsgs.end()) { // the library's message
+    if (*msg == MPI_MESSAGE_NULL || *msg == MPI_MESSAGE_NO_PROC || !handles(buf, count, dt, 0, &route))
+      return next.MPI_Imrecv(buf, count, dt, msg, req);
+    counters.irecvs++;
+    if (!route.rec->packer) {
+      *req = add(std::make_unique<LibIrecvOp>(buf, count, dt, MPI_ANY_SOURCE, MPI_ANY_TAG, MPI_COMM_WORLD, msg));
+    } else {
+      const int64_t bytes = packed_bytes(route.rec, count, dt, MPI_COMM_WORLD);
+      char *origin = static_cast<char *>(route.ptr.dptr) - route.rec->desc.start;
+      *req = add(std::make_unique<IrecvOp>(route.rec, origin, count, dt, MPI_ANY_SOURCE, MPI_ANY_TAG,
+                                           MPI_COMM_WORLD, route.ptr.device, bytes, msg));
+    }
+    *msg = MPI_MESSAGE_NULL;
+    return MPI_SUCCESS;
+  }
+  std::unique_ptr<Probed> p = std::move(it->second);
+  probedMsgs.erase(it);
+  *msg = MPI_MESSAGE_NULL;
+  const MPI_Comm comm = p->comm;
+  if (!handles(buf, count, dt, 0, &route)) {
+    *req = add(std::make_unique<HostIrecvOp>(buf, count, dt, MPI_ANY_SOURCE, MPI_ANY_TAG, comm, std::move(p)));
+    return MPI_SUCCESS;
+  }
+  counters.irecvs++;
+  if (!route.rec->packer) {
+    *req = add(std::make_unique<LibIrecvOp>(buf, count, dt, MPI_ANY_SOURCE, MPI_ANY_TAG, comm, nullptr, std::move(p)));
+    return MPI_SUCCESS;
+  }
+  const int64_t bytes = packed_bytes(route.rec, count, dt, comm);
+  char *origin = static_cast<char *>(route.ptr.dptr) - route.rec->desc.start;
+  *req = add(std::make_unique<IrecvOp>(route.rec, origin, count, dt, MPI_ANY_SOURCE, MPI_ANY_TAG, comm,
+                                       route.ptr.device, bytes, nullptr, std::move(p)));
+  return MPI_SUCCESS;
+}
+
+int mrecv(void *buf, int count, MPI_Datatype dt, MPI_Message *msg, MPI_Status *status) {
+  Route route;
+  if (!probedMsgs.count(uint32_t(*msg)) && !handles(buf, count, dt, 0, &route))
+    return next.MPI_Mrecv(buf, count, dt, msg, status); // the library's message into host memory
+  MPI_Request r = MPI_REQUEST_NULL;
+  const int rc = imrecv(buf, count, dt, msg, &r);
+  if (rc != MPI_SUCCESS) return rc;
+  return is_tempi_request(r) ? wait(&r, status) : next.MPI_Wait(&r, status);
 }
 
 } // namespace p2p

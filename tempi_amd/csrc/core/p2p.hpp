@@ -32,8 +32,9 @@
 //            here with LOG_FATAL: SURVEY F10)
 // Receives are adaptive: a TEMPI device receive lands in pinned host memory
 // and recognises an IPC descriptor by size + 16-byte magic, so it works with
-// any sender method. An IPC send needs a TEMPI receive on the other side
-// (device buffer, or a blocking MPI_Recv of any buffer).
+// any sender method. Host receives (MPI_Recv, MPI_Irecv, MPI_Sendrecv, the
+// collectives' host blocks) and the probe family recognise descriptors too,
+// so an application never sees one.
 #pragma once
 
 #include "gpu.hpp"
@@ -120,6 +121,31 @@ int test(MPI_Request *req, int *flag, MPI_Status *status);
 // blocking MPI_Recv into a host buffer that may receive an IPC descriptor
 int recv_host_ipc_aware(void *buf, int count, MPI_Datatype dt, int source, int tag, MPI_Comm comm,
                         MPI_Status *status, bool *handled);
+
+// ----------------------------------------------------- descriptor-aware receives
+// A TEMPI device send to a co-located rank may travel as a descriptor (IPC
+// slab, IPC COPY, DIRECT) instead of its bytes. Every receive an application
+// can post must therefore see the payload, as it would with the reference's
+// senders, which always send MPI_PACKED bytes (/root/reference/src/internal/
+// sender.cpp:109,161, async_operation.cpp:127,261).
+//
+// true when a host-buffer receive from `source` could meet a descriptor
+// (TEMPI active with a GPU, and the source is this node or MPI_ANY_SOURCE)
+bool host_recv_aware(int source, MPI_Comm comm);
+// MPI_Irecv into host memory that recognises a descriptor and lands its bytes
+int irecv_host(void *buf, int count, MPI_Datatype dt, int source, int tag, MPI_Comm comm, MPI_Request *req);
+// MPI_Probe (flag == nullptr) / MPI_Iprobe: a descriptor is reported with its
+// payload size (MPI_Get_count works on the status). To look at a message of a
+// descriptor's size the probe must receive it; it is then kept, still
+// matchable, and the next receive or probe that matches takes it from there.
+int probe(int source, int tag, MPI_Comm comm, int *flag, MPI_Status *status);
+// MPI_Mprobe (flag == nullptr) / MPI_Improbe: a descriptor becomes a TEMPI
+// message handle (outside the library's handle space), the rest stay the
+// library's
+int mprobe(int source, int tag, MPI_Comm comm, int *flag, MPI_Message *msg, MPI_Status *status);
+// MPI_Mrecv / MPI_Imrecv of either kind of message into host or device memory
+int mrecv(void *buf, int count, MPI_Datatype dt, MPI_Message *msg, MPI_Status *status);
+int imrecv(void *buf, int count, MPI_Datatype dt, MPI_Message *msg, MPI_Request *req);
 
 } // namespace p2p
 } // namespace tempi
