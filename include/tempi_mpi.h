@@ -40,6 +40,9 @@
  *                                                    with its payload size and received
  *                                                    as its payload, into host or device
  *                                                    memory
+ *   MPI_Barrier      (not interposed)                keeps TEMPI operations moving
+ *                                                    while it waits (a peer may need
+ *                                                    this rank's progress)
  *   MPI_Alltoallv    src/alltoallv.cpp:14-68         device-buffer alltoallv
  *   MPI_Neighbor_alltoallw  src/neighbor_alltoallw.cpp:11-18 (-> internal/
  *                    neighbor_alltoallw.cpp:19-77)   per-edge Isend/Irecv when
@@ -106,6 +109,7 @@ int MPI_Mprobe(int source, int tag, MPI_Comm comm, MPI_Message *message, MPI_Sta
 int MPI_Improbe(int source, int tag, MPI_Comm comm, int *flag, MPI_Message *message, MPI_Status *status);
 int MPI_Mrecv(void *buf, int count, MPI_Datatype datatype, MPI_Message *message, MPI_Status *status);
 int MPI_Imrecv(void *buf, int count, MPI_Datatype datatype, MPI_Message *message, MPI_Request *request);
+int MPI_Barrier(MPI_Comm comm);
 int MPI_Alltoallv(const void *sendbuf, const int sendcounts[], const int sdispls[],
                   MPI_Datatype sendtype, void *recvbuf, const int recvcounts[], const int rdispls[],
                   MPI_Datatype recvtype, MPI_Comm comm);

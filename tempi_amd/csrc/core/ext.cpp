@@ -102,7 +102,8 @@ TEMPI_EXPORT int64_t tempi_mpi_constant(const char *name, int *found) {
       H(MPI_THREAD_FUNNELED), H(MPI_THREAD_SERIALIZED), H(MPI_THREAD_MULTIPLE),
       H(MPI_MAX_PROCESSOR_NAME), H(MPI_UNDEFINED),
       P(MPI_STATUS_IGNORE), P(MPI_STATUSES_IGNORE), P(MPI_IN_PLACE), P(MPI_UNWEIGHTED), H(MPI_INFO_NULL),
-      H(MPI_ERRORS_RETURN), H(MPI_ERRORS_ARE_FATAL),
+      H(MPI_ERRORS_RETURN), H(MPI_ERRORS_ARE_FATAL), H(MPI_MESSAGE_NULL), H(MPI_MESSAGE_NO_PROC),
+      {"sizeof(MPI_Message)", int64_t(sizeof(MPI_Message))},
       {"sizeof(MPI_Status)", int64_t(sizeof(MPI_Status))},
       {"sizeof(MPI_Aint)", int64_t(sizeof(MPI_Aint))},
       {"sizeof(MPI_Datatype)", int64_t(sizeof(MPI_Datatype))},

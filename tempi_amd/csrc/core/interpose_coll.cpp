@@ -116,7 +116,7 @@ int isir(const void *sendbuf, const int *scounts, const int *sdispls, MPI_Dataty
       p2p::Route route;
       if (p2p::handles(b, rcounts[p], rtype, p, &route))
         p2p::irecv(b, rcounts[p], rtype, p, tag, comm, &r, route);
-      else if (p2p::host_recv_aware(p, comm)) // a host block a peer's device send may reach as a descriptor
+      else if (p2p::host_recv_aware(p, tag, comm)) // a host block a peer's device send may reach as a descriptor
         p2p::irecv_host(b, rcounts[p], rtype, p, tag, comm, &r);
       else
         next.MPI_Irecv(b, rcounts[p], rtype, p, tag, comm, &r);
@@ -227,4 +227,25 @@ TEMPI_EXPORT int MPI_Alltoallv(const void *sendbuf, const int sendcounts[], cons
     break;
   }
   return rc;
+}
+
+// MPI_Barrier: not interposed by the reference. A rank blocked in the
+// library's barrier makes no TEMPI progress, and a peer may be waiting on it:
+// for the bytes of an IPC message it could not map (the NACK re-send), for an
+// ack that frees a slab. While TEMPI has operations in flight the barrier is
+// an MPI_Ibarrier completed under TEMPI's progress loop -- on every rank
+// whenever TEMPI is active, since a blocking and a non-blocking barrier do
+// not match each other (whether a rank is busy is its own business).
+TEMPI_EXPORT int MPI_Barrier(MPI_Comm comm) {
+  resolve_next();
+  if (!state.active) return next.MPI_Barrier(comm);
+  MPI_Request r = MPI_REQUEST_NULL;
+  int rc = MPI_Ibarrier(comm, &r);
+  if (rc != MPI_SUCCESS) return rc;
+  for (;;) {
+    int flag = 0;
+    rc = next.MPI_Test(&r, &flag, MPI_STATUS_IGNORE);
+    if (rc != MPI_SUCCESS || flag) return rc;
+    if (p2p::busy()) p2p::progress();
+  }
 }

@@ -75,7 +75,7 @@ TEMPI_EXPORT int MPI_Irecv(void *buf, int count, MPI_Datatype datatype, int sour
     return p2p::irecv(buf, count, datatype, source, tag, comm, request, route);
   if (state.active) p2p::progress(false);
   // a host buffer: a co-located TEMPI device send may arrive as a descriptor
-  if (p2p::host_recv_aware(source, comm)) return p2p::irecv_host(buf, count, datatype, source, tag, comm, request);
+  if (p2p::host_recv_aware(source, tag, comm)) return p2p::irecv_host(buf, count, datatype, source, tag, comm, request);
   counters.lib_recvs++;
   return next.MPI_Irecv(buf, count, datatype, source, tag, comm, request);
 }
@@ -291,7 +291,7 @@ TEMPI_EXPORT int MPI_Sendrecv(const void *sendbuf, int sendcount, MPI_Datatype s
   // could meet a descriptor
   const bool mine = state.active && (p2p::handles(sendbuf, sendcount, sendtype, dest, &sr) ||
                                      p2p::handles(recvbuf, recvcount, recvtype, source, &rr) ||
-                                     p2p::host_recv_aware(source, comm));
+                                     p2p::host_recv_aware(source, recvtag, comm));
   if (!mine) {
     if (state.active && p2p::send_gated(comm, dest)) p2p::drain_sends(comm, dest); // keep send order
     return next.MPI_Sendrecv(sendbuf, sendcount, sendtype, dest, sendtag, recvbuf, recvcount, recvtype, source,

@@ -41,6 +41,7 @@
   X(MPI_Improbe)                                                               \
   X(MPI_Mrecv)                                                                 \
   X(MPI_Imrecv)                                                                \
+  X(MPI_Barrier)                                                               \
   X(MPI_Alltoallv)                                                             \
   X(MPI_Neighbor_alltoallv)                                                    \
   X(MPI_Neighbor_alltoallw)                                                    \

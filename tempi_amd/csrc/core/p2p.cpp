@@ -115,6 +115,7 @@ std::unordered_map<uint64_t, std::shared_ptr<DirectShared>> directShared; // sen
 uint64_t nextDirectToken = 1;
 bool directEnabled = true;
 bool ipcSystemLoads = true; // TEMPI_IPC_PLAIN_LOADS=1 turns off TEMPI_HIP_ITEM_REMOTE (A/B only)
+bool hostRecvAware = true;  // TEMPI_NO_HOST_RECV=1: host receives go straight to the library (A/B only)
 
 MPI_Comm ctrlComm = MPI_COMM_NULL; // private duplicate of MPI_COMM_WORLD for acks
 int tagUb = 32767;
@@ -1097,6 +1098,7 @@ struct IrecvOp : Op {
       next.MPI_Test(&lib, &flag, &st);
       if (flag) {
         lib = MPI_REQUEST_NULL;
+        st.MPI_ERROR = MPI_SUCCESS; // (MPI_Test leaves it unset)
         lib_done(st);
       }
     }
@@ -1549,6 +1551,7 @@ void init() {
   gpuAwareLibrary = std::getenv("TEMPI_MPI_GPU_AWARE") != nullptr;
   directEnabled = std::getenv("TEMPI_NO_DIRECT") == nullptr;
   ipcSystemLoads = std::getenv("TEMPI_IPC_PLAIN_LOADS") == nullptr;
+  hostRecvAware = std::getenv("TEMPI_NO_HOST_RECV") == nullptr;
   ipcCopyEnabled = std::getenv("TEMPI_NO_IPC_COPY") == nullptr;
   collCopyEnabled = std::getenv("TEMPI_NO_COLL_COPY") == nullptr;
   if (const char *s = std::getenv("TEMPI_IPC_COPY_MIN_BYTES")) ipcCopyMinBytes = std::atoll(s);
@@ -2007,9 +2010,11 @@ int recv_host_ipc_aware(void *buf, int count, MPI_Datatype dt, int source, int t
   return land(raw, n, st);
 }
 
-bool host_recv_aware(int source, MPI_Comm comm) {
+bool host_recv_aware(int source, int tag, MPI_Comm comm) {
   if (!state.active || !gpu::available() || source == MPI_PROC_NULL) return false;
-  if (std::getenv("TEMPI_NO_HOST_RECV") != nullptr) return false; // A/B only: host receives straight to the library
+  for (const auto &p : probed) // a probe holds a message it may match
+    if (probed_matches(*p, source, tag, comm)) return true;
+  if (!hostRecvAware) return false; // TEMPI_NO_HOST_RECV (A/B only): host receives straight to the library
   return source == MPI_ANY_SOURCE || topology::colocated(comm, source);
 }
 
@@ -2043,7 +2048,7 @@ void report(const Probed &p, MPI_Status *status) {
 } // namespace
 
 int probe(int source, int tag, MPI_Comm comm, int *flag, MPI_Status *status) {
-  if (source == MPI_PROC_NULL || !state.active)
+  if (source == MPI_PROC_NULL || !state.active || !gpu::available()) // no descriptors can arrive
     return flag ? next.MPI_Iprobe(source, tag, comm, flag, status) : next.MPI_Probe(source, tag, comm, status);
   if (flag && busy()) progress(false);
   for (;;) {
@@ -2092,7 +2097,7 @@ int probe(int source, int tag, MPI_Comm comm, int *flag, MPI_Status *status) {
 }
 
 int mprobe(int source, int tag, MPI_Comm comm, int *flag, MPI_Message *msg, MPI_Status *status) {
-  if (source == MPI_PROC_NULL || !state.active)
+  if (source == MPI_PROC_NULL || !state.active || !gpu::available()) // no descriptors can arrive
     return flag ? next.MPI_Improbe(source, tag, comm, flag, msg, status) : next.MPI_Mprobe(source, tag, comm, msg, status);
   if (flag && busy()) progress(false);
   auto claim = [&](std::unique_ptr<Probed> p) { // a TEMPI message handle, outside the library's handle space

@@ -130,8 +130,9 @@ int recv_host_ipc_aware(void *buf, int count, MPI_Datatype dt, int source, int t
 // sender.cpp:109,161, async_operation.cpp:127,261).
 //
 // true when a host-buffer receive from `source` could meet a descriptor
-// (TEMPI active with a GPU, and the source is this node or MPI_ANY_SOURCE)
-bool host_recv_aware(int source, MPI_Comm comm);
+// (TEMPI active with a GPU, and the source is this node or MPI_ANY_SOURCE),
+// or a message a probe is holding
+bool host_recv_aware(int source, int tag, MPI_Comm comm);
 // MPI_Irecv into host memory that recognises a descriptor and lands its bytes
 int irecv_host(void *buf, int count, MPI_Datatype dt, int source, int tag, MPI_Comm comm, MPI_Request *req);
 // MPI_Probe (flag == nullptr) / MPI_Iprobe: a descriptor is reported with its

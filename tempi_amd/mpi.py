@@ -71,7 +71,7 @@ class MPI:
         for n in ("BYTE", "CHAR", "SHORT", "INT", "LONG", "FLOAT", "DOUBLE", "PACKED", "INT64_T",
                   "UINT8_T", "COMM_WORLD", "COMM_SELF", "REQUEST_NULL", "ORDER_C", "ORDER_FORTRAN",
                   "SUCCESS", "ERR_TRUNCATE", "ANY_SOURCE", "ANY_TAG", "SUM", "MAX", "MIN",
-                  "DATATYPE_NULL", "PROC_NULL", "UNDEFINED"):
+                  "DATATYPE_NULL", "PROC_NULL", "UNDEFINED", "ERRORS_RETURN", "ERRORS_ARE_FATAL"):
             setattr(self, n, self.const("MPI_" + n))
         self.STATUS_IGNORE = ctypes.c_void_p(self.const("MPI_STATUS_IGNORE"))
         self.STATUSES_IGNORE = ctypes.c_void_p(self.const("MPI_STATUSES_IGNORE"))
@@ -362,6 +362,58 @@ class MPI:
         flag = ctypes.c_int(0)
         self._call("MPI_Test", ctypes.byref(r), ctypes.byref(flag), self.STATUS_IGNORE)
         return bool(flag.value), r.value
+
+    # ------------------------------------------------ probes / matched receives
+    def Comm_set_errhandler(self, errhandler, comm=None):
+        self._call("MPI_Comm_set_errhandler", self.h(self.COMM_WORLD if comm is None else comm), self.h(errhandler))
+
+    def Probe(self, source, tag, t, comm=None):
+        """MPI_Probe: (source, tag, count of t)"""
+        st = self._status()
+        self._call("MPI_Probe", source, tag, self.h(self.COMM_WORLD if comm is None else comm), st)
+        return self._decode(st, t)
+
+    def Iprobe(self, source, tag, t, comm=None):
+        """MPI_Iprobe: None, or (source, tag, count of t)"""
+        st, flag = self._status(), ctypes.c_int(0)
+        self._call("MPI_Iprobe", source, tag, self.h(self.COMM_WORLD if comm is None else comm), ctypes.byref(flag),
+                   st)
+        return self._decode(st, t) if flag.value else None
+
+    def Mprobe(self, source, tag, t, comm=None):
+        """MPI_Mprobe: (message, (source, tag, count of t))"""
+        st, m = self._status(), self.Handle()
+        self._call("MPI_Mprobe", source, tag, self.h(self.COMM_WORLD if comm is None else comm), ctypes.byref(m), st)
+        return m.value, self._decode(st, t)
+
+    def Improbe(self, source, tag, t, comm=None):
+        """MPI_Improbe: None, or (message, (source, tag, count of t))"""
+        st, m, flag = self._status(), self.Handle(), ctypes.c_int(0)
+        self._call("MPI_Improbe", source, tag, self.h(self.COMM_WORLD if comm is None else comm), ctypes.byref(flag),
+                   ctypes.byref(m), st)
+        return (m.value, self._decode(st, t)) if flag.value else None
+
+    def Mrecv(self, buf, count, t, message):
+        """MPI_Mrecv: (source, tag, count of t)"""
+        st, m = self._status(), self.Handle(message)
+        self._call("MPI_Mrecv", ctypes.c_void_p(buf), count, self.h(t), ctypes.byref(m), st)
+        return self._decode(st, t)
+
+    def Imrecv(self, buf, count, t, message):
+        r, m = self.Request(), self.Handle(message)
+        self._call("MPI_Imrecv", ctypes.c_void_p(buf), count, self.h(t), ctypes.byref(m), ctypes.byref(r))
+        return r.value
+
+    def Wait_rc(self, req):
+        """MPI_Wait without raising: (rc, MPI_ERROR of the status)"""
+        r, st = self.Request(req), self._status()
+        rc = self.L.MPI_Wait(ctypes.byref(r), st)
+        return rc, ctypes.c_int.from_buffer(st, self.const("offsetof(MPI_Status,MPI_ERROR)")).value
+
+    def Recv_rc(self, buf, count, t, source, tag, comm=None):
+        """MPI_Recv without raising: rc"""
+        return self.L.MPI_Recv(ctypes.c_void_p(buf), count, self.h(t), source, tag,
+                               self.h(self.COMM_WORLD if comm is None else comm), self.STATUS_IGNORE)
 
     def Alltoallv(self, sbuf, scounts, sdispls, stype, rbuf, rcounts, rdispls, rtype, comm=None):
         n = len(scounts)

@@ -1,7 +1,12 @@
 """Run under mpiexec: MPI_Alltoallv through libtempi.so with a random sparse
 byte-count matrix (the shape of SquareMat::make_random_sparse,
 /root/reference/support/squaremat.cpp:52-75), verifying every received byte.
-Args: [--device] [--scale S] [--nnz K] [--type byte|vec]"""
+Args: [--device] [--scale S] [--nnz K] [--mixed alt|hostrank]
+--mixed (with --device) puts some blocks in host memory: alt = even ranks
+send from the GPU and receive into the host, odd ranks the reverse;
+hostrank = rank 0's buffers are all on the host. The ranks then disagree on
+where their memory is, and must still meet (one route on every
+rank, descriptor-aware host receives)."""
 import os
 import sys
 
@@ -15,6 +20,7 @@ args = sys.argv[1:]
 device = "--device" in args
 scale = int(args[args.index("--scale") + 1]) if "--scale" in args else 1000
 nnz = int(args[args.index("--nnz") + 1]) if "--nnz" in args else 2
+mixed = args[args.index("--mixed") + 1] if "--mixed" in args else None
 mpi = tempi_amd.get_mpi()
 if device:
     import torch
@@ -53,16 +59,22 @@ expected = recv.copy()
 for s in range(n):
     expected[rdispl[s]:rdispl[s] + rcounts[s]] = payload(s, rank, rcounts[s])
 
-if device:
+send_dev = recv_dev = device
+if mixed == "alt":
+    send_dev, recv_dev = rank % 2 == 0, rank % 2 == 1
+elif mixed == "hostrank":
+    send_dev = recv_dev = rank != 0
+if send_dev:
     dsend = torch.from_numpy(send).cuda()
+if recv_dev:
     drecv = torch.from_numpy(recv).cuda()
+if device:
     torch.cuda.synchronize()
-    sp, rp = dsend.data_ptr(), drecv.data_ptr()
-else:
-    sp, rp = send.ctypes.data, recv.ctypes.data
+sp = dsend.data_ptr() if send_dev else send.ctypes.data
+rp = drecv.data_ptr() if recv_dev else recv.ctypes.data
 for it in range(3):
     mpi.Alltoallv(sp, scounts, sdispl, mpi.BYTE, rp, rcounts, rdispl, mpi.BYTE)
-got = drecv.cpu().numpy() if device else recv
+got = drecv.cpu().numpy() if recv_dev else recv
 errors = int((got != expected).sum())
 total = mpi.Allreduce_double(float(errors), op=mpi.SUM)
 if rank == 0:

@@ -87,6 +87,34 @@ def test_alltoallv_device(gpu, method, ranks, scale, nnz):
     assert rc == 0 and "RESULT errors=0" in out, out[-3000:]
 
 
+@pytest.mark.parametrize("mixed", ["alt", "hostrank"])
+@pytest.mark.parametrize("ranks,scale", [(2, 100000), (3, 1000), (4, 10)])
+def test_alltoallv_mixed_host_device(gpu, mixed, ranks, scale):
+    """ranks whose blocks are in different memories (host / device) still
+    meet: every rank takes TEMPI's route, host receives land descriptors"""
+    rc, out = mpi_launch.run(ranks, mpi_launch.py("alltoallv.py", "--device", "--scale", str(scale), "--nnz", "3",
+                                                  "--mixed", mixed), timeout=240)
+    assert rc == 0 and "RESULT errors=0" in out, out[-3000:]
+
+
+@pytest.mark.parametrize("n,method", [(2, "AUTO"), (1, "AUTO"), (2, "XCOPY"), (2, "IPC"), (2, "ONESHOT"),
+                                      (2, "STAGED"), (1, "NO_DIRECT"), (2, "IPC_FAULT")])
+def test_every_receive_sees_payload(gpu, n, method):
+    """a device strided send (ONESHOT / IPC slab / IPC COPY / DIRECT) received
+    by host MPI_Irecv, MPI_Probe + MPI_Recv, MPI_Iprobe, MPI_Mprobe + MPI_Mrecv
+    (host and device), MPI_Improbe + MPI_Imrecv, MPI_Sendrecv: payload bytes
+    and counts exact; then MPI_ERR_TRUNCATE from every receive kind"""
+    env = dict(METHODS.get(method, {}))
+    if method == "NO_DIRECT":
+        env["TEMPI_NO_DIRECT"] = "1"
+    rc, out = mpi_launch.run(n, mpi_launch.py("anyrecv.py"), env=env, timeout=240)
+    assert rc == 0 and "RESULT errors=0" in out, out[-4000:]
+    if n == 2 and method == "AUTO":  # the routes the cases are named for were taken
+        line = next(l for l in out.splitlines() if l.startswith("rank 0 counters"))
+        c = dict(kv.split("=") for kv in line.split()[3:])
+        assert int(c["ipc"]) > 0 and int(c["ipc_copy"]) > 0 and int(c["oneshot"]) > 0, line
+
+
 @pytest.mark.parametrize("ranks,env", [(1, {}), (2, {}), (3, {}), (4, {}), (2, {"TEMPI_DATATYPE_ONESHOT": "1"}),
                                        (3, {"TEMPI_NO_DIRECT": "1"})])
 def test_neighbor_collectives_device(gpu, ranks, env):
