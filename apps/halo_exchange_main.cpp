@@ -21,6 +21,8 @@ int main(int argc, char **argv) {
   for (int i = 1; i < argc; ++i) {
     if (!std::strcmp(argv[i], "--check"))
       check = 1;
+    else if (!std::strcmp(argv[i], "--check-control")) // a planted error the check must find
+      check = 2;
     else if (!std::strcmp(argv[i], "--neighbor"))
       neighbor = 1;
     else if (!std::strcmp(argv[i], "--quants") && i + 1 < argc)

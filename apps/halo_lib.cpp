@@ -89,6 +89,32 @@ __global__ void fill_kernel(uint64_t *buf, size_t pitchWords, int ysize, I3 lcr,
   }
 }
 
+// --check on the GPU: every cell of the padded block (interior and all 26 halo
+// regions, with periodic wrap) against the owner's value; one mismatch count
+// per workgroup, summed on the host
+constexpr int kCheckBlock = 256, kCheckGrid = 2048;
+__global__ void __launch_bounds__(kCheckBlock) check_kernel(const uint64_t *buf, size_t pitchWords, int ysize,
+                                                            int zsize, int xsize, I3 origin, I3 global, int r, int q,
+                                                            unsigned long long *blockErrors) {
+  const int64_t n = int64_t(xsize) * ysize * zsize;
+  unsigned long long bad = 0;
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+    const int x = int(i % xsize), y = int((i / xsize) % ysize), z = int(i / (int64_t(xsize) * ysize));
+    const int64_t gx = (origin.x + x - r + global.x) % global.x;
+    const int64_t gy = (origin.y + y - r + global.y) % global.y;
+    const int64_t gz = (origin.z + z - r + global.z) % global.z;
+    bad += buf[(size_t(z) * ysize + size_t(y)) * pitchWords + size_t(x)] != cell_value(gx, gy, gz, q);
+  }
+  __shared__ unsigned long long part[kCheckBlock];
+  part[threadIdx.x] = bad;
+  __syncthreads();
+  for (int s = kCheckBlock / 2; s > 0; s >>= 1) {
+    if (int(threadIdx.x) < s) part[threadIdx.x] += part[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) blockErrors[blockIdx.x] = part[0];
+}
+
 // TEMPI's own entry points, when the interposer is linked (weak: the app runs
 // unchanged on a plain MPI)
 extern "C" __attribute__((weak)) void tempi_reset_counters(void);
@@ -268,26 +294,20 @@ tempi_bench_halo(int nIters, int gx, int gy, int gz, int nQuants, int radius, in
 
   long long errors = 0;
   if (check) {
-    std::vector<uint64_t> h(static_cast<size_t>(bufBytes / 8));
+    // check == 2: a negative control -- one planted wrong cell (rank 0,
+    // quantity 0, the halo corner at (0, 0, 0)) must be counted
+    if (check == 2 && rank == 0) HIPCHECK(hipMemset(bufs[0], 0x5A, 8));
+    unsigned long long *dErr = nullptr;
+    HIPCHECK(hipMalloc(&dErr, sizeof(unsigned long long) * kCheckGrid));
+    std::vector<unsigned long long> hErr(kCheckGrid);
     for (int qi = 0; qi < nQuants; ++qi) {
-      HIPCHECK(hipMemcpy(h.data(), bufs[size_t(qi)], bufBytes, hipMemcpyDeviceToHost));
-      for (int z = 0; z < zsize; ++z)
-        for (int y = 0; y < ysize; ++y)
-          for (int x = 0; x < lcr.x + 2 * radius; ++x) {
-            const bool inX = x >= radius && x < radius + lcr.x, inY = y >= radius && y < radius + lcr.y,
-                       inZ = z >= radius && z < radius + lcr.z;
-            // every cell (interior and all 26 halo regions) must hold the
-            // owner's value; only the 8 "edges of edges" are all set too
-            const int64_t gx = (origin.x + x - radius + global.x) % global.x;
-            const int64_t gy = (origin.y + y - radius + global.y) % global.y;
-            const int64_t gz = (origin.z + z - radius + global.z) % global.z;
-            (void)inX;
-            (void)inY;
-            (void)inZ;
-            const uint64_t got = h[(size_t(z) * ysize + size_t(y)) * (pitch / 8) + size_t(x)];
-            if (got != cell_value(gx, gy, gz, qi)) ++errors;
-          }
+      hipLaunchKernelGGL(check_kernel, dim3(kCheckGrid), dim3(kCheckBlock), 0, 0,
+                         reinterpret_cast<const uint64_t *>(bufs[size_t(qi)]), pitch / 8, ysize, zsize,
+                         lcr.x + 2 * radius, origin, global, radius, qi, dErr);
+      HIPCHECK(hipMemcpy(hErr.data(), dErr, sizeof(unsigned long long) * kCheckGrid, hipMemcpyDeviceToHost));
+      for (unsigned long long e : hErr) errors += (long long)e;
     }
+    HIPCHECK(hipFree(dErr));
     MPI_Allreduce(MPI_IN_PLACE, &errors, 1, MPI_LONG_LONG, MPI_SUM, MPI_COMM_WORLD);
   }
 

@@ -43,6 +43,8 @@ typedef struct tempi_counters_t {
   uint64_t send_ipc_copy;  /* IPC sends the receiver copied out of the sender's object */
   uint64_t copy_resends;   /* IPC COPY sends answered through the host instead */
   uint64_t ipc_maps_replaced; /* peer mappings closed because the peer freed and replaced that allocation */
+  uint64_t canary_ok;   /* peers on another GPU whose mapped memory read back right at first contact */
+  uint64_t canary_fail; /* ... and those that did not (IPC with them off: host-staged transfers) */
 } tempi_counters_t;
 void tempi_get_counters(tempi_counters_t *out);
 void tempi_reset_counters(void);

@@ -23,6 +23,9 @@ struct Counters {
   uint64_t neighbor_colls = 0; // neighbourhood collectives on device buffers
   uint64_t send_ipc_copy = 0, copy_resends = 0; // IPC COPY sends; those answered through the host
   uint64_t ipc_maps_replaced = 0; // peer allocation mappings closed because the peer replaced them
+  // first contact with a peer on another GPU: its memory read back through
+  // the remote-load kernel agreed with a DMA read (ok) or did not (fail)
+  uint64_t canary_ok = 0, canary_fail = 0;
   // kernel time of synchronous MPI_Pack / MPI_Unpack while profiling is on
   double pack_kernel_ms = 0, unpack_kernel_ms = 0;
   uint64_t pack_timed = 0, unpack_timed = 0;

@@ -65,6 +65,8 @@ TEMPI_EXPORT void tempi_get_counters(tempi_counters_t *o) {
   o->send_ipc_copy = c.send_ipc_copy;
   o->copy_resends = c.copy_resends;
   o->ipc_maps_replaced = c.ipc_maps_replaced;
+  o->canary_ok = c.canary_ok;
+  o->canary_fail = c.canary_fail;
 }
 
 TEMPI_EXPORT void tempi_reset_counters(void) { counters = Counters(); }

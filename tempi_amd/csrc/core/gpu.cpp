@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <mutex>
+#include <unistd.h>
 #include <vector>
 
 namespace tempi {
@@ -63,6 +64,11 @@ uint32_t identity(int device) {
     tempi_hip_device_uuid(device, u);
     uint32_t h = 2166136261u;
     for (unsigned char c : u) h = (h ^ c) * 16777619u;
+    // TEMPI_FAKE_FOREIGN_GPU (tests): every process sees its GPU under an
+    // identity of its own, so peers sharing this box's GPU take the
+    // cross-GPU paths (system-scope loads, the first-contact canary)
+    static const bool fakeForeign = std::getenv("TEMPI_FAKE_FOREIGN_GPU") != nullptr;
+    if (fakeForeign) h = (h ^ uint32_t(getpid())) * 16777619u;
     ids[size_t(device)] = h ? h : 1;
   }
   return ids[size_t(device)];

@@ -276,6 +276,59 @@ void *peer_pointer(const IpcDesc &d) {
   return p;
 }
 
+// First contact with a peer on ANOTHER GPU. This pool's boxes have one GPU,
+// so the cross-GPU IPC path is first met on the driver's 8-GPU node: before
+// the transport trusts a mapping of that peer's memory, the first bytes a
+// descriptor names are read twice -- by the remote-load copy kernel the
+// receiver uses (TEMPI_HIP_ITEM_REMOTE, system-scope loads) and by a DMA copy
+// (hipMemcpy) -- and compared on the host. A failed read or a mismatch turns
+// IPC with that peer off: this message and every later one go through the
+// host (the NACK path). Once per peer; at most 64 KiB.
+std::vector<signed char> canaryVerdict; // per world rank: 0 untested, 1 passed, -1 failed
+bool faultCanary = false;               // TEMPI_FAULT_CANARY: the comparison fails (tests)
+
+bool canary(int world, const void *peerBytes, int64_t n, int device) {
+  if (world < 0) return true;
+  if (canaryVerdict.size() <= size_t(world)) canaryVerdict.resize(size_t(world) + 1, 0);
+  signed char &v = canaryVerdict[size_t(world)];
+  if (v) return v > 0;
+  n = std::min<int64_t>(n, 64 * 1024);
+  if (n <= 0) return true; // nothing to read yet: decide on a later message
+  int cur = 0;
+  tempi_hip_get_device(&cur);
+  if (cur != device) tempi_hip_set_device(device);
+  std::vector<unsigned char> viaKernel(size_t(n), 0), viaDma(size_t(n), 1);
+  void *scratch = nullptr;
+  bool ok = tempi_hip_malloc(&scratch, size_t(n)) == 0;
+  if (ok) {
+    tempi_hip_copy_item c{};
+    c.dst_first = scratch;
+    c.src_first = peerBytes;
+    c.dst.block = n;
+    c.dst.ndims = 0;
+    c.src = c.dst;
+    c.flags = TEMPI_HIP_ITEM_REMOTE;
+    void *s = gpu::stream(device);
+    ok = tempi_hip_copy_batch(&c, 1, s) == 0 && tempi_hip_stream_synchronize(s) == 0 &&
+         tempi_hip_memcpy(viaKernel.data(), scratch, size_t(n)) == 0 &&
+         tempi_hip_memcpy(viaDma.data(), peerBytes, size_t(n)) == 0;
+    tempi_hip_free(scratch);
+  }
+  if (cur != device) tempi_hip_set_device(cur);
+  if (ok && faultCanary) viaDma[0] ^= 0xFF;
+  ok = ok && viaKernel == viaDma;
+  v = ok ? 1 : -1;
+  if (ok) {
+    counters.canary_ok++;
+    LOG_DEBUG("canary: rank " << world << "'s GPU memory reads back right (" << n << " B)");
+  } else {
+    counters.canary_fail++;
+    LOG_WARN("canary: rank " << world << "'s GPU memory does not read back right through IPC");
+    mark_ipc_broken(world);
+  }
+  return ok;
+}
+
 // ack payload: 0 = pulled, release the slab; 1 = could not map it, send the
 // bytes through the host on (ctrlComm, ackTag)
 int ackCodes[3] = {0, 1, 2};
@@ -1196,6 +1249,9 @@ struct IrecvOp : Op {
       const bool local = xd.senderPid == int32_t(getpid());
       if (!local) recycle_alloc_maps();
       const char *src = (local && xd.device != device) ? nullptr : peer_object(xd);
+      if (src && !local && xd.gpu != gpu::identity(device) &&
+          !canary(xd.senderWorld, src, std::min(xd.desc.block, xd.bytes), device))
+        src = nullptr; // (the peer is now marked: the NACK below says so)
       tempi_hip_desc mine;
       if (src && elems * size == xd.bytes && rec->flat(elems, &mine) && copy_ok(mine, xd.desc)) {
         xcopy = true;
@@ -1232,7 +1288,10 @@ struct IrecvOp : Op {
         return truncate(d.bytes);
       }
       void *base = peer_pointer(d);
-      if (!base) { // cannot map the sender's slab: ask for the bytes via the host
+      if (base && d.senderPid != int32_t(getpid()) && d.gpu != gpu::identity(device) &&
+          !canary(d.senderWorld, static_cast<const char *>(base) + d.offset, d.bytes, device))
+        base = nullptr;
+      if (!base) { // cannot map (or trust) the sender's slab: ask for the bytes via the host
         ipc = false;
         fallback = true;
         next.MPI_Irecv(hslab->host, int(d.bytes), MPI_PACKED, d.senderWorld, d.ackTag, ctrlComm, &lib);
@@ -1552,6 +1611,8 @@ void init() {
   directEnabled = std::getenv("TEMPI_NO_DIRECT") == nullptr;
   ipcSystemLoads = std::getenv("TEMPI_IPC_PLAIN_LOADS") == nullptr;
   hostRecvAware = std::getenv("TEMPI_NO_HOST_RECV") == nullptr;
+  faultCanary = std::getenv("TEMPI_FAULT_CANARY") != nullptr;
+  canaryVerdict.clear();
   ipcCopyEnabled = std::getenv("TEMPI_NO_IPC_COPY") == nullptr;
   collCopyEnabled = std::getenv("TEMPI_NO_COLL_COPY") == nullptr;
   if (const char *s = std::getenv("TEMPI_IPC_COPY_MIN_BYTES")) ipcCopyMinBytes = std::atoll(s);

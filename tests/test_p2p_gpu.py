@@ -67,12 +67,39 @@ def test_pingpong_nd(gpu, method, total, block):
     (4, "64 64 16", {"TEMPI_IPC_COPY_MIN_BYTES": "1", "TEMPI_IPC_COPY_MIN_BLOCK": "1"}, []),
     (2, "40", {"TEMPI_IPC_COPY_MIN_BYTES": "1", "TEMPI_IPC_COPY_MIN_BLOCK": "1", "TEMPI_STREAMS": "3"}, []),
     (2, "40", {"TEMPI_IPC_COPY_MIN_BYTES": "1", "TEMPI_FAULT_IPC_OPEN": "1"}, []),
-    (4, "32", {"TEMPI_IPC_COPY_MIN_BYTES": "1", "TEMPI_IPC_COPY_MIN_BLOCK": "1"}, ["--neighbor"])])
+    (4, "32", {"TEMPI_IPC_COPY_MIN_BYTES": "1", "TEMPI_IPC_COPY_MIN_BLOCK": "1"}, ["--neighbor"]),
+    # 8 ranks on (2, 2, 2), the decomposition of the driver's 8-GPU node, with
+    # the stream lanes one rank per GPU gets (3)
+    (8, "64", {}, []), (8, "64", {}, ["--neighbor"]), (8, "64", {"TEMPI_STREAMS": "3"}, []),
+    (8, "48", {"TEMPI_STREAMS": "3"}, ["--neighbor"]),
+    (8, "64", {"TEMPI_IPC_COPY_MIN_BYTES": "1", "TEMPI_IPC_COPY_MIN_BLOCK": "1", "TEMPI_STREAMS": "3"}, []),
+    # every rank sees the GPU under an identity of its own: the cross-GPU
+    # paths (system-scope loads, first-contact canary) between ranks of one GPU
+    (4, "64 64 16", {"TEMPI_FAKE_FOREIGN_GPU": "1"}, []),
+    (8, "64", {"TEMPI_FAKE_FOREIGN_GPU": "1", "TEMPI_STREAMS": "3"}, []),
+    (2, "40", {"TEMPI_FAKE_FOREIGN_GPU": "1", "TEMPI_IPC_COPY_MIN_BYTES": "1", "TEMPI_IPC_COPY_MIN_BLOCK": "1"}, []),
+    (4, "64 64 16", {"TEMPI_FAKE_FOREIGN_GPU": "1", "TEMPI_FAULT_CANARY": "1"}, [])])
 def test_halo_exchange_content(gpu, ranks, grid, env, extra):
     rc, out = mpi_launch.run(ranks, [os.path.join(LIB, "halo_exchange"), "2"] + grid.split() + ["--quants", "2", "--check"] + extra,
                              env=env, timeout=300)
     r = _json_line(out)
     assert rc == 0 and r["checked"] and r["errors"] == 0, out[-3000:]
+
+
+def test_halo_exchange_512_full_check(gpu):
+    """config 4 at its full size, 1 rank, 8 quantities: every cell of every
+    quantity checked (on the GPU)"""
+    rc, out = mpi_launch.run(1, [os.path.join(LIB, "halo_exchange"), "2", "512", "--check"], timeout=240)
+    r = _json_line(out)
+    assert rc == 0 and r["checked"] and r["errors"] == 0 and r["lcr"] == [512, 512, 512], out[-3000:]
+
+
+def test_halo_check_finds_a_planted_error(gpu):
+    """negative control: the GPU check counts one corrupted halo cell"""
+    rc, out = mpi_launch.run(2, [os.path.join(LIB, "halo_exchange"), "1", "32", "--quants", "2", "--check-control"],
+                             timeout=120)
+    r = _json_line(out)
+    assert r["checked"] and r["errors"] == 1, out[-3000:]
 
 
 A2AV = {"AUTO": {}, "STAGED": {"TEMPI_ALLTOALLV_STAGED": "1"}, "ISIR_STAGED": {"TEMPI_ALLTOALLV_ISIR_STAGED": "1"},
@@ -115,6 +142,23 @@ def test_every_receive_sees_payload(gpu, n, method):
         assert int(c["ipc"]) > 0 and int(c["ipc_copy"]) > 0 and int(c["oneshot"]) > 0, line
 
 
+@pytest.mark.parametrize("fault", [False, True])
+@pytest.mark.parametrize("method", ["AUTO", "XCOPY"])
+def test_cross_gpu_first_contact_canary(gpu, method, fault):
+    """a peer that looks like another GPU (TEMPI_FAKE_FOREIGN_GPU) is read
+    through the remote-load kernel only after its first descriptor's bytes
+    read back the same through that kernel and through DMA; a mismatch
+    (TEMPI_FAULT_CANARY) turns IPC with it off and the bytes still arrive"""
+    env = dict(METHODS[method], TEMPI_FAKE_FOREIGN_GPU="1")
+    if fault:
+        env["TEMPI_FAULT_CANARY"] = "1"
+    rc, out = mpi_launch.run(2, mpi_launch.py("anyrecv.py"), env=env, timeout=240)
+    assert rc == 0 and "RESULT errors=0" in out, out[-4000:]
+    line = next(l for l in out.splitlines() if l.startswith("rank 1 counters"))
+    c = dict(kv.split("=") for kv in line.split()[3:])
+    assert (int(c["canary_ok"]), int(c["canary_fail"])) == ((0, 1) if fault else (1, 0)), line
+
+
 @pytest.mark.parametrize("ranks,env", [(1, {}), (2, {}), (3, {}), (4, {}), (2, {"TEMPI_DATATYPE_ONESHOT": "1"}),
                                        (3, {"TEMPI_NO_DIRECT": "1"})])
 def test_neighbor_collectives_device(gpu, ranks, env):
@@ -125,12 +169,18 @@ def test_neighbor_collectives_device(gpu, ranks, env):
     assert rc == 0 and "RESULT errors=0" in out, out[-3000:]
 
 
-@pytest.mark.parametrize("ranks,scale,density", [(2, 100000, 1.0), (3, 1000, 0.5), (4, 10, 1.0), (4, 100000, 0.25),
-                                                    (2, 1000000, 1.0), (3, 10000, 1.0)])
-def test_alltoallv_sparse_app(gpu, ranks, scale, density):
+@pytest.mark.parametrize("ranks,scale,density,env", [
+    (2, 100000, 1.0, {}), (3, 1000, 0.5, {}), (4, 10, 1.0, {}), (4, 100000, 0.25, {}), (2, 1000000, 1.0, {}),
+    (3, 10000, 1.0, {}),
+    # 8 ranks, config 5's own rank count: the reference's scales x densities
+    # (bench_alltoallv_random_sparse.cpp:140-222), and the 3 lanes of one rank per GPU
+    (8, 1, 1.0, {}), (8, 100, 0.5, {}), (8, 10000, 0.125, {}), (8, 100000, 0.05, {}), (8, 1000000, 0.25, {}),
+    (8, 10, 1.0, {"TEMPI_STREAMS": "3"}), (8, 100000, 0.5, {"TEMPI_STREAMS": "3"}),
+    (8, 1000000, 1.0, {"TEMPI_STREAMS": "3"})])
+def test_alltoallv_sparse_app(gpu, ranks, scale, density, env):
     """config 5 app: the reference's random sparse matrices, every byte checked"""
     rc, out = mpi_launch.run(ranks, [os.path.join(LIB, "alltoallv_sparse"), "3", "--scale", str(scale), "--density",
-                                     str(density), "--check"], timeout=240)
+                                     str(density), "--check"], env=env, timeout=240)
     r = _json_line(out)
     assert rc == 0 and r["checked"] and r["errors"] == 0, out[-3000:]
 

@@ -371,3 +371,113 @@ def test_batched_kernel_c_abi(mpi, gpu, seed, remote):
         exp = np.zeros_like(c["host"])
         c["tm"].unpack(c["tm"].pack(c["host"], c["origin"], c["count"]), exp, c["origin"], c["count"])
         assert np.array_equal(c["src"].cpu().numpy(), exp)
+
+
+def _slab_rounds(H, host_ptr, dev_ptr, obj, n_rows, rounds, seed):
+    """kernel writes the slab -> host reads it; host writes the reused slab ->
+    kernel reads it; `rounds` times, as the transport does it: kernels on a
+    non-blocking stream of TEMPI's kind, completion seen by polling an event
+    (no device-wide synchronisation between the host's write and the kernel
+    that reads). Returns (host-read mismatches, kernel-read mismatches) in
+    bytes."""
+    torch = _torch()
+    d = HipDesc()
+    d.block, d.ndims = 64, 1
+    d.counts[0], d.strides[0] = n_rows, 128
+    vp = ctypes.c_void_p
+    H.tempi_hip_pack.argtypes = [vp, vp, ctypes.POINTER(HipDesc), vp]
+    H.tempi_hip_unpack.argtypes = [vp, vp, ctypes.POINTER(HipDesc), vp]
+    H.tempi_hip_stream_create.argtypes = [ctypes.POINTER(vp)]
+    H.tempi_hip_stream_destroy.argtypes = [vp]
+    H.tempi_hip_stream_synchronize.argtypes = [vp]
+    H.tempi_hip_event_create.argtypes = [ctypes.POINTER(vp), ctypes.c_int]
+    H.tempi_hip_event_record.argtypes = [vp, vp]
+    H.tempi_hip_event_query.argtypes = [vp]
+    H.tempi_hip_event_destroy.argtypes = [vp]
+    s, ev = vp(), vp()
+    assert H.tempi_hip_stream_create(ctypes.byref(s)) == 0
+    assert H.tempi_hip_event_create(ctypes.byref(ev), 0) == 0
+
+    def run_and_poll():
+        assert H.tempi_hip_event_record(ev, s) == 0
+        while True:
+            q = H.tempi_hip_event_query(ev)
+            if q == 0:
+                return
+            assert q == 1, q
+
+    nbytes = n_rows * 64
+    slab = np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(host_ptr))
+    view = obj.view(n_rows, 128)[:, :64]
+    rng = np.random.default_rng(seed)
+    bad_host = bad_kernel = 0
+    try:
+        for _ in range(rounds):
+            obj.copy_(torch.from_numpy(rng.integers(0, 256, obj.numel(), dtype=np.uint8)).to(obj.device))
+            torch.cuda.synchronize()
+            # a kernel writes the slab (the sender's gather), the host reads it (the library sends it)
+            assert H.tempi_hip_pack(dev_ptr, obj.data_ptr(), ctypes.byref(d), s) == 0
+            run_and_poll()
+            bad_host += int((slab != view.reshape(-1).cpu().numpy()).sum())
+            # the host writes the reused slab (the library receives into it), a kernel reads it (the scatter)
+            new = rng.integers(0, 256, nbytes, dtype=np.uint8)
+            slab[:] = new
+            assert H.tempi_hip_unpack(obj.data_ptr(), dev_ptr, ctypes.byref(d), s) == 0
+            run_and_poll()
+            bad_kernel += int((view.reshape(-1).cpu().numpy() != new).sum())
+    finally:
+        H.tempi_hip_stream_synchronize(s)
+        H.tempi_hip_event_destroy(ev)
+        H.tempi_hip_stream_destroy(s)
+    return bad_host, bad_kernel
+
+
+def test_pinned_slab_reuse_ordering(gpu):
+    """The ordering behind round 1's host-route mismatch (commit d840279), run
+    deterministically: a pinned slab that a kernel wrote and the host read is
+    rewritten by the host -- not a HIP operation, so no HIP fence orders it
+    against lines the GPU kept from the slab's earlier use -- and then read by
+    a kernel, and reused, 64 times in one process. TEMPI's pinned slabs
+    (tempi_hip_host_alloc) are fine-grained, so the GPU keeps none of their
+    lines: every byte must arrive both ways."""
+    torch = _torch()
+    import tempi_amd
+
+    H = ctypes.CDLL(tempi_amd.LIBTEMPI_HIP)
+    H.tempi_hip_host_alloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p),
+                                       ctypes.c_size_t]
+    H.tempi_hip_host_free.argtypes = [ctypes.c_void_p]
+    rows = 4096
+    host, dev = ctypes.c_void_p(), ctypes.c_void_p()
+    assert H.tempi_hip_host_alloc(ctypes.byref(host), ctypes.byref(dev), rows * 64) == 0
+    try:
+        obj = torch.zeros(rows * 128, dtype=torch.uint8, device=gpu)
+        assert _slab_rounds(H, host.value, dev.value, obj, rows, 64, 11) == (0, 0)
+    finally:
+        H.tempi_hip_host_free(host)
+
+
+def test_pinned_slab_reuse_coarse_grained_contrast(gpu, capsys):
+    """The same rounds on a coarse-grained slab (hipHostMalloc without
+    hipHostMallocCoherent, HIP's default before d840279). Reported, not
+    asserted: whether this box's L2 returns a stale line here is the
+    hazard the fine-grained allocation rules out."""
+    torch = _torch()
+    import tempi_amd
+
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipHostMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_uint]
+    hip.hipHostGetDevicePointer.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p, ctypes.c_uint]
+    hip.hipHostFree.argtypes = [ctypes.c_void_p]
+    H = ctypes.CDLL(tempi_amd.LIBTEMPI_HIP)
+    rows = 4096
+    host, dev = ctypes.c_void_p(), ctypes.c_void_p()
+    assert hip.hipHostMalloc(ctypes.byref(host), rows * 64, 0x2 | 0x1 | 0x80000000) == 0  # mapped, portable, non-coherent
+    assert hip.hipHostGetDevicePointer(ctypes.byref(dev), host, 0) == 0
+    try:
+        obj = torch.zeros(rows * 128, dtype=torch.uint8, device=gpu)
+        bad = _slab_rounds(H, host.value, dev.value, obj, rows, 64, 12)
+        with capsys.disabled():
+            print(f"\n[coarse-grained slab] stale bytes over 64 rounds: host read {bad[0]}, kernel read {bad[1]}")
+    finally:
+        hip.hipHostFree(host)
