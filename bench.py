@@ -29,6 +29,7 @@ Other modes (not the driver's line):
 """
 import argparse
 import json
+import math
 import os
 import subprocess
 import sys
@@ -60,6 +61,8 @@ def parse():
     p.add_argument("--a2av-iters", type=int, default=20)
     p.add_argument("--no-p2p", action="store_true", help="skip configs 3 and 5 at N > 1")
     p.add_argument("--sweep", default=None, help="run the config-2 sweep and write JSON records here")
+    p.add_argument("--no-sweep-geomean", action="store_true",
+                   help="skip the 1 GiB points of the config-2 sweep in the default line (sweep_geomean)")
     p.add_argument("--inner", action="store_true", help=argparse.SUPPRESS)  # child for --traffic
     return p.parse_args()
 
@@ -469,11 +472,11 @@ def alltoallv(args, world):
             "points": out}
 
 
-def sweep(args, mpi, torch, dev, path):
-    """Config-2 sweep: 2D subarray and 3D subarray, block 1 B - 4 KiB."""
+def sweep(args, mpi, torch, dev, path, sizes=(1 << 20, 16 << 20, 256 << 20, 1 << 30), quiet=False):
+    """Config-2 sweep: 2D subarray and 3D subarray, block 1 B - 4 KiB.
+    Returns the records (also written to `path` when given)."""
     recs = []
     blocks = [1, 2, 3, 4, 8, 12, 16, 24, 32, 64, 128, 256, 512, 1024, 2048, 4096]
-    sizes = [1 << 20, 16 << 20, 256 << 20, 1 << 30]
     for packed_target in sizes:
         for bl in blocks:
             strides = sorted({2 * bl, bl + 16} | ({512} if bl <= 256 else set()))
@@ -522,11 +525,41 @@ def sweep(args, mpi, torch, dev, path):
                            "pack_alg_gbs": 2 * payload / (pk_ms * 1e-3) / 1e9,
                            "unpack_alg_gbs": 2 * payload / (up_ms * 1e-3) / 1e9}
                     recs.append(rec)
-                    print(json.dumps(rec), flush=True)
+                    if not quiet:
+                        print(json.dumps(rec), flush=True)
                     mpi.Type_free(t)
                     del src, pk
-    with open(path, "w") as f:
-        json.dump(recs, f, indent=1)
+    if path:
+        with open(path, "w") as f:
+            json.dump(recs, f, indent=1)
+    return recs
+
+
+def sweep_geomean(args, mpi, torch, dev):
+    """The config-2 sweep's 1 GiB points (2D and 3D subarrays, block 1 B -
+    4 KiB, strides 2*bl / bl+16 / 512): geometric mean of algorithmic GB/s
+    (kernel time, HIP events), and how many reach 70 % of the 8 TB/s spec."""
+    recs = sweep(args, mpi, torch, dev, None, sizes=(1 << 30,), quiet=True)
+    if not recs:
+        return None
+
+    def gm(xs):
+        return math.exp(sum(math.log(x) for x in xs) / len(xs))
+
+    pk = [r["pack_alg_gbs"] for r in recs]
+    up = [r["unpack_alg_gbs"] for r in recs]
+    worst = sorted(recs, key=lambda r: min(r["pack_alg_gbs"], r["unpack_alg_gbs"]))[:3]
+    return {"points": len(recs), "packed_bytes": 1 << 30,
+            "pack_GBps": round(gm(pk), 1), "unpack_GBps": round(gm(up), 1),
+            "pack_frac": round(gm(pk) / HBM_PEAK_GBS, 4), "unpack_frac": round(gm(up) / HBM_PEAK_GBS, 4),
+            "pack_ge_0.7": sum(x >= 0.7 * HBM_PEAK_GBS for x in pk),
+            "unpack_ge_0.7": sum(x >= 0.7 * HBM_PEAK_GBS for x in up),
+            "worst": [{"shape": r["shape"], "block": r["block"], "stride": r["stride"],
+                       "pack_GBps": round(r["pack_alg_gbs"], 1), "unpack_GBps": round(r["unpack_alg_gbs"], 1)}
+                      for r in worst],
+            "workload": "config 2 at 1 GiB packed: MPI_Type_create_subarray 2D {rows, S} and 3D {z+2, y+3, S}, "
+                        "block 1 B - 4 KiB, S in {2*bl, bl+16, 512 (bl <= 256)}; kernel time per MPI_Pack / "
+                        "MPI_Unpack from HIP events on TEMPI's stream"}
 
 
 def main():
@@ -549,6 +582,9 @@ def main():
         if args.inner:
             return
         torch.cuda.empty_cache()
+        if world == 1 and not args.no_sweep_geomean:
+            rec["sweep_geomean"] = sweep_geomean(args, mpi, torch, dev)
+            torch.cuda.empty_cache()
         if not args.no_halo:
             h = halo(args, mpi, world)
             if rank == 0:

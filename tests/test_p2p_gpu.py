@@ -194,7 +194,9 @@ def test_completion_family_device(gpu, method):
 
 
 @pytest.mark.parametrize("env", [METHODS["XCOPY"], dict(METHODS["XCOPY"], TEMPI_FAULT_IPC_OPEN="1"),
-                                 dict(METHODS["XCOPY"], TEMPI_STREAMS="3")], ids=["copy", "unmapped", "lanes"])
+                                 dict(METHODS["XCOPY"], TEMPI_STREAMS="3"),
+                                 dict(METHODS["XCOPY"], TEMPI_FAKE_FOREIGN_GPU="1")],
+                         ids=["copy", "unmapped", "lanes", "foreign"])
 def test_ipc_copy_receivers(gpu, env):
     """IPC COPY against every receiver: same and other strided shapes (copy
     kernel), a receive type too deep for it and a host receive (the sender
