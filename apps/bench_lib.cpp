@@ -25,6 +25,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <numeric>
 #include <random>
 #include <vector>
@@ -81,6 +82,35 @@ __host__ __device__ inline unsigned char a2av_byte(int64_t i, int src, int dst) 
   return (unsigned char)((i * 31 + src * 7 + dst * 13) & 0xFF);
 }
 
+// TEMPI_BENCH_HOST=1: the same workload on pageable host memory -- the
+// library path the reference takes for host buffers (with TEMPI_DISABLE=1:
+// the host MPI alone, bench.py's CPU baselines)
+bool host_buffers() {
+  const char *e = std::getenv("TEMPI_BENCH_HOST");
+  return e && *e && *e != '0';
+}
+void *buf_alloc(size_t n) {
+  void *p = nullptr;
+  if (host_buffers())
+    p = std::aligned_alloc(4096, (std::max<size_t>(n, 1) + 4095) / 4096 * 4096);
+  else
+    HIPCHECK(hipMalloc(&p, std::max<size_t>(n, 1)));
+  return p;
+}
+void buf_free(void *p) {
+  if (host_buffers())
+    std::free(p);
+  else
+    HIPCHECK(hipFree(p));
+}
+// bytes between a host vector and a benchmark buffer (either kind)
+void buf_copy(void *dst, const void *src, size_t n) {
+  if (host_buffers())
+    std::memcpy(dst, src, n);
+  else
+    HIPCHECK(hipMemcpy(dst, src, n, hipMemcpyDefault));
+}
+
 } // namespace
 
 EXPORT int tempi_bench_pingpong(int iters, long total, long bl, long stride, int check, int setDevice, char *json,
@@ -92,19 +122,18 @@ EXPORT int tempi_bench_pingpong(int iters, long total, long bl, long stride, int
   const int nblocks = int(total / bl);
   if (setDevice) {
     int ndev = 0;
-    HIPCHECK(hipGetDeviceCount(&ndev));
-    HIPCHECK(hipSetDevice(rank % ndev));
+    if (hipGetDeviceCount(&ndev) != hipSuccess) ndev = 0; // (host buffers need no GPU)
+    if (ndev > 0) HIPCHECK(hipSetDevice(rank % ndev));
   }
   MPI_Datatype t;
   MPI_Type_vector(nblocks, int(bl), int(stride), MPI_BYTE, &t);
   MPI_Type_commit(&t);
   MPI_Aint lb, ext;
   MPI_Type_get_extent(t, &lb, &ext);
-  char *buf;
-  HIPCHECK(hipMalloc(&buf, size_t(ext)));
+  char *buf = static_cast<char *>(buf_alloc(size_t(ext)));
   std::vector<unsigned char> h(static_cast<size_t>(ext));
   for (size_t i = 0; i < h.size(); ++i) h[i] = (unsigned char)((i * 131 + size_t(rank) * 7) & 0xFF);
-  HIPCHECK(hipMemcpy(buf, h.data(), h.size(), hipMemcpyHostToDevice));
+  buf_copy(buf, h.data(), h.size());
 
   std::vector<double> times;
   long errors = 0;
@@ -125,7 +154,7 @@ EXPORT int tempi_bench_pingpong(int iters, long total, long bl, long stride, int
     // every block now holds rank 0's original bytes; the gaps keep each
     // rank's own pattern
     std::vector<unsigned char> g(static_cast<size_t>(ext));
-    HIPCHECK(hipMemcpy(g.data(), buf, g.size(), hipMemcpyDeviceToHost));
+    buf_copy(g.data(), buf, g.size());
     for (long b = 0; b < nblocks; ++b)
       for (long k = 0; k < stride && b * stride + k < long(ext); ++k) {
         const size_t i = size_t(b * stride + k);
@@ -139,12 +168,12 @@ EXPORT int tempi_bench_pingpong(int iters, long total, long bl, long stride, int
     const double oneway = trimean(times) / 2;
     std::snprintf(json, size_t(jsonCap),
                   "{\"total\": %ld, \"block\": %ld, \"stride\": %ld, \"iters\": %d, \"oneway_us\": %.2f, "
-                  "\"GBps\": %.3f, \"checked\": %s, \"errors\": %ld, \"method\": \"%s\"}",
+                  "\"GBps\": %.3f, \"checked\": %s, \"errors\": %ld, \"method\": \"%s\", \"buffers\": \"%s\"}",
                   total, bl, stride, iters, oneway * 1e6, double(total) / oneway / 1e9, check ? "true" : "false",
-                  errors, method_name());
+                  errors, method_name(), host_buffers() ? "host" : "device");
   }
   MPI_Type_free(&t);
-  HIPCHECK(hipFree(buf));
+  buf_free(buf);
   return errors ? 3 : 0;
 }
 
@@ -161,8 +190,8 @@ EXPORT int tempi_bench_alltoallv(int iters, int scale, double density, int seed,
   MPI_Comm_size(MPI_COMM_WORLD, &size);
   if (setDevice) {
     int ndev = 0;
-    HIPCHECK(hipGetDeviceCount(&ndev));
-    HIPCHECK(hipSetDevice(rank % ndev));
+    if (hipGetDeviceCount(&ndev) != hipSuccess) ndev = 0; // (host buffers need no GPU)
+    if (ndev > 0) HIPCHECK(hipSetDevice(rank % ndev));
   }
   const int rowNnz = int(density * size + 0.5);
   const std::vector<int64_t> mat = random_sparse(size, rowNnz, 1, 10, scale, seed);
@@ -193,10 +222,13 @@ EXPORT int tempi_bench_alltoallv(int iters, int scale, double density, int seed,
       }
     maxOut = std::max(maxOut, std::max(o, in));
   }
-  unsigned char *sbuf, *rbuf;
-  HIPCHECK(hipMalloc(&sbuf, size_t(std::max<int64_t>(sbytes, 1))));
-  HIPCHECK(hipMalloc(&rbuf, size_t(std::max<int64_t>(rbytes, 1))));
-  {
+  unsigned char *sbuf = static_cast<unsigned char *>(buf_alloc(size_t(sbytes)));
+  unsigned char *rbuf = static_cast<unsigned char *>(buf_alloc(size_t(rbytes)));
+  if (host_buffers()) {
+    for (int d = 0; d < size; ++d)
+      for (int64_t i = 0; i < sc[size_t(d)]; ++i) sbuf[sd[size_t(d)] + i] = a2av_byte(i, rank, d);
+    std::memset(rbuf, 0xEE, size_t(std::max<int64_t>(rbytes, 1)));
+  } else {
     std::vector<int64_t> hd(static_cast<size_t>(size)), hc(static_cast<size_t>(size));
     for (int p = 0; p < size; ++p) {
       hd[size_t(p)] = sd[size_t(p)];
@@ -225,7 +257,7 @@ EXPORT int tempi_bench_alltoallv(int iters, int scale, double density, int seed,
   long errors = 0;
   if (check) {
     std::vector<unsigned char> h(size_t(std::max<int64_t>(rbytes, 1)));
-    HIPCHECK(hipMemcpy(h.data(), rbuf, h.size(), hipMemcpyDeviceToHost));
+    buf_copy(h.data(), rbuf, h.size());
     for (int p = 0; p < size; ++p)
       for (int64_t i = 0; i < rc[size_t(p)]; ++i)
         if (h[size_t(rd[size_t(p)] + i)] != a2av_byte(i, p, rank)) ++errors;
@@ -236,11 +268,12 @@ EXPORT int tempi_bench_alltoallv(int iters, int scale, double density, int seed,
     std::snprintf(json, size_t(jsonCap),
                   "{\"ranks\": %d, \"scale\": %d, \"density\": %.4f, \"row_nnz\": %d, \"seed\": %d, \"iters\": %d, "
                   "\"min_us\": %.2f, \"trimean_us\": %.2f, \"total_bytes\": %lld, \"max_pairwise_bytes\": %lld, "
-                  "\"max_gpu_out_or_in_bytes\": %lld, \"checked\": %s, \"errors\": %ld}",
+                  "\"max_gpu_out_or_in_bytes\": %lld, \"checked\": %s, \"errors\": %ld, \"buffers\": \"%s\"}",
                   size, scale, density, rowNnz, seed, iters, tmin * 1e6, trimean(times) * 1e6, (long long)total,
-                  (long long)maxPair, (long long)maxOut, check ? "true" : "false", errors);
+                  (long long)maxPair, (long long)maxOut, check ? "true" : "false", errors,
+                  host_buffers() ? "host" : "device");
   }
-  HIPCHECK(hipFree(sbuf));
-  HIPCHECK(hipFree(rbuf));
+  buf_free(sbuf);
+  buf_free(rbuf);
   return errors ? 3 : 0;
 }

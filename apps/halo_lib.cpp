@@ -115,6 +115,14 @@ __global__ void __launch_bounds__(kCheckBlock) check_kernel(const uint64_t *buf,
   if (threadIdx.x == 0) blockErrors[blockIdx.x] = part[0];
 }
 
+// TEMPI_BENCH_HOST=1: the same exchange on pageable host memory -- the
+// library path the reference takes for host buffers. With TEMPI_DISABLE=1 it
+// is the host MPI's own strided Isend / Irecv: bench.py's CPU baseline.
+static bool host_buffers() {
+  const char *e = std::getenv("TEMPI_BENCH_HOST");
+  return e && *e && *e != '0';
+}
+
 // TEMPI's own entry points, when the interposer is linked (weak: the app runs
 // unchanged on a plain MPI)
 extern "C" __attribute__((weak)) void tempi_reset_counters(void);
@@ -140,8 +148,8 @@ tempi_bench_halo(int nIters, int gx, int gy, int gz, int nQuants, int radius, in
 
   // one GPU per rank on the node (ranks beyond the GPU count share)
   int ndev = 0;
-  HIPCHECK(hipGetDeviceCount(&ndev));
-  if (setDevice) {
+  if (hipGetDeviceCount(&ndev) != hipSuccess) ndev = 0; // (host buffers need no GPU)
+  if (setDevice && ndev > 0) {
     MPI_Comm node;
     MPI_Comm_split_type(MPI_COMM_WORLD, MPI_COMM_TYPE_SHARED, rank, MPI_INFO_NULL, &node);
     int lr;
@@ -173,13 +181,25 @@ tempi_bench_halo(int nIters, int gx, int gy, int gz, int nQuants, int radius, in
   const size_t bufBytes = pitch * size_t(ysize) * size_t(zsize);
 
   std::vector<char *> bufs(static_cast<size_t>(nQuants));
+  const bool onHost = host_buffers();
   for (int qi = 0; qi < nQuants; ++qi) {
+    if (onHost) {
+      bufs[size_t(qi)] = static_cast<char *>(std::aligned_alloc(4096, (bufBytes + 4095) / 4096 * 4096));
+      std::memset(bufs[size_t(qi)], 0xEE, bufBytes);
+      uint64_t *b = reinterpret_cast<uint64_t *>(bufs[size_t(qi)]);
+      for (int z = 0; z < lcr.z; ++z)
+        for (int y = 0; y < lcr.y; ++y)
+          for (int x = 0; x < lcr.x; ++x)
+            b[(size_t(z + radius) * ysize + size_t(y + radius)) * (pitch / 8) + size_t(x + radius)] =
+                cell_value(origin.x + x, origin.y + y, origin.z + z, qi);
+      continue;
+    }
     HIPCHECK(hipMalloc(&bufs[size_t(qi)], bufBytes));
     HIPCHECK(hipMemset(bufs[size_t(qi)], 0xEE, bufBytes));
     hipLaunchKernelGGL(fill_kernel, dim3(1024), dim3(256), 0, 0, reinterpret_cast<uint64_t *>(bufs[size_t(qi)]),
                        pitch / 8, ysize, lcr, origin, global, radius, qi);
   }
-  HIPCHECK(hipDeviceSynchronize());
+  if (!onHost) HIPCHECK(hipDeviceSynchronize());
 
   struct Dir {
     int dx, dy, dz, nbr;
@@ -296,18 +316,38 @@ tempi_bench_halo(int nIters, int gx, int gy, int gz, int nQuants, int radius, in
   if (check) {
     // check == 2: a negative control -- one planted wrong cell (rank 0,
     // quantity 0, the halo corner at (0, 0, 0)) must be counted
-    if (check == 2 && rank == 0) HIPCHECK(hipMemset(bufs[0], 0x5A, 8));
-    unsigned long long *dErr = nullptr;
-    HIPCHECK(hipMalloc(&dErr, sizeof(unsigned long long) * kCheckGrid));
-    std::vector<unsigned long long> hErr(kCheckGrid);
-    for (int qi = 0; qi < nQuants; ++qi) {
-      hipLaunchKernelGGL(check_kernel, dim3(kCheckGrid), dim3(kCheckBlock), 0, 0,
-                         reinterpret_cast<const uint64_t *>(bufs[size_t(qi)]), pitch / 8, ysize, zsize,
-                         lcr.x + 2 * radius, origin, global, radius, qi, dErr);
-      HIPCHECK(hipMemcpy(hErr.data(), dErr, sizeof(unsigned long long) * kCheckGrid, hipMemcpyDeviceToHost));
-      for (unsigned long long e : hErr) errors += (long long)e;
+    if (check == 2 && rank == 0) {
+      if (onHost)
+        std::memset(bufs[0], 0x5A, 8);
+      else
+        HIPCHECK(hipMemset(bufs[0], 0x5A, 8));
     }
-    HIPCHECK(hipFree(dErr));
+    if (onHost) {
+      const int xsize = lcr.x + 2 * radius;
+      for (int qi = 0; qi < nQuants; ++qi) {
+        const uint64_t *b = reinterpret_cast<const uint64_t *>(bufs[size_t(qi)]);
+        for (int z = 0; z < zsize; ++z)
+          for (int y = 0; y < ysize; ++y)
+            for (int x = 0; x < xsize; ++x) {
+              const int64_t gx = (origin.x + x - radius + global.x) % global.x;
+              const int64_t gy = (origin.y + y - radius + global.y) % global.y;
+              const int64_t gz = (origin.z + z - radius + global.z) % global.z;
+              errors += b[(size_t(z) * ysize + size_t(y)) * (pitch / 8) + size_t(x)] != cell_value(gx, gy, gz, qi);
+            }
+      }
+    } else {
+      unsigned long long *dErr = nullptr;
+      HIPCHECK(hipMalloc(&dErr, sizeof(unsigned long long) * kCheckGrid));
+      std::vector<unsigned long long> hErr(kCheckGrid);
+      for (int qi = 0; qi < nQuants; ++qi) {
+        hipLaunchKernelGGL(check_kernel, dim3(kCheckGrid), dim3(kCheckBlock), 0, 0,
+                           reinterpret_cast<const uint64_t *>(bufs[size_t(qi)]), pitch / 8, ysize, zsize,
+                           lcr.x + 2 * radius, origin, global, radius, qi, dErr);
+        HIPCHECK(hipMemcpy(hErr.data(), dErr, sizeof(unsigned long long) * kCheckGrid, hipMemcpyDeviceToHost));
+        for (unsigned long long e : hErr) errors += (long long)e;
+      }
+      HIPCHECK(hipFree(dErr));
+    }
     MPI_Allreduce(MPI_IN_PLACE, &errors, 1, MPI_LONG_LONG, MPI_SUM, MPI_COMM_WORLD);
   }
 
@@ -331,13 +371,13 @@ tempi_bench_halo(int nIters, int gx, int gy, int gz, int nQuants, int radius, in
                 "\"payload_bytes_per_iter_per_rank0\": %.0f, \"total_bytes_per_iter\": %.0f, "
                 "\"max_peer_bytes_per_iter\": %.0f, \"aggregate_GBps\": %.2f, \"busiest_link_GBps\": %.2f, "
                 "\"remote_bytes_per_iter\": %.0f, \"links_used\": %.0f, "
-                "\"checked\": %s, \"errors\": %lld, \"api\": \"%s\", \"rank0_us_per_iter\": {\"isend\": %.1f, "
+                "\"checked\": %s, \"errors\": %lld, \"api\": \"%s\", \"buffers\": \"%s\", \"rank0_us_per_iter\": {\"isend\": %.1f, "
                 "\"irecv\": %.1f, \"wait\": %.1f}}\n",
                 size, global.x, global.y, global.z, dims.x, dims.y, dims.z, lcr.x, lcr.y, lcr.z, nQuants, radius,
                 nIters, tIter * 1e6, *std::min_element(times.begin(), times.end()) * 1e6, bytesPerIter, totalBytes,
                 maxLinkAll, totalBytes / tIter / 1e9, maxLinkAll / tIter / 1e9, remote[0], remote[1],
                 check ? "true" : "false", errors,
-                neighbor ? "MPI_Neighbor_alltoallw" : "MPI_Isend/MPI_Irecv/MPI_Wait",
+                neighbor ? "MPI_Neighbor_alltoallw" : "MPI_Isend/MPI_Irecv/MPI_Wait", onHost ? "host" : "device",
                 tIsend / nIters * 1e6, tIrecv / nIters * 1e6, tWait / nIters * 1e6);
   }
   if (graph != MPI_COMM_NULL) MPI_Comm_free(&graph);
@@ -345,6 +385,11 @@ tempi_bench_halo(int nIters, int gx, int gy, int gz, int nQuants, int radius, in
     MPI_Type_free(&D.interior);
     MPI_Type_free(&D.exterior);
   }
-  for (char *b : bufs) HIPCHECK(hipFree(b));
+  for (char *b : bufs) {
+    if (onHost)
+      std::free(b);
+    else
+      HIPCHECK(hipFree(b));
+  }
   return errors ? 3 : 0;
 }

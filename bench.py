@@ -63,6 +63,8 @@ def parse():
     p.add_argument("--sweep", default=None, help="run the config-2 sweep and write JSON records here")
     p.add_argument("--no-sweep-geomean", action="store_true",
                    help="skip the 1 GiB points of the config-2 sweep in the default line (sweep_geomean)")
+    p.add_argument("--no-measure-system", action="store_true",
+                   help="N > 1: do not measure this node's perf.json when it is missing")
     p.add_argument("--inner", action="store_true", help=argparse.SUPPRESS)  # child for --traffic
     return p.parse_args()
 
@@ -156,6 +158,61 @@ def cpu_baseline(mpi, pitch, block, seconds):
                    f"{rows * block >> 20} MiB packed, {n} pack+unpack pairs in {el:.1f} s, pinned to 1 core "
                    f"of {model}"),
     }
+
+
+def _cpu_model():
+    try:
+        return [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
+    except Exception:
+        return "unknown"
+
+
+def library_path_baselines(args):
+    """CPU baselines of configs 3-5: the same apps on pageable host buffers
+    with TEMPI_DISABLE=1, i.e. the host MPI's own strided Isend / Irecv /
+    Send / Recv / Alltoallv (the reference's path for host memory), each a
+    child MPI job of its own, bounded to a few seconds."""
+    import tempi_amd
+
+    env = {k: v for k, v in os.environ.items() if not k.startswith(("PMI_", "MPI_LOCAL", "HYDRA_"))}
+    env.update({"TEMPI_DISABLE": "1", "TEMPI_BENCH_HOST": "1", "HYDRA_LAUNCHER": "fork"})
+    lib = tempi_amd.LIBDIR
+
+    def run(n, argv, timeout=240):
+        r = subprocess.run(["timeout", "-k", "10", str(timeout), "/opt/conda/bin/mpiexec", "-n", str(n)] + argv,
+                           stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env)
+        for line in r.stdout.splitlines():
+            if line.startswith("{"):
+                return json.loads(line)
+        return None
+
+    model = _cpu_model()
+    out = {}
+    h = run(1, [os.path.join(lib, "halo_exchange"), "2", str(args.halo_grid)])
+    if h:
+        out["halo"] = {"value": h["us_per_iter"], "unit": "us/iter", "higher_is_better": False, "cores": 1,
+                       "kind": "reference",
+                       "sample": (f"halo_exchange {args.halo_grid}^3, 8 quantities, 1 rank, pageable host buffers, "
+                                  f"TEMPI_DISABLE=1 (MPICH 3.3.2 packs the subarray types on the CPU), 2 iterations "
+                                  f"after 1 warm-up, one core of {model}")}
+    pp = []
+    for total, bl in ((4 << 20, 512), (4 << 20, 64), (1 << 20, 8)):
+        r = run(2, [os.path.join(lib, "pingpong_nd"), "20", str(total), str(bl)])
+        if r:
+            pp.append({"total": total, "block": bl, "oneway_us": r["oneway_us"], "GBps": r["GBps"]})
+    if pp:
+        out["pingpong"] = {"points": pp, "unit": "us one-way", "higher_is_better": False, "cores": 2,
+                           "kind": "reference",
+                           "sample": (f"pingpong_nd vector(total/bl, bl, 512) MPI_Send/MPI_Recv, 2 ranks on one host, "
+                                      f"pageable host buffers, TEMPI_DISABLE=1, 20 round trips, 2 cores of {model}")}
+    a = run(8, [os.path.join(lib, "alltoallv_sparse"), "20", "--scale", "100000", "--density", "1.0"])
+    if a:
+        out["alltoallv"] = {"value": a["min_us"], "unit": "us", "higher_is_better": False, "cores": 8,
+                            "kind": "reference",
+                            "sample": (f"alltoallv_sparse scale 1e5 density 1.0 (the reference's random sparse "
+                                       f"matrix, seed 101), 8 ranks, pageable host buffers, TEMPI_DISABLE=1, min of 20, "
+                                       f"8 cores of {model}")}
+    return out
 
 
 def run_traffic_passes(args, kernel_substr):
@@ -411,6 +468,105 @@ def halo(args, mpi, world, grid=None):
     return out
 
 
+def tempi_cache_dir():
+    """TEMPI_CACHE_DIR as libtempi resolves it (tempi_amd/csrc/core/env.cpp)"""
+    if os.environ.get("TEMPI_CACHE_DIR"):
+        return os.environ["TEMPI_CACHE_DIR"]
+    if os.environ.get("XDG_CACHE_HOME"):
+        return os.path.join(os.environ["XDG_CACHE_HOME"], "tempi")
+    if os.environ.get("HOME"):
+        return os.path.join(os.environ["HOME"], ".tempi")
+    return "/var/tmp"
+
+
+def node_perf_model(args, mpi, pg, rank, world, shared_gpu):
+    """AUTO's model on this node: when TEMPI_CACHE_DIR/perf.json is missing,
+    rank 0 measures it with apps/measure_system --quick (a 2-rank MPI job of
+    its own, a child process: ranks 0 and 1 of the node, GPUs 0 and 1), then
+    every rank re-reads the model. Reports which file AUTO uses."""
+    import ctypes
+
+    import tempi_amd
+
+    path = os.path.join(tempi_cache_dir(), "perf.json")
+    info = {"perf_json": path, "measured_here": False}
+    if rank == 0 and not os.path.exists(path) and not args.no_measure_system:
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        env = {k: v for k, v in os.environ.items() if not k.startswith(("PMI_", "MPI_LOCAL", "HYDRA_"))}
+        env["HYDRA_LAUNCHER"] = "fork"
+        exe = os.path.join(tempi_amd.LIBDIR, "measure_system")
+        t0 = time.perf_counter()
+        r = subprocess.run(["timeout", "-k", "10", "400", "/opt/conda/bin/mpiexec", "-n", "2", exe, "--quick", "--out",
+                            path], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env)
+        info["measure_seconds"] = round(time.perf_counter() - t0, 1)
+        info["measured_here"] = r.returncode == 0 and os.path.exists(path)
+        if not info["measured_here"]:
+            info["measure_error"] = (r.stdout or "")[-400:]
+    barrier(pg)
+    mpi.L.tempi_perf_reload()
+    buf = ctypes.create_string_buffer(4096)
+    mpi.L.tempi_perf_source.argtypes = [ctypes.c_char_p, ctypes.c_int]
+    loaded = mpi.L.tempi_perf_source(buf, 4096)
+    info["auto_model"] = buf.value.decode() if loaded == 1 else "built-in policy (no perf.json)"
+    if shared_gpu:
+        info["note"] = ("shared GPU: the ranks share this box's MI355X, so a curve measured here is not an "
+                        "xGMI curve")
+    return info
+
+
+def _smi_bytes(v):
+    """an amd-smi metric value ({'value': x, 'unit': 'KB'} or 'N/A') in bytes"""
+    if isinstance(v, dict) and isinstance(v.get("value"), (int, float)):
+        unit = str(v.get("unit", "B")).upper()
+        return float(v["value"]) * {"B": 1, "KB": 1024, "KIB": 1024, "MB": 1 << 20, "MIB": 1 << 20,
+                                    "GB": 1 << 30, "GIB": 1 << 30}.get(unit, 1)
+    if isinstance(v, (int, float)):
+        return float(v)
+    return None
+
+
+def xgmi_snapshot():
+    """amd-smi xgmi -m: {(gpu, peer): (read_bytes, write_bytes)} of the xGMI
+    links that report data counters, or None when the tool or the counters
+    are unavailable (a one-GPU box reports only its SELF link, 'N/A')"""
+    import shutil
+
+    if not shutil.which("amd-smi"):
+        return None
+    try:
+        r = subprocess.run(["amd-smi", "xgmi", "-m", "--json"], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                           text=True, timeout=30)
+        data = json.loads(r.stdout)
+    except Exception:
+        return None
+    out = {}
+    groups = data.get("xgmi_metric", []) if isinstance(data, dict) else data
+    for grp in groups:
+        for g in (grp if isinstance(grp, list) else [grp]):
+            for i, link in enumerate((g.get("link_metrics") or {}).get("links", [])):
+                rd, wr = _smi_bytes(link.get("read")), _smi_bytes(link.get("write"))
+                if rd is None and wr is None:
+                    continue
+                out[(g.get("gpu"), link.get("gpu", i))] = (rd or 0.0, wr or 0.0)
+    return out or None
+
+
+def xgmi_delta(before, after, units_of_work, algorithmic_bytes, seconds):
+    """counter-based xGMI bytes between two snapshots, per unit of work, next
+    to the algorithmic bytes the app computed"""
+    if before is None or after is None:
+        return {"available": False,
+                "note": "amd-smi reports no xGMI data counters on this node (one GPU: only its SELF link)"}
+    rd = sum(max(0.0, after[k][0] - before[k][0]) for k in after if k in before)
+    wr = sum(max(0.0, after[k][1] - before[k][1]) for k in after if k in before)
+    moved = max(rd, wr)
+    return {"available": True, "source": "amd-smi xgmi -m (per-link accumulated read / write data, all GPUs)",
+            "read_bytes": int(rd), "write_bytes": int(wr), "per_unit_bytes": int(moved / max(units_of_work, 1)),
+            "algorithmic_per_unit_bytes": int(algorithmic_bytes),
+            "counter_GBps": round(moved / seconds / 1e9, 1) if seconds > 0 else None,
+            "links_reporting": len(after)}
+
+
 def apps_lib():
     import ctypes
 
@@ -585,10 +741,28 @@ def main():
         if world == 1 and not args.no_sweep_geomean:
             rec["sweep_geomean"] = sweep_geomean(args, mpi, torch, dev)
             torch.cuda.empty_cache()
+        shared_gpu = world > max(torch.cuda.device_count(), 1)
+        if world > 1:
+            pm = node_perf_model(args, mpi, pg, rank, world, shared_gpu)
+            if rank == 0:
+                rec["perf_model"] = pm
         if not args.no_halo:
+            barrier(pg)
+            snap0 = xgmi_snapshot() if world > 1 and rank == 0 else None
+            t0 = time.perf_counter()
             h = halo(args, mpi, world)
+            barrier(pg)
+            el = time.perf_counter() - t0
             if rank == 0:
                 rec["halo"] = h
+                if world > 1 and h:
+                    iters = args.halo_iters + 1  # the app's warm-up iteration moves the same bytes
+                    x = xgmi_delta(snap0, xgmi_snapshot(), iters,
+                                   (h.get("roofline") or {}).get("remote_bytes_per_iter", 0), el)
+                    if shared_gpu:
+                        x["note"] = ("shared GPU: the ranks share this box's MI355X, no byte crosses xGMI; "
+                                     "the algorithmic fractions above only say the bytes never left HBM")
+                    h["xgmi_counters"] = x
             if world > 1:  # the reference scripts' weak scaling: 512 * N^(1/3) per edge
                 hw = halo(args, mpi, world, grid=int(round(args.halo_grid * world ** (1.0 / 3.0))))
                 if rank == 0:
@@ -625,6 +799,11 @@ def main():
                                                 "bound at the 6.3 TB/s achievable rate")
             if not args.no_cpu_baseline:
                 rec["cpu_baseline"] = cpu_baseline(mpi, args.pitch, args.block, args.cpu_seconds)
+                lb = library_path_baselines(args)
+                if lb:
+                    rec["cpu_baselines_configs_3_5"] = lb
+                    if "halo" in lb and rec.get("halo"):
+                        rec["halo"]["cpu_baseline"] = lb["halo"]
         if rank == 0:
             print(json.dumps(rec), flush=True)
     finally:

@@ -79,6 +79,13 @@ double tempi_interp_time(const double *times, int n, int64_t bytes);
 double tempi_interp_2d(const double *table, int rows, int cols, int64_t bytes, int64_t block);
 /* 1 when TEMPI_CACHE_DIR/perf.json was loaded at MPI_Init */
 int tempi_perf_loaded(void);
+/* the file AUTO's model was read from (this node's TEMPI_CACHE_DIR/perf.json,
+   or the shipped MI355X model) into path[cap]; "" and 0 for the built-in
+   policy, 1 when a model is loaded */
+int tempi_perf_source(char *path, int cap);
+/* re-read the model, e.g. after apps/measure_system wrote this node's
+   perf.json (call on every rank) */
+void tempi_perf_reload(void);
 /* parse + re-emit a perf.json document (schema check); 0 on success */
 int tempi_perf_roundtrip(const char *json_in, char *json_out, int cap);
 /* override TEMPI_DATATYPE_* at run time: 0 AUTO, 1 ONESHOT, 2 DEVICE,

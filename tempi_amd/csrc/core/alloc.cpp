@@ -1,4 +1,5 @@
 // tempi_amd/csrc/core/alloc.cpp -- see alloc.hpp
+#include "trace.hpp"
 #include "alloc.hpp"
 
 #include "gpu.hpp"
@@ -37,6 +38,7 @@ Slab *SlabPool::get(size_t n, int device) {
       }
     }
   }
+  TEMPI_RANGE(kind_ == DEVICE ? "tempi::slab alloc (device)" : "tempi::slab alloc (pinned)");
   Slab *s = new Slab();
   s->size = size_t(1) << c;
   s->device = device;

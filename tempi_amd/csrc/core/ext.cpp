@@ -4,12 +4,14 @@
 #include "counters.hpp"
 #include "env.hpp"
 #include "gpu.hpp"
+#include "p2p.hpp"
 #include "perf_model.hpp"
 #include "state.hpp"
 #include "type_cache.hpp"
 
 #include "tempi_ext.h"
 
+#include <cstdio>
 #include <cstring>
 
 #define TEMPI_EXPORT extern "C" __attribute__((visibility("default")))
@@ -146,6 +148,16 @@ TEMPI_EXPORT double tempi_interp_2d(const double *table, int rows, int cols, int
 }
 
 TEMPI_EXPORT int tempi_perf_loaded(void) { return systemPerformanceLoaded ? 1 : 0; }
+
+TEMPI_EXPORT int tempi_perf_source(char *path, int cap) {
+  if (!path || cap <= 0) return -1;
+  std::snprintf(path, size_t(cap), "%s", systemPerformanceSource.c_str());
+  return systemPerformanceLoaded ? 1 : 0;
+}
+
+TEMPI_EXPORT void tempi_perf_reload(void) {
+  if (state.active) p2p::reload_perf_model();
+}
 
 TEMPI_EXPORT int tempi_perf_roundtrip(const char *json_in, char *json_out, int cap) {
   SystemPerformance sp;

@@ -18,6 +18,7 @@
 //   ISIR_REMOTE_STAGED   IPC for co-located peers, STAGED for the others
 // Messages travel on a private duplicate of the communicator, so they never
 // match the application's own point-to-point traffic.
+#include "trace.hpp"
 #include "alloc.hpp"
 #include "counters.hpp"
 #include "env.hpp"
@@ -190,6 +191,7 @@ TEMPI_EXPORT int MPI_Alltoallv(const void *sendbuf, const int sendcounts[], cons
                                MPI_Datatype sendtype, void *recvbuf, const int recvcounts[], const int rdispls[],
                                MPI_Datatype recvtype, MPI_Comm comm) {
   resolve_next();
+  TEMPI_RANGE("MPI_Alltoallv");
   auto lib = [&] {
     return next.MPI_Alltoallv(sendbuf, sendcounts, sdispls, sendtype, recvbuf, recvcounts, rdispls, recvtype,
                               comm);
@@ -238,6 +240,7 @@ TEMPI_EXPORT int MPI_Alltoallv(const void *sendbuf, const int sendcounts[], cons
 // not match each other (whether a rank is busy is its own business).
 TEMPI_EXPORT int MPI_Barrier(MPI_Comm comm) {
   resolve_next();
+  TEMPI_RANGE("MPI_Barrier");
   if (!state.active) return next.MPI_Barrier(comm);
   MPI_Request r = MPI_REQUEST_NULL;
   int rc = MPI_Ibarrier(comm, &r);

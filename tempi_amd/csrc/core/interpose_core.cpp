@@ -11,6 +11,7 @@
 // insize are checked (MPI_ERR_TRUNCATE instead of an overrun), a type with no
 // strided form goes to the library instead of a null packer, and
 // MPI_Init_thread is interposed too (F8).
+#include "trace.hpp"
 #include "counters.hpp"
 #include "env.hpp"
 #include "gpu.hpp"
@@ -52,6 +53,7 @@ void init_after_mpi() {
   MPI_Comm_rank(MPI_COMM_WORLD, &state.worldRank);
   MPI_Comm_size(MPI_COMM_WORLD, &state.worldSize);
   logRank = state.worldRank;
+  trace::init();
   hostTiming = std::getenv("TEMPI_PRINT_COUNTERS") || std::getenv("TEMPI_HOST_TIMING");
   gpu::init();
   types_init();
@@ -310,11 +312,13 @@ int unpack(const void *inbuf, int insize, int *position, void *outbuf, int outco
 TEMPI_EXPORT int MPI_Pack(const void *inbuf, int incount, MPI_Datatype datatype, void *outbuf,
                           int outsize, int *position, MPI_Comm comm) {
   resolve_next();
+  TEMPI_RANGE("MPI_Pack");
   return tempi::pack(inbuf, incount, datatype, outbuf, outsize, position, comm);
 }
 
 TEMPI_EXPORT int MPI_Unpack(const void *inbuf, int insize, int *position, void *outbuf, int outcount,
                             MPI_Datatype datatype, MPI_Comm comm) {
   resolve_next();
+  TEMPI_RANGE("MPI_Unpack");
   return tempi::unpack(inbuf, insize, position, outbuf, outcount, datatype, comm);
 }

@@ -30,6 +30,7 @@
 // Cartesian and (non-distributed) graph topologies are handled too, with
 // MPI_PROC_NULL neighbours skipped. Edges between the same pair of ranks are
 // matched in edge order, as the library's own implementation does.
+#include "trace.hpp"
 #include "counters.hpp"
 #include "gpu.hpp"
 #include "next_mpi.hpp"
@@ -157,6 +158,7 @@ TEMPI_EXPORT int MPI_Neighbor_alltoallw(const void *sendbuf, const int sendcount
                                         const MPI_Datatype sendtypes[], void *recvbuf, const int recvcounts[],
                                         const MPI_Aint rdispls[], const MPI_Datatype recvtypes[], MPI_Comm comm) {
   resolve_next();
+  TEMPI_RANGE("MPI_Neighbor_alltoallw");
   auto lib = [&] {
     return next.MPI_Neighbor_alltoallw(sendbuf, sendcounts, sdispls, sendtypes, recvbuf, recvcounts, rdispls,
                                        recvtypes, comm);
@@ -174,6 +176,7 @@ TEMPI_EXPORT int MPI_Neighbor_alltoallv(const void *sendbuf, const int sendcount
                                         MPI_Datatype sendtype, void *recvbuf, const int recvcounts[],
                                         const int rdispls[], MPI_Datatype recvtype, MPI_Comm comm) {
   resolve_next();
+  TEMPI_RANGE("MPI_Neighbor_alltoallv");
   auto lib = [&] {
     return next.MPI_Neighbor_alltoallv(sendbuf, sendcounts, sdispls, sendtype, recvbuf, recvcounts, rdispls,
                                        recvtype, comm);

@@ -5,6 +5,7 @@
 // recv.cpp:19-44, isend.cpp:11-16, irecv.cpp:11-16, wait.cpp:11-16), except
 // that requests TEMPI owns are understood by MPI_Waitall and MPI_Test too
 // (SURVEY F8), and library waits keep TEMPI operations progressing.
+#include "trace.hpp"
 #include "counters.hpp"
 #include "next_mpi.hpp"
 #include "p2p.hpp"
@@ -21,6 +22,7 @@ using namespace tempi;
 TEMPI_EXPORT int MPI_Send(const void *buf, int count, MPI_Datatype datatype, int dest, int tag,
                           MPI_Comm comm) {
   resolve_next();
+  TEMPI_RANGE("MPI_Send");
   p2p::Route route;
   if (!p2p::handles(buf, count, datatype, dest, &route)) {
     counters.lib_sends++;
@@ -37,6 +39,7 @@ TEMPI_EXPORT int MPI_Send(const void *buf, int count, MPI_Datatype datatype, int
 TEMPI_EXPORT int MPI_Recv(void *buf, int count, MPI_Datatype datatype, int source, int tag, MPI_Comm comm,
                           MPI_Status *status) {
   resolve_next();
+  TEMPI_RANGE("MPI_Recv");
   p2p::Route route;
   if (p2p::handles(buf, count, datatype, source, &route)) {
     counters.recvs++;
@@ -55,6 +58,7 @@ TEMPI_EXPORT int MPI_Recv(void *buf, int count, MPI_Datatype datatype, int sourc
 TEMPI_EXPORT int MPI_Isend(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm,
                            MPI_Request *request) {
   resolve_next();
+  TEMPI_RANGE("MPI_Isend");
   p2p::Route route;
   if (p2p::handles(buf, count, datatype, dest, &route))
     return p2p::isend(buf, count, datatype, dest, tag, comm, request, route);
@@ -70,6 +74,7 @@ TEMPI_EXPORT int MPI_Isend(const void *buf, int count, MPI_Datatype datatype, in
 TEMPI_EXPORT int MPI_Irecv(void *buf, int count, MPI_Datatype datatype, int source, int tag, MPI_Comm comm,
                            MPI_Request *request) {
   resolve_next();
+  TEMPI_RANGE("MPI_Irecv");
   p2p::Route route;
   if (p2p::handles(buf, count, datatype, source, &route))
     return p2p::irecv(buf, count, datatype, source, tag, comm, request, route);
@@ -82,6 +87,7 @@ TEMPI_EXPORT int MPI_Irecv(void *buf, int count, MPI_Datatype datatype, int sour
 
 TEMPI_EXPORT int MPI_Wait(MPI_Request *request, MPI_Status *status) {
   resolve_next();
+  TEMPI_RANGE("MPI_Wait");
   if (!state.active) return next.MPI_Wait(request, status);
   if (p2p::is_tempi_request(*request)) return p2p::wait(request, status);
   if (!p2p::busy()) return next.MPI_Wait(request, status);
@@ -103,6 +109,7 @@ TEMPI_EXPORT int MPI_Test(MPI_Request *request, int *flag, MPI_Status *status) {
 
 TEMPI_EXPORT int MPI_Waitall(int count, MPI_Request requests[], MPI_Status statuses[]) {
   resolve_next();
+  TEMPI_RANGE("MPI_Waitall");
   if (!state.active) return next.MPI_Waitall(count, requests, statuses);
   bool any = false;
   for (int i = 0; i < count && !any; ++i) any = p2p::is_tempi_request(requests[i]);
@@ -286,6 +293,7 @@ TEMPI_EXPORT int MPI_Sendrecv(const void *sendbuf, int sendcount, MPI_Datatype s
                               void *recvbuf, int recvcount, MPI_Datatype recvtype, int source, int recvtag,
                               MPI_Comm comm, MPI_Status *status) {
   resolve_next();
+  TEMPI_RANGE("MPI_Sendrecv");
   p2p::Route sr, rr;
   // TEMPI's when either side is a device object, or when the host receive
   // could meet a descriptor
@@ -313,6 +321,7 @@ TEMPI_EXPORT int MPI_Sendrecv(const void *sendbuf, int sendcount, MPI_Datatype s
 // matched receive lands the payload (p2p.hpp).
 TEMPI_EXPORT int MPI_Probe(int source, int tag, MPI_Comm comm, MPI_Status *status) {
   resolve_next();
+  TEMPI_RANGE("MPI_Probe");
   return p2p::probe(source, tag, comm, nullptr, status);
 }
 
@@ -323,6 +332,7 @@ TEMPI_EXPORT int MPI_Iprobe(int source, int tag, MPI_Comm comm, int *flag, MPI_S
 
 TEMPI_EXPORT int MPI_Mprobe(int source, int tag, MPI_Comm comm, MPI_Message *message, MPI_Status *status) {
   resolve_next();
+  TEMPI_RANGE("MPI_Mprobe");
   return p2p::mprobe(source, tag, comm, nullptr, message, status);
 }
 
@@ -334,6 +344,7 @@ TEMPI_EXPORT int MPI_Improbe(int source, int tag, MPI_Comm comm, int *flag, MPI_
 
 TEMPI_EXPORT int MPI_Mrecv(void *buf, int count, MPI_Datatype datatype, MPI_Message *message, MPI_Status *status) {
   resolve_next();
+  TEMPI_RANGE("MPI_Mrecv");
   if (!state.active) return next.MPI_Mrecv(buf, count, datatype, message, status);
   return p2p::mrecv(buf, count, datatype, message, status);
 }

@@ -1,4 +1,5 @@
 // tempi_amd/csrc/core/p2p.cpp -- see p2p.hpp
+#include "trace.hpp"
 #include "p2p.hpp"
 
 #include "alloc.hpp"
@@ -616,6 +617,7 @@ int nextLane = 0; // round robin over the scatter lanes
 
 void flush_list(PendingList &list, bool pack) {
   if (list.empty()) return;
+  TEMPI_RANGE(pack ? "tempi::launch gathers" : "tempi::launch scatters/copies");
   ScopedNs timer(counters.ns_flush);
   // gathers (and anything ordered after one) run on lane 0; scatters and
   // copies take the other lanes in turn, so consecutive batches overlap
@@ -1632,6 +1634,11 @@ void init() {
   int *ub = nullptr;
   MPI_Comm_get_attr(MPI_COMM_WORLD, MPI_TAG_UB, &ub, &flag);
   if (flag && ub) tagUb = *ub;
+}
+
+void reload_perf_model() {
+  systemPerformanceLoaded = import_system_performance(&systemPerformance);
+  modelCache.clear();
 }
 
 void finalize() {

@@ -47,6 +47,8 @@ namespace p2p {
 
 void init();
 void finalize();
+// re-read the perf model (after measure_system wrote this node's perf.json)
+void reload_perf_model();
 
 // what handles() found out, handed on to isend / irecv
 struct Route {

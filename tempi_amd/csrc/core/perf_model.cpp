@@ -21,6 +21,7 @@ namespace tempi {
 
 SystemPerformance systemPerformance;
 bool systemPerformanceLoaded = false;
+std::string systemPerformanceSource;
 
 bool SystemPerformance::empty() const {
   return intraNodeCpuCpuPingpong.empty() && intraNodeGpuGpuPingpong.empty() && d2h.empty() && packDevice.empty();
@@ -387,8 +388,15 @@ bool import_system_performance(SystemPerformance *sp) {
   // this node's own measurement first (TEMPI_CACHE_DIR/perf.json, as in the
   // reference), then the shipped MI355X model unless TEMPI_NO_SHIPPED_PERF;
   // with neither, AUTO uses the built-in policy (the reference stops: F10)
-  if (load_file(perf_path(), sp)) return true;
-  if (!std::getenv("TEMPI_NO_SHIPPED_PERF") && load_file(shipped_path(), sp)) return true;
+  systemPerformanceSource.clear();
+  if (load_file(perf_path(), sp)) {
+    systemPerformanceSource = perf_path();
+    return true;
+  }
+  if (!std::getenv("TEMPI_NO_SHIPPED_PERF") && load_file(shipped_path(), sp)) {
+    systemPerformanceSource = shipped_path();
+    return true;
+  }
   LOG_DEBUG("no perf.json: AUTO uses the built-in policy");
   return false;
 }

@@ -74,5 +74,6 @@ bool export_system_performance(const SystemPerformance &sp);
 
 extern SystemPerformance systemPerformance;
 extern bool systemPerformanceLoaded;
+extern std::string systemPerformanceSource; // the file AUTO's model came from ("" = built-in policy)
 
 } // namespace tempi

@@ -1,0 +1,59 @@
+"""The config 3-5 apps on pageable host buffers (TEMPI_BENCH_HOST=1), on CPU:
+the library path the reference takes for host memory, which is also
+bench.py's CPU baseline (TEMPI_DISABLE=1), and the same apps with TEMPI
+loaded and active but no GPU (every call reaches the library through the
+interposer). Every exchanged byte is checked; the halo runs the
+decompositions of 1, 2, 4 and 8 ranks, the alltoallv config 5's 8 ranks."""
+import json
+import os
+
+import pytest
+
+from tests import mpi_launch
+
+LIB = os.path.join(mpi_launch.ROOT, "tempi_amd", "lib")
+HOST = {"TEMPI_BENCH_HOST": "1"}
+MODES = {"library": dict(HOST, TEMPI_DISABLE="1"), "interposed": HOST}
+
+
+def _json(out):
+    for line in out.splitlines():
+        if line.startswith("{"):
+            return json.loads(line)
+    raise AssertionError(out[-3000:])
+
+
+@pytest.mark.parametrize("mode", list(MODES))
+@pytest.mark.parametrize("ranks,grid,extra", [(1, "24", []), (2, "24", []), (4, "24", []), (8, "24", []),
+                                              (8, "24", ["--neighbor"]), (3, "18", [])])
+def test_halo_host(mode, ranks, grid, extra):
+    rc, out = mpi_launch.run(ranks, [os.path.join(LIB, "halo_exchange"), "2", grid, "--quants", "2", "--check"] + extra,
+                             env=MODES[mode], timeout=200)
+    r = _json(out)
+    assert rc == 0 and r["checked"] and r["errors"] == 0 and r["buffers"] == "host", out[-3000:]
+    if ranks == 8:
+        assert r["dims"] == [2, 2, 2]
+
+
+def test_halo_host_check_finds_a_planted_error():
+    rc, out = mpi_launch.run(2, [os.path.join(LIB, "halo_exchange"), "1", "16", "--quants", "1", "--check-control"],
+                             env=MODES["library"], timeout=120)
+    assert _json(out)["errors"] == 1, out[-3000:]
+
+
+@pytest.mark.parametrize("mode", list(MODES))
+@pytest.mark.parametrize("total,block", [(1024, 8), (1 << 20, 64), (1 << 20, 1)])
+def test_pingpong_host(mode, total, block):
+    rc, out = mpi_launch.run(2, [os.path.join(LIB, "pingpong_nd"), "3", str(total), str(block), "--check"],
+                             env=MODES[mode], timeout=120)
+    r = _json(out)
+    assert rc == 0 and r["checked"] and r["errors"] == 0 and r["buffers"] == "host", out[-3000:]
+
+
+@pytest.mark.parametrize("mode", list(MODES))
+@pytest.mark.parametrize("ranks,scale,density", [(8, 1000, 1.0), (8, 10, 0.5), (8, 100000, 0.125), (3, 100, 1.0)])
+def test_alltoallv_host(mode, ranks, scale, density):
+    rc, out = mpi_launch.run(ranks, [os.path.join(LIB, "alltoallv_sparse"), "2", "--scale", str(scale), "--density",
+                                     str(density), "--check"], env=MODES[mode], timeout=120)
+    r = _json(out)
+    assert rc == 0 and r["checked"] and r["errors"] == 0 and r["buffers"] == "host", out[-3000:]

@@ -1,0 +1,76 @@
+"""bench.py's host-side helpers for the N > 1 line, without a GPU: the
+amd-smi xGMI counter parsing (the one-GPU box's real output, and a
+synthetic two-link node), counter deltas against the algorithmic bytes,
+and TEMPI_CACHE_DIR resolution (the same rule as tempi_amd/csrc/core/env.cpp)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+# `amd-smi xgmi -m --json` on this pool's one-GPU MI355X box (ROCm 7.2.0)
+ONE_GPU = {"xgmi_metric": [[{"gpu": 0, "bdf": "0000:72:00.0", "link_metrics": {
+    "bit_rate": {"value": 38, "unit": "Gb/s"}, "max_bandwidth": {"value": 608, "unit": "Gb/s"}, "link_type": "N/A",
+    "links": [{"gpu": 0, "bdf": "0000:72:00.0", "read": "N/A", "write": "N/A"}]}}]]}
+
+
+def node(read_kb, write_kb):
+    """two GPUs, one link each way, with accumulated data counters in KB"""
+    gpus = []
+    for g in (0, 1):
+        gpus.append({"gpu": g, "link_metrics": {"links": [
+            {"gpu": 1 - g, "read": {"value": read_kb[g], "unit": "KB"}, "write": {"value": write_kb[g], "unit": "KB"}},
+            {"gpu": g, "read": "N/A", "write": "N/A"}]}})
+    return {"xgmi_metric": [gpus]}
+
+
+def fake_smi(monkeypatch, doc):
+    monkeypatch.setattr("shutil.which", lambda name: "/usr/bin/amd-smi")
+
+    def run(cmd, **kw):
+        assert cmd[:3] == ["amd-smi", "xgmi", "-m"]
+        return subprocess.CompletedProcess(cmd, 0, json.dumps(doc), "")
+
+    monkeypatch.setattr(bench.subprocess, "run", run)
+
+
+def test_one_gpu_box_has_no_xgmi_counters(monkeypatch):
+    fake_smi(monkeypatch, ONE_GPU)
+    assert bench.xgmi_snapshot() is None
+    d = bench.xgmi_delta(None, None, 11, 1000, 1.0)
+    assert d["available"] is False and "SELF" in d["note"]
+
+
+def test_xgmi_delta_per_iteration(monkeypatch):
+    fake_smi(monkeypatch, node([100, 200], [300, 400]))
+    a = bench.xgmi_snapshot()
+    assert a == {(0, 1): (100 * 1024.0, 300 * 1024.0), (1, 0): (200 * 1024.0, 400 * 1024.0)}
+    fake_smi(monkeypatch, node([100 + 1100, 200 + 1100], [300 + 1100, 400 + 1100]))
+    b = bench.xgmi_snapshot()
+    d = bench.xgmi_delta(a, b, 11, 2 * 100 * 1024, 0.5)
+    assert d["available"] and d["read_bytes"] == d["write_bytes"] == 2 * 1100 * 1024
+    assert d["per_unit_bytes"] == 2 * 100 * 1024 and d["algorithmic_per_unit_bytes"] == 2 * 100 * 1024
+    assert d["counter_GBps"] == round(2 * 1100 * 1024 / 0.5 / 1e9, 1) and d["links_reporting"] == 2
+
+
+def test_smi_units():
+    assert bench._smi_bytes({"value": 3, "unit": "KB"}) == 3072
+    assert bench._smi_bytes({"value": 2, "unit": "MB"}) == 2 << 20
+    assert bench._smi_bytes("N/A") is None
+    assert bench._smi_bytes(5) == 5.0
+
+
+@pytest.mark.parametrize("env,expect", [({"TEMPI_CACHE_DIR": "/x/c"}, "/x/c"),
+                                        ({"XDG_CACHE_HOME": "/x/xdg"}, "/x/xdg/tempi"),
+                                        ({"HOME": "/x/h"}, "/x/h/.tempi")])
+def test_cache_dir(monkeypatch, env, expect):
+    for k in ("TEMPI_CACHE_DIR", "XDG_CACHE_HOME", "HOME"):
+        monkeypatch.delenv(k, raising=False)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    assert bench.tempi_cache_dir() == expect
