@@ -45,6 +45,7 @@ typedef struct tempi_counters_t {
   uint64_t ipc_maps_replaced; /* peer mappings closed because the peer freed and replaced that allocation */
   uint64_t canary_ok;   /* peers on another GPU whose mapped memory read back right at first contact */
   uint64_t canary_fail; /* ... and those that did not (IPC with them off: host-staged transfers) */
+  uint64_t self_matched; /* messages to this same process matched inside TEMPI (no library message) */
 } tempi_counters_t;
 void tempi_get_counters(tempi_counters_t *out);
 void tempi_reset_counters(void);

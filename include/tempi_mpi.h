@@ -40,6 +40,14 @@
  *                                                    with its payload size and received
  *                                                    as its payload, into host or device
  *                                                    memory
+ *   MPI_Ssend / MPI_Bsend / MPI_Rsend / MPI_Issend / MPI_Ibsend / MPI_Irsend /
+ *   MPI_Send_init / MPI_Ssend_init / MPI_Bsend_init / MPI_Rsend_init /
+ *   MPI_Recv_init / MPI_Sendrecv_replace
+ *                    (not interposed)                forwarded; when they concern
+ *                                                    this same rank, TEMPI's self
+ *                                                    channel hands what it holds to
+ *                                                    the library first (keeps MPI
+ *                                                    matching order)
  *   MPI_Barrier      (not interposed)                keeps TEMPI operations moving
  *                                                    while it waits (a peer may need
  *                                                    this rank's progress)
@@ -109,6 +117,27 @@ int MPI_Mprobe(int source, int tag, MPI_Comm comm, MPI_Message *message, MPI_Sta
 int MPI_Improbe(int source, int tag, MPI_Comm comm, int *flag, MPI_Message *message, MPI_Status *status);
 int MPI_Mrecv(void *buf, int count, MPI_Datatype datatype, MPI_Message *message, MPI_Status *status);
 int MPI_Imrecv(void *buf, int count, MPI_Datatype datatype, MPI_Message *message, MPI_Request *request);
+int MPI_Ssend(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm);
+int MPI_Bsend(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm);
+int MPI_Rsend(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm);
+int MPI_Issend(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm,
+               MPI_Request *request);
+int MPI_Ibsend(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm,
+               MPI_Request *request);
+int MPI_Irsend(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm,
+               MPI_Request *request);
+int MPI_Send_init(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm,
+                  MPI_Request *request);
+int MPI_Ssend_init(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm,
+                   MPI_Request *request);
+int MPI_Bsend_init(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm,
+                   MPI_Request *request);
+int MPI_Rsend_init(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm,
+                   MPI_Request *request);
+int MPI_Recv_init(void *buf, int count, MPI_Datatype datatype, int source, int tag, MPI_Comm comm,
+                  MPI_Request *request);
+int MPI_Sendrecv_replace(void *buf, int count, MPI_Datatype datatype, int dest, int sendtag, int source,
+                         int recvtag, MPI_Comm comm, MPI_Status *status);
 int MPI_Barrier(MPI_Comm comm);
 int MPI_Alltoallv(const void *sendbuf, const int sendcounts[], const int sdispls[],
                   MPI_Datatype sendtype, void *recvbuf, const int recvcounts[], const int rdispls[],

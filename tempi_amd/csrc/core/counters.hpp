@@ -26,6 +26,7 @@ struct Counters {
   // first contact with a peer on another GPU: its memory read back through
   // the remote-load kernel agreed with a DMA read (ok) or did not (fail)
   uint64_t canary_ok = 0, canary_fail = 0;
+  uint64_t self_matched = 0; // messages to this process matched in TEMPI's self channel
   // kernel time of synchronous MPI_Pack / MPI_Unpack while profiling is on
   double pack_kernel_ms = 0, unpack_kernel_ms = 0;
   uint64_t pack_timed = 0, unpack_timed = 0;

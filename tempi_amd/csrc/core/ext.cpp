@@ -69,6 +69,7 @@ TEMPI_EXPORT void tempi_get_counters(tempi_counters_t *o) {
   o->ipc_maps_replaced = c.ipc_maps_replaced;
   o->canary_ok = c.canary_ok;
   o->canary_fail = c.canary_fail;
+  o->self_matched = c.self_matched;
 }
 
 TEMPI_EXPORT void tempi_reset_counters(void) { counters = Counters(); }

@@ -119,8 +119,10 @@ int isir(const void *sendbuf, const int *scounts, const int *sdispls, MPI_Dataty
         p2p::irecv(b, rcounts[p], rtype, p, tag, comm, &r, route);
       else if (p2p::host_recv_aware(p, tag, comm)) // a host block a peer's device send may reach as a descriptor
         p2p::irecv_host(b, rcounts[p], rtype, p, tag, comm, &r);
-      else
+      else {
+        p2p::self_spill(comm, p); // (a library receive from this rank: TEMPI's self channel hands over first)
         next.MPI_Irecv(b, rcounts[p], rtype, p, tag, comm, &r);
+      }
       reqs.push_back(r);
     }
   for (int p : order)
@@ -131,8 +133,10 @@ int isir(const void *sendbuf, const int *scounts, const int *sdispls, MPI_Dataty
       p2p::Route route;
       if (p2p::handles(b, scounts[p], stype, p, &route))
         p2p::isend(b, scounts[p], stype, p, tag, comm, &r, route, force);
-      else
+      else {
+        p2p::self_spill(comm, p);
         next.MPI_Isend(b, scounts[p], stype, p, tag, comm, &r);
+      }
       reqs.push_back(r);
     }
   int err = MPI_SUCCESS;
@@ -175,6 +179,7 @@ void coll_finalize() {
 
 // the application frees `comm`: drop what TEMPI cached for the handle
 void comm_release(MPI_Comm comm) {
+  p2p::self_forget(comm);
   topology::uncache(comm);
   auto it = privateComms.find(comm);
   if (it != privateComms.end()) {

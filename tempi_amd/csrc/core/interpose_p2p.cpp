@@ -26,6 +26,7 @@ TEMPI_EXPORT int MPI_Send(const void *buf, int count, MPI_Datatype datatype, int
   p2p::Route route;
   if (!p2p::handles(buf, count, datatype, dest, &route)) {
     counters.lib_sends++;
+    p2p::self_spill(comm, dest);
     if (state.active && p2p::send_gated(comm, dest)) p2p::drain_sends(comm, dest); // keep send order
     return next.MPI_Send(buf, count, datatype, dest, tag, comm);
   }
@@ -64,6 +65,7 @@ TEMPI_EXPORT int MPI_Isend(const void *buf, int count, MPI_Datatype datatype, in
     return p2p::isend(buf, count, datatype, dest, tag, comm, request, route);
   if (state.active) {
     p2p::progress(false);
+    p2p::self_spill(comm, dest);
     if (p2p::send_gated(comm, dest)) // behind a send still gathering: keep send order
       return p2p::isend_host(buf, count, datatype, dest, tag, comm, request);
   }
@@ -81,6 +83,7 @@ TEMPI_EXPORT int MPI_Irecv(void *buf, int count, MPI_Datatype datatype, int sour
   if (state.active) p2p::progress(false);
   // a host buffer: a co-located TEMPI device send may arrive as a descriptor
   if (p2p::host_recv_aware(source, tag, comm)) return p2p::irecv_host(buf, count, datatype, source, tag, comm, request);
+  p2p::self_spill(comm, source);
   counters.lib_recvs++;
   return next.MPI_Irecv(buf, count, datatype, source, tag, comm, request);
 }
@@ -301,6 +304,8 @@ TEMPI_EXPORT int MPI_Sendrecv(const void *sendbuf, int sendcount, MPI_Datatype s
                                      p2p::handles(recvbuf, recvcount, recvtype, source, &rr) ||
                                      p2p::host_recv_aware(source, recvtag, comm));
   if (!mine) {
+    p2p::self_spill(comm, dest);
+    p2p::self_spill(comm, source);
     if (state.active && p2p::send_gated(comm, dest)) p2p::drain_sends(comm, dest); // keep send order
     return next.MPI_Sendrecv(sendbuf, sendcount, sendtype, dest, sendtag, recvbuf, recvcount, recvtype, source,
                              recvtag, comm, status);
@@ -355,3 +360,62 @@ TEMPI_EXPORT int MPI_Imrecv(void *buf, int count, MPI_Datatype datatype, MPI_Mes
   if (!state.active) return next.MPI_Imrecv(buf, count, datatype, message, request);
   return p2p::imrecv(buf, count, datatype, message, request);
 }
+
+// The send modes and persistent requests TEMPI does not carry go to the
+// library unchanged -- after the self channel of the communicator spills when
+// they concern this same rank (p2p.hpp: self_spill), since the library would
+// otherwise hold a message to this rank that a receive waiting in TEMPI never
+// sees.
+#define TEMPI_SPILL_THEN(peer, call)                                                               \
+  resolve_next();                                                                                  \
+  if (state.active) p2p::self_spill(comm, peer);                                                   \
+  return call;
+
+TEMPI_EXPORT int MPI_Ssend(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm) {
+  TEMPI_SPILL_THEN(dest, next.MPI_Ssend(buf, count, datatype, dest, tag, comm))
+}
+TEMPI_EXPORT int MPI_Bsend(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm) {
+  TEMPI_SPILL_THEN(dest, next.MPI_Bsend(buf, count, datatype, dest, tag, comm))
+}
+TEMPI_EXPORT int MPI_Rsend(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm) {
+  TEMPI_SPILL_THEN(dest, next.MPI_Rsend(buf, count, datatype, dest, tag, comm))
+}
+TEMPI_EXPORT int MPI_Issend(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm,
+                            MPI_Request *request) {
+  TEMPI_SPILL_THEN(dest, next.MPI_Issend(buf, count, datatype, dest, tag, comm, request))
+}
+TEMPI_EXPORT int MPI_Ibsend(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm,
+                            MPI_Request *request) {
+  TEMPI_SPILL_THEN(dest, next.MPI_Ibsend(buf, count, datatype, dest, tag, comm, request))
+}
+TEMPI_EXPORT int MPI_Irsend(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm,
+                            MPI_Request *request) {
+  TEMPI_SPILL_THEN(dest, next.MPI_Irsend(buf, count, datatype, dest, tag, comm, request))
+}
+TEMPI_EXPORT int MPI_Send_init(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm,
+                               MPI_Request *request) {
+  TEMPI_SPILL_THEN(dest, next.MPI_Send_init(buf, count, datatype, dest, tag, comm, request))
+}
+TEMPI_EXPORT int MPI_Ssend_init(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm,
+                                MPI_Request *request) {
+  TEMPI_SPILL_THEN(dest, next.MPI_Ssend_init(buf, count, datatype, dest, tag, comm, request))
+}
+TEMPI_EXPORT int MPI_Bsend_init(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm,
+                                MPI_Request *request) {
+  TEMPI_SPILL_THEN(dest, next.MPI_Bsend_init(buf, count, datatype, dest, tag, comm, request))
+}
+TEMPI_EXPORT int MPI_Rsend_init(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm,
+                                MPI_Request *request) {
+  TEMPI_SPILL_THEN(dest, next.MPI_Rsend_init(buf, count, datatype, dest, tag, comm, request))
+}
+TEMPI_EXPORT int MPI_Recv_init(void *buf, int count, MPI_Datatype datatype, int source, int tag, MPI_Comm comm,
+                               MPI_Request *request) {
+  TEMPI_SPILL_THEN(source, next.MPI_Recv_init(buf, count, datatype, source, tag, comm, request))
+}
+TEMPI_EXPORT int MPI_Sendrecv_replace(void *buf, int count, MPI_Datatype datatype, int dest, int sendtag, int source,
+                                      int recvtag, MPI_Comm comm, MPI_Status *status) {
+  resolve_next();
+  if (state.active) p2p::self_spill(comm, source);
+  TEMPI_SPILL_THEN(dest, next.MPI_Sendrecv_replace(buf, count, datatype, dest, sendtag, source, recvtag, comm, status))
+}
+#undef TEMPI_SPILL_THEN

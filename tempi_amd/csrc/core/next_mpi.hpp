@@ -42,6 +42,18 @@
   X(MPI_Mrecv)                                                                 \
   X(MPI_Imrecv)                                                                \
   X(MPI_Barrier)                                                               \
+  X(MPI_Ssend)                                                                 \
+  X(MPI_Bsend)                                                                 \
+  X(MPI_Rsend)                                                                 \
+  X(MPI_Issend)                                                                \
+  X(MPI_Ibsend)                                                                \
+  X(MPI_Irsend)                                                                \
+  X(MPI_Send_init)                                                             \
+  X(MPI_Ssend_init)                                                            \
+  X(MPI_Bsend_init)                                                            \
+  X(MPI_Rsend_init)                                                            \
+  X(MPI_Recv_init)                                                             \
+  X(MPI_Sendrecv_replace)                                                      \
   X(MPI_Alltoallv)                                                             \
   X(MPI_Neighbor_alltoallv)                                                    \
   X(MPI_Neighbor_alltoallw)                                                    \

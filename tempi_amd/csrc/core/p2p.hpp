@@ -93,6 +93,15 @@ bool local_copy(const void *sbuf, int scount, MPI_Datatype stype, void *rbuf, in
                 MPI_Request *req);
 void start_queued();
 
+// Messages of this process to itself are matched inside TEMPI while every
+// such message of the communicator can be (p2p.cpp, "self channel"). An
+// operation on a message to / from this rank that the channel cannot carry
+// calls self_spill first: peer = the other end's rank in comm (a send's dest,
+// a receive's or probe's source, MPI_ANY_SOURCE included); no-op for other
+// ranks. self_forget drops the channel of a communicator being freed.
+void self_spill(MPI_Comm comm, int peer);
+void self_forget(MPI_Comm comm);
+
 bool send_gated(MPI_Comm comm, int dest);
 int isend_host(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Comm comm, MPI_Request *req);
 void drain_sends(MPI_Comm comm, int dest);

@@ -50,6 +50,7 @@ def test_pingpong_nd(gpu, method, total, block):
 
 @pytest.mark.parametrize("ranks,grid,env,extra", [
     (1, "48", {}, []), (2, "48", {}, []), (4, "40", {}, []), (3, "30", {}, []), (1, "128", {}, []),
+    (1, "48", {"TEMPI_NO_SELF_CHANNEL": "1"}, []), (2, "48", {"TEMPI_NO_SELF_CHANNEL": "1"}, []),
     (1, "48", {"TEMPI_NO_DIRECT": "1"}, []), (2, "40", {"TEMPI_FAULT_IPC_OPEN": "1"}, []),
     (4, "32", {"TEMPI_DATATYPE_ONESHOT": "1"}, []),
     (1, "48", {}, ["--neighbor"]), (2, "40", {}, ["--neighbor"]), (4, "32", {}, ["--neighbor"]),
@@ -235,7 +236,18 @@ def test_send_order_across_routes(gpu, n, method):
     assert rc == 0 and "RESULT errors=0" in out, out[-3000:]
 
 
+@pytest.mark.parametrize("n,env", [(1, {}), (2, {}), (1, {"TEMPI_NO_SELF_CHANNEL": "1"}), (1, {"TEMPI_NO_DIRECT": "1"}),
+                                   (1, {"TEMPI_STREAMS": "3"})])
+def test_self_channel(gpu, n, env):
+    """messages of a process to itself matched inside TEMPI: earliest send /
+    earliest receive / MPI_ANY_TAG, and the spill to the library on a host
+    send, an MPI_ANY_SOURCE receive, a probe, an MPI_Issend, a cancel"""
+    rc, out = mpi_launch.run(n, mpi_launch.py("selfchan.py"), env=env, timeout=200)
+    assert rc == 0 and "RESULT errors=0" in out, out[-4000:]
+
+
 @pytest.mark.parametrize("n,seed,env", [(1, 7, {}), (2, 7, {}), (3, 11, {}), (4, 5, {}),
+                                        (1, 23, {"TEMPI_NO_SELF_CHANNEL": "1"}), (2, 29, {"TEMPI_NO_SELF_CHANNEL": "1"}),
                                         (3, 13, {"TEMPI_STREAMS": "3"}), (2, 17, {"TEMPI_NO_IPC_COPY": "1"}),
                                         (2, 19, {"TEMPI_NO_DIRECT": "1"})])
 def test_transport_fuzz(gpu, n, seed, env):
