@@ -120,6 +120,8 @@ template <int W> struct Unroll {
 };
 
 constexpr int kBlock = TEMPI_BLOCK;
+// the interleaved tiles index whole 64-lane waves (tile + wave * 64, j * 64 + lane over kBlock entries)
+static_assert(kBlock % 64 == 0 && kBlock >= 64 && kBlock <= 1024, "packer workgroups are whole 64-lane waves");
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
@@ -549,7 +551,7 @@ template <int W, int ND> __global__ __launch_bounds__(kBlock) void unpack_il_ker
 // the rows, but the per-word path spends one 1/2/4-byte load instruction per
 // row. Here a workgroup's kBlock x 16 bytes of packed output covers rows [rl, rh] of one
 // inner segment, whose window the workgroup streams into LDS
-// with 16-byte coalesced loads (<= 16 KiB + s); each lane then gathers its 16 output bytes
+// with 16-byte coalesced loads (<= kBlock*16*kDenseRatio + s bytes); each lane then gathers its 16 output bytes
 // from LDS (ds_read_u8) and writes them with one 16-byte store -- the "LDS
 // staging to transpose narrow strided blocks into wide contiguous writes" of
 // the design. A tile whose rows straddle two segments of an outer dimension
@@ -561,6 +563,8 @@ template <int W, int ND> __global__ __launch_bounds__(kBlock) void unpack_il_ker
 constexpr int kDenseRatio = 4;
 constexpr int kDenseLds = kBlock * 16 * kDenseRatio + 512;
 constexpr int kDenseMaxBlock = 32;
+static_assert(kDenseLds <= 64 * 1024, "the dense window must fit a workgroup's LDS allocation (gfx950: 64 KiB per "
+                                      "workgroup of the CU's 160 KiB)");
 
 template <int ND>
 __global__ __launch_bounds__(kBlock) void pack_dense_kernel(const KArgs<ND> a) {
@@ -1024,8 +1028,8 @@ int run_batch(bool pack, const tempi_hip_batch_item *items, int n, hipStream_t s
 // payload once each way instead of twice. Each side keeps its own shape: the
 // virtual packed word q is decoded independently into a src and a dst offset.
 //
-// A workgroup owns kBlock * 16/W consecutive words; word j of a lane is
-// tileBase + j * kBlock + lane, so every load/store instruction of a wave
+// A workgroup owns kCopyBlock * 16/W consecutive words; word j of a lane is
+// tileBase + j * kCopyBlock + lane, so every load/store instruction of a wave
 // touches 64 consecutive words (coalesced whenever rows are longer than a few
 // words). Each side has at most kCopyND dimensions after normalisation (the
 // unbounded outermost one lives in the last slot; the unused slots in between
@@ -1033,12 +1037,14 @@ int run_batch(bool pack, const tempi_hip_batch_item *items, int n, hipStream_t s
 // caller packs + unpacks through a slab instead.
 constexpr int kCopyND = 3;
 // The copy kernels keep 256-lane workgroups: on the halo regions 128 measured
-// 2-5 % slower (tools/gpu_block_ab.sh), while the single-object packers gain
+// 2-5 % slower (round 1, profiles/r01/block_ab_s9.jsonl), while the single-object packers gain
 // from 128 (see TEMPI_BLOCK)
 #ifndef TEMPI_COPY_BLOCK
 #define TEMPI_COPY_BLOCK 256
 #endif
 constexpr int kCopyBlock = TEMPI_COPY_BLOCK;
+static_assert(kCopyBlock % 64 == 0 && kCopyBlock >= 64 && kCopyBlock <= 1024,
+              "copy kernels interleave whole 64-lane waves");
 
 struct CSide {
   char *first;
