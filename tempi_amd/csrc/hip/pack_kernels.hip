@@ -563,8 +563,9 @@ template <int W, int ND> __global__ __launch_bounds__(kBlock) void unpack_il_ker
 constexpr int kDenseRatio = 4;
 constexpr int kDenseLds = kBlock * 16 * kDenseRatio + 512;
 constexpr int kDenseMaxBlock = 32;
-static_assert(kDenseLds <= 64 * 1024, "the dense window must fit a workgroup's LDS allocation (gfx950: 64 KiB per "
-                                      "workgroup of the CU's 160 KiB)");
+// a workgroup's window must fit the CU's 160 KiB of LDS with room for a
+// second workgroup on the CU (so <= 64 KiB)
+static_assert(kDenseLds <= 64 * 1024, "dense window too large for LDS");
 
 template <int ND>
 __global__ __launch_bounds__(kBlock) void pack_dense_kernel(const KArgs<ND> a) {
