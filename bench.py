@@ -61,6 +61,8 @@ def parse():
     p.add_argument("--a2av-iters", type=int, default=20)
     p.add_argument("--no-p2p", action="store_true", help="skip configs 3 and 5 at N > 1")
     p.add_argument("--sweep", default=None, help="run the config-2 sweep and write JSON records here")
+    p.add_argument("--sweep-sizes", default=None,
+                   help="comma-separated packed sizes for --sweep (default 1 MiB, 16 MiB, 256 MiB, 1 GiB)")
     p.add_argument("--no-sweep-geomean", action="store_true",
                    help="skip the 1 GiB points of the config-2 sweep in the default line (sweep_geomean)")
     p.add_argument("--no-measure-system", action="store_true",
@@ -732,7 +734,10 @@ def main():
     try:
         assert mpi.gpu_available(), "libtempi.so found no GPU"
         if args.sweep:
-            sweep(args, mpi, torch, dev, args.sweep)
+            if args.sweep_sizes:
+                sweep(args, mpi, torch, dev, args.sweep, sizes=tuple(int(x) for x in args.sweep_sizes.split(",")))
+            else:
+                sweep(args, mpi, torch, dev, args.sweep)
             return
         rec = headline(args, mpi, torch, rank, world, pg, dev)
         if args.inner:
