@@ -498,7 +498,7 @@ def node_perf_model(args, mpi, pg, rank, world, shared_gpu):
         env["HYDRA_LAUNCHER"] = "fork"
         exe = os.path.join(tempi_amd.LIBDIR, "measure_system")
         t0 = time.perf_counter()
-        r = subprocess.run(["timeout", "-k", "10", "400", "/opt/conda/bin/mpiexec", "-n", "2", exe, "--quick", "--out",
+        r = subprocess.run(["timeout", "-k", "10", "120", "/opt/conda/bin/mpiexec", "-n", "2", exe, "--quick", "--out",
                             path], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env)
         info["measure_seconds"] = round(time.perf_counter() - t0, 1)
         info["measured_here"] = r.returncode == 0 and os.path.exists(path)
