@@ -1,6 +1,6 @@
 // apps/halo_exchange_main.cpp -- CLI for the 3D halo exchange of
 // apps/halo_lib.cpp (config 4):
-//   mpiexec -n N halo_exchange ITERS X [Y Z] [--quants N] [--radius R] [--check] [--neighbor]
+//   mpiexec -n N halo_exchange ITERS X [Y Z] [--quants N] [--radius R] [--check] [--neighbor] [--reorder]
 #include <mpi.h>
 
 #include <cstdio>
@@ -24,7 +24,9 @@ int main(int argc, char **argv) {
     else if (!std::strcmp(argv[i], "--check-control")) // a planted error the check must find
       check = 2;
     else if (!std::strcmp(argv[i], "--neighbor"))
-      neighbor = 1;
+      neighbor |= 1;
+    else if (!std::strcmp(argv[i], "--reorder")) // placed ranks (TEMPI_PLACEMENT_*)
+      neighbor |= 2;
     else if (!std::strcmp(argv[i], "--quants") && i + 1 < argc)
       nQuants = std::atoi(argv[++i]);
     else if (!std::strcmp(argv[i], "--radius") && i + 1 < argc)
@@ -33,7 +35,7 @@ int main(int argc, char **argv) {
       pos.push_back(std::atoi(argv[i]));
   }
   if (pos.size() != 2 && pos.size() != 4) {
-    if (!rank) std::fprintf(stderr, "usage: %s ITERS X [Y Z] [--quants N] [--radius R] [--check] [--neighbor]\n", argv[0]);
+    if (!rank) std::fprintf(stderr, "usage: %s ITERS X [Y Z] [--quants N] [--radius R] [--check] [--neighbor] [--reorder]\n", argv[0]);
     MPI_Abort(MPI_COMM_WORLD, 1);
   }
   std::vector<char> json(4096, 0);

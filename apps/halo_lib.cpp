@@ -15,6 +15,10 @@
 // by list position, which guarantees only equal sizes. (2) --check verifies
 // every halo byte against the value the owning rank wrote.
 //
+// --reorder: the ranks are first placed by MPI_Dist_graph_create_adjacent
+// (reorder = 1, bytes per edge as weights), and every rank plays the rank it
+// is given on that communicator (Isend/Irecv, or --neighbor on the graph).
+//
 // --neighbor: the same exchange as one MPI_Neighbor_alltoallw per quantity
 // on an MPI_Dist_graph_create_adjacent communicator (26 out-edges toward each
 // direction d, 26 in-edges from the neighbour at -d; repeated edges between
@@ -23,7 +27,7 @@
 // Library form: tempi_bench_halo() (libtempi_apps.so), called by bench.py
 // inside the driver's torch.distributed launch; the CLI wrapper is
 // apps/halo_exchange_main.cpp:
-//   halo_exchange ITERS X [Y Z] [--quants N] [--radius R] [--check] [--neighbor]
+//   halo_exchange ITERS X [Y Z] [--quants N] [--radius R] [--check] [--neighbor] [--reorder]
 // Result: one JSON object (rank 0).
 #include <hip/hip_runtime.h>
 #include <mpi.h>
@@ -144,6 +148,7 @@ tempi_bench_halo(int nIters, int gx, int gy, int gz, int nQuants, int radius, in
   int rank, size;
   MPI_Comm_rank(MPI_COMM_WORLD, &rank);
   MPI_Comm_size(MPI_COMM_WORLD, &size);
+  const int worldRank = rank; // (--reorder may give this process another rank)
   I3 global{gx, gy, gz};
 
   // one GPU per rank on the node (ranks beyond the GPU count share)
@@ -172,7 +177,38 @@ tempi_bench_halo(int nIters, int gx, int gy, int gz, int nQuants, int radius, in
       dims.x *= f;
     }
   }
-  const I3 me{rank % dims.x, (rank / dims.x) % dims.y, rank / (dims.x * dims.y)};
+  auto coords = [&](int r) { return I3{r % dims.x, (r / dims.x) % dims.y, r / (dims.x * dims.y)}; };
+  auto nbr_of = [&](I3 m, int dx, int dy, int dz) {
+    const I3 n{(m.x + dx + dims.x) % dims.x, (m.y + dy + dims.y) % dims.y, (m.z + dz + dims.z) % dims.z};
+    return n.x + n.y * dims.x + n.z * dims.x * dims.y;
+  };
+
+  // --reorder (neighbor & 2): the graph is created first, with reorder = 1
+  // and each edge's bytes as its weight, and this process then plays the
+  // rank it is given, as the reference's bench does
+  // (bench_halo_exchange.cpp:343-360); with TEMPI_PLACEMENT_* and several
+  // nodes TEMPI's placement chooses that rank
+  const bool reorder = (neighbor & 2) != 0;
+  MPI_Comm comm = MPI_COMM_WORLD, graph = MPI_COMM_NULL;
+  if (reorder) {
+    const I3 w = coords(rank);
+    std::vector<int> in, out, inW, outW;
+    for (int dz = -1; dz <= 1; ++dz)
+      for (int dy = -1; dy <= 1; ++dy)
+        for (int dx = -1; dx <= 1; ++dx) {
+          if (!dx && !dy && !dz) continue;
+          const int bytes = (dx ? radius : lcr.x) * (dy ? radius : lcr.y) * (dz ? radius : lcr.z) * 8 * nQuants;
+          out.push_back(nbr_of(w, dx, dy, dz));
+          in.push_back(nbr_of(w, -dx, -dy, -dz));
+          outW.push_back(bytes);
+          inW.push_back(bytes);
+        }
+    MPI_Dist_graph_create_adjacent(MPI_COMM_WORLD, int(in.size()), in.data(), inW.data(), int(out.size()),
+                                   out.data(), outW.data(), MPI_INFO_NULL, 1, &graph);
+    MPI_Comm_rank(graph, &rank);
+    comm = graph;
+  }
+  const I3 me = coords(rank);
   const I3 origin{me.x * lcr.x, me.y * lcr.y, me.z * lcr.z};
   const int q = 8; // bytes per quantity
   const size_t width = size_t(lcr.x + 2 * radius) * q;
@@ -232,9 +268,7 @@ tempi_bench_halo(int nIters, int gx, int gy, int gz, int nQuants, int radius, in
     for (int dy = -1; dy <= 1; ++dy)
       for (int dx = -1; dx <= 1; ++dx) {
         if (!dx && !dy && !dz) continue;
-        I3 n{(me.x + dx + dims.x) % dims.x, (me.y + dy + dims.y) % dims.y, (me.z + dz + dims.z) % dims.z};
-        Dir D{dx, dy, dz, n.x + n.y * dims.x + n.z * dims.x * dims.y, halo_type(dx, dy, dz, false),
-              halo_type(dx, dy, dz, true), 0};
+        Dir D{dx, dy, dz, nbr_of(me, dx, dy, dz), halo_type(dx, dy, dz, false), halo_type(dx, dy, dz, true), 0};
         MPI_Type_size(D.interior, &D.bytes);
         dirs.push_back(D);
       }
@@ -250,11 +284,11 @@ tempi_bench_halo(int nIters, int gx, int gy, int gz, int nQuants, int radius, in
 
   // neighbourhood form: out-edge i toward dirs[i], in-edge i from the
   // neighbour at -dirs[i] (whose send toward dirs[i] fills exterior(-dirs[i]))
-  MPI_Comm graph = MPI_COMM_NULL;
   std::vector<int> nbrIn, nbrOut, ncount(dirs.size(), 1);
+  long long graphErrors = 0; // the placed graph's neighbours against this rank's own
   std::vector<MPI_Aint> ndispl(dirs.size(), 0);
   std::vector<MPI_Datatype> nsend, nrecv;
-  if (neighbor) {
+  if (neighbor & 1) {
     for (const Dir &D : dirs) {
       nbrOut.push_back(D.nbr);
       nsend.push_back(D.interior);
@@ -264,8 +298,18 @@ tempi_bench_halo(int nIters, int gx, int gy, int gz, int nQuants, int radius, in
           nrecv.push_back(E.exterior);
         }
     }
-    MPI_Dist_graph_create_adjacent(MPI_COMM_WORLD, int(nbrIn.size()), nbrIn.data(), MPI_UNWEIGHTED,
-                                   int(nbrOut.size()), nbrOut.data(), MPI_UNWEIGHTED, MPI_INFO_NULL, 0, &graph);
+    if (!reorder)
+      MPI_Dist_graph_create_adjacent(MPI_COMM_WORLD, int(nbrIn.size()), nbrIn.data(), MPI_UNWEIGHTED,
+                                     int(nbrOut.size()), nbrOut.data(), MPI_UNWEIGHTED, MPI_INFO_NULL, 0, &graph);
+  }
+  if (reorder) {
+    std::vector<int> gin(dirs.size()), gout(dirs.size()), gw(dirs.size());
+    MPI_Dist_graph_neighbors(graph, int(dirs.size()), gin.data(), gw.data(), int(dirs.size()), gout.data(),
+                             gw.data());
+    for (size_t i = 0; i < dirs.size(); ++i) {
+      graphErrors += gout[i] != dirs[i].nbr;
+      graphErrors += gin[i] != nbr_of(me, -dirs[i].dx, -dirs[i].dy, -dirs[i].dz);
+    }
   }
 
   std::vector<double> times;
@@ -281,7 +325,7 @@ tempi_bench_halo(int nIters, int gx, int gy, int gz, int nQuants, int radius, in
     for (int sub = 0; sub < 3; ++sub) {
       MPI_Barrier(MPI_COMM_WORLD);
       const double t0 = MPI_Wtime();
-      if (neighbor) {
+      if (neighbor & 1) {
         for (int qi = 0; qi < nQuants; ++qi)
           MPI_Neighbor_alltoallw(bufs[size_t(qi)], ncount.data(), ndispl.data(), nsend.data(), bufs[size_t(qi)],
                                  ncount.data(), ndispl.data(), nrecv.data(), graph);
@@ -293,13 +337,12 @@ tempi_bench_halo(int nIters, int gx, int gy, int gz, int nQuants, int radius, in
       size_t ri = 0;
       for (int qi = 0; qi < nQuants; ++qi)
         for (const Dir &D : dirs)
-          MPI_Isend(bufs[size_t(qi)], 1, D.interior, D.nbr, dir_code(D.dx, D.dy, D.dz) + 27 * qi, MPI_COMM_WORLD,
-                    &reqs[ri++]);
+          MPI_Isend(bufs[size_t(qi)], 1, D.interior, D.nbr, dir_code(D.dx, D.dy, D.dz) + 27 * qi, comm, &reqs[ri++]);
       const double t1 = MPI_Wtime();
       for (int qi = 0; qi < nQuants; ++qi)
         for (const Dir &D : dirs)
-          MPI_Irecv(bufs[size_t(qi)], 1, D.exterior, D.nbr, dir_code(-D.dx, -D.dy, -D.dz) + 27 * qi,
-                    MPI_COMM_WORLD, &reqs[ri++]);
+          MPI_Irecv(bufs[size_t(qi)], 1, D.exterior, D.nbr, dir_code(-D.dx, -D.dy, -D.dz) + 27 * qi, comm,
+                    &reqs[ri++]);
       const double t2 = MPI_Wtime();
       for (MPI_Request &r : reqs) MPI_Wait(&r, MPI_STATUS_IGNORE);
       const double t3 = MPI_Wtime();
@@ -312,7 +355,7 @@ tempi_bench_halo(int nIters, int gx, int gy, int gz, int nQuants, int radius, in
     if (it >= warm) times.push_back(exch);
   }
 
-  long long errors = 0;
+  long long errors = graphErrors;
   if (check) {
     // check == 2: a negative control -- one planted wrong cell (rank 0,
     // quantity 0, the halo corner at (0, 0, 0)) must be counted
@@ -348,8 +391,8 @@ tempi_bench_halo(int nIters, int gx, int gy, int gz, int nQuants, int radius, in
       }
       HIPCHECK(hipFree(dErr));
     }
-    MPI_Allreduce(MPI_IN_PLACE, &errors, 1, MPI_LONG_LONG, MPI_SUM, MPI_COMM_WORLD);
   }
+  MPI_Allreduce(MPI_IN_PLACE, &errors, 1, MPI_LONG_LONG, MPI_SUM, MPI_COMM_WORLD);
 
   double maxLinkAll = maxLink;
   MPI_Allreduce(MPI_IN_PLACE, &maxLinkAll, 1, MPI_DOUBLE, MPI_MAX, MPI_COMM_WORLD);
@@ -365,19 +408,21 @@ tempi_bench_halo(int nIters, int gx, int gy, int gz, int nQuants, int radius, in
     }
   MPI_Allreduce(MPI_IN_PLACE, remote, 2, MPI_DOUBLE, MPI_SUM, MPI_COMM_WORLD);
   const double tIter = trimean(times);
-  if (rank == 0 && json && jsonCap > 0) {
+  if (worldRank == 0 && json && jsonCap > 0) {
     std::snprintf(json, size_t(jsonCap), "{\"ranks\": %d, \"global\": [%d, %d, %d], \"dims\": [%d, %d, %d], \"lcr\": [%d, %d, %d], "
                 "\"quants\": %d, \"radius\": %d, \"iters\": %d, \"us_per_iter\": %.2f, \"us_min\": %.2f, "
                 "\"payload_bytes_per_iter_per_rank0\": %.0f, \"total_bytes_per_iter\": %.0f, "
                 "\"max_peer_bytes_per_iter\": %.0f, \"aggregate_GBps\": %.2f, \"busiest_link_GBps\": %.2f, "
                 "\"remote_bytes_per_iter\": %.0f, \"links_used\": %.0f, "
-                "\"checked\": %s, \"errors\": %lld, \"api\": \"%s\", \"buffers\": \"%s\", \"rank0_us_per_iter\": {\"isend\": %.1f, "
+                "\"checked\": %s, \"errors\": %lld, \"api\": \"%s\", \"reorder\": %s, \"buffers\": \"%s\", "
+                "\"rank0_us_per_iter\": {\"isend\": %.1f, "
                 "\"irecv\": %.1f, \"wait\": %.1f}}\n",
                 size, global.x, global.y, global.z, dims.x, dims.y, dims.z, lcr.x, lcr.y, lcr.z, nQuants, radius,
                 nIters, tIter * 1e6, *std::min_element(times.begin(), times.end()) * 1e6, bytesPerIter, totalBytes,
                 maxLinkAll, totalBytes / tIter / 1e9, maxLinkAll / tIter / 1e9, remote[0], remote[1],
                 check ? "true" : "false", errors,
-                neighbor ? "MPI_Neighbor_alltoallw" : "MPI_Isend/MPI_Irecv/MPI_Wait", onHost ? "host" : "device",
+                (neighbor & 1) ? "MPI_Neighbor_alltoallw" : "MPI_Isend/MPI_Irecv/MPI_Wait", reorder ? "true" : "false",
+                onHost ? "host" : "device",
                 tIsend / nIters * 1e6, tIrecv / nIters * 1e6, tWait / nIters * 1e6);
   }
   if (graph != MPI_COMM_NULL) MPI_Comm_free(&graph);

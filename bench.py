@@ -67,6 +67,9 @@ def parse():
                    help="skip the 1 GiB points of the config-2 sweep in the default line (sweep_geomean)")
     p.add_argument("--no-measure-system", action="store_true",
                    help="N > 1: do not measure this node's perf.json when it is missing")
+    p.add_argument("--extras-deadline", type=float, default=900.0,
+                   help="seconds after the headline within which the line's other sections must finish; past it "
+                        "rank 0 prints the line so far, marked incomplete, and every rank exits")
     p.add_argument("--inner", action="store_true", help=argparse.SUPPRESS)  # child for --traffic
     return p.parse_args()
 
@@ -425,7 +428,7 @@ def halo(args, mpi, world, grid=None):
     g = grid or args.halo_grid
     rc = L.tempi_bench_halo(args.halo_iters, g, g, g, 8, 3, 0, 0, 0, buf, 4096)
     if rc != 0:
-        raise SystemExit(f"halo exchange failed rc={rc}")
+        raise RuntimeError(f"halo exchange failed rc={rc}")
     if not buf.value:
         return None
     r = json.loads(buf.value.decode())
@@ -594,7 +597,7 @@ def pingpong(args, world):
         buf = ctypes.create_string_buffer(1024)
         rc = L.tempi_bench_pingpong(args.pp_iters, total, bl, 512, 0, 0, buf, 1024)
         if rc != 0:
-            raise SystemExit(f"pingpong failed rc={rc}")
+            raise RuntimeError(f"pingpong failed rc={rc}")
         if buf.value:
             r = json.loads(buf.value.decode())
             r["xgmi_frac"] = round(r["GBps"] / XGMI_LINK_GBS, 4)
@@ -616,7 +619,7 @@ def alltoallv(args, world):
         buf = ctypes.create_string_buffer(1024)
         rc = L.tempi_bench_alltoallv(args.a2av_iters, scale, density, 101, 0, 0, buf, 1024)
         if rc != 0:
-            raise SystemExit(f"alltoallv failed rc={rc}")
+            raise RuntimeError(f"alltoallv failed rc={rc}")
         if buf.value:
             r = json.loads(buf.value.decode())
             # every GPU pair has its own xGMI link: the largest pairwise
@@ -720,6 +723,46 @@ def sweep_geomean(args, mpi, torch, dev):
                         "MPI_Unpack from HIP events on TEMPI's stream"}
 
 
+class Sections:
+    """The sections after the headline (sweep, halo, configs 3 and 5,
+    traffic, CPU baselines) are evidence beside the metric, not the metric:
+    one that raises is recorded as {"error": ...} in its field, and one that
+    has not finished `deadline` seconds after the headline (a hang on a node
+    this pool never ran, e.g. the first cross-GPU IPC) ends the run with the
+    line so far, its "incomplete" field naming the section."""
+
+    def __init__(self, rec, rank, deadline):
+        import threading
+
+        self.rec, self.rank, self.current = rec, rank, "start"
+        self.timer = threading.Timer(deadline, self._expire, args=(deadline,))
+        self.timer.daemon = True
+        self.timer.start()
+
+    def _expire(self, deadline):
+        if self.rank == 0:
+            line = dict(self.rec)
+            line["incomplete"] = {"section": self.current, "deadline_s": deadline}
+            try:
+                print(json.dumps(line), flush=True)
+            except Exception as e:  # a section was mutating the record
+                print(json.dumps({k: line[k] for k in ("metric", "value", "unit", "n_gpus")} |
+                                 {"incomplete": {"section": self.current, "deadline_s": deadline,
+                                                 "print_error": str(e)}}), flush=True)
+        sys.stdout.flush()
+        os._exit(0)
+
+    def run(self, name, fn, *a, **kw):
+        self.current = name
+        try:
+            return fn(*a, **kw)
+        except Exception as e:
+            return {"error": f"{type(e).__name__}: {e}"}
+
+    def done(self):
+        self.timer.cancel()
+
+
 def main():
     args = parse()
     rank, world, local, pg, keep = dist_setup(args)
@@ -743,24 +786,25 @@ def main():
         if args.inner:
             return
         torch.cuda.empty_cache()
+        sec = Sections(rec, rank, args.extras_deadline)
         if world == 1 and not args.no_sweep_geomean:
-            rec["sweep_geomean"] = sweep_geomean(args, mpi, torch, dev)
+            rec["sweep_geomean"] = sec.run("sweep_geomean", sweep_geomean, args, mpi, torch, dev)
             torch.cuda.empty_cache()
         shared_gpu = world > max(torch.cuda.device_count(), 1)
         if world > 1:
-            pm = node_perf_model(args, mpi, pg, rank, world, shared_gpu)
+            pm = sec.run("perf_model", node_perf_model, args, mpi, pg, rank, world, shared_gpu)
             if rank == 0:
                 rec["perf_model"] = pm
         if not args.no_halo:
             barrier(pg)
             snap0 = xgmi_snapshot() if world > 1 and rank == 0 else None
             t0 = time.perf_counter()
-            h = halo(args, mpi, world)
+            h = sec.run("halo", halo, args, mpi, world)
             barrier(pg)
             el = time.perf_counter() - t0
             if rank == 0:
                 rec["halo"] = h
-                if world > 1 and h:
+                if world > 1 and h and "error" not in h:
                     iters = args.halo_iters + 1  # the app's warm-up iteration moves the same bytes
                     x = xgmi_delta(snap0, xgmi_snapshot(), iters,
                                    (h.get("roofline") or {}).get("remote_bytes_per_iter", 0), el)
@@ -769,28 +813,35 @@ def main():
                                      "the algorithmic fractions above only say the bytes never left HBM")
                     h["xgmi_counters"] = x
             if world > 1:  # the reference scripts' weak scaling: 512 * N^(1/3) per edge
-                hw = halo(args, mpi, world, grid=int(round(args.halo_grid * world ** (1.0 / 3.0))))
+                hw = sec.run("halo_weak", halo, args, mpi, world,
+                             grid=int(round(args.halo_grid * world ** (1.0 / 3.0))))
                 if rank == 0:
                     rec["halo_weak"] = hw
         if world > 1 and not args.no_p2p:
-            pp = pingpong(args, world)
-            a2 = alltoallv(args, world)
+            barrier(pg)
+            pp = sec.run("pingpong", pingpong, args, world)
+            barrier(pg)
+            a2 = sec.run("alltoallv", alltoallv, args, world)
             if rank == 0:
                 rec["pingpong"] = pp
                 rec["alltoallv"] = a2
         if rank == 0 and world == 1:
             if not args.no_traffic:
-                tr = run_traffic_passes(args, "pack_kernel")
-                if tr:
+                tr = sec.run("traffic", run_traffic_passes, args, "pack_kernel")
+                if isinstance(tr, dict):
+                    rec["roofline"]["traffic_error"] = tr["error"]
+                elif tr:
                     rec["roofline"]["traffic"] = int(tr[0] + tr[1])
                     rec["roofline"]["traffic_read"] = int(tr[0])
                     rec["roofline"]["traffic_write"] = int(tr[1])
                     rec["roofline"]["traffic_source"] = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, "
                                                          "per launch of pack_kernel/unpack_kernel, FETCH_SIZE x2 "
                                                          "(gfx950)")
-                if "halo" in rec and rec["halo"]:
-                    ht = halo_traffic(args)
-                    if ht:
+                if rec.get("halo") and "error" not in rec["halo"]:
+                    ht = sec.run("halo_traffic", halo_traffic, args)
+                    if isinstance(ht, dict):
+                        rec["halo"]["roofline"]["traffic_error"] = ht["error"]
+                    elif ht:
                         hr = rec["halo"]["roofline"]
                         tr_iter = ht[0] + ht[1]
                         lb = tr_iter / (HBM_ACHIEVABLE_GBS * 1e9)
@@ -803,12 +854,14 @@ def main():
                                                 "copy kernels of halo_exchange 3 GRID, per iteration, FETCH_SIZE x2; "
                                                 "bound at the 6.3 TB/s achievable rate")
             if not args.no_cpu_baseline:
-                rec["cpu_baseline"] = cpu_baseline(mpi, args.pitch, args.block, args.cpu_seconds)
-                lb = library_path_baselines(args)
+                rec["cpu_baseline"] = sec.run("cpu_baseline", cpu_baseline, mpi, args.pitch, args.block,
+                                              args.cpu_seconds)
+                lb = sec.run("cpu_baselines_configs_3_5", library_path_baselines, args)
                 if lb:
                     rec["cpu_baselines_configs_3_5"] = lb
-                    if "halo" in lb and rec.get("halo"):
+                    if "halo" in lb and rec.get("halo") and "error" not in rec["halo"]:
                         rec["halo"]["cpu_baseline"] = lb["halo"]
+        sec.done()
         if rank == 0:
             print(json.dumps(rec), flush=True)
     finally:

@@ -97,6 +97,23 @@ void tempi_set_datatype_method(int method);
    (tools/measure_system repeats a measurement until they do) */
 int tempi_sp800_90b_iid(const double *samples, int n, int perms, uint64_t seed);
 
+/* rank placement (MPI_Dist_graph_create_adjacent with reorder = 1 and
+   TEMPI_PLACEMENT_KAHIP / _METIS / _RANDOM; /root/reference/src/
+   dist_graph_create_adjacent.cpp:55-470). tempi_partition splits the graph
+   given as CSR (xadj[n + 1], adjncy; adjwgt NULL = unit weights; each entry
+   u -> v adds its weight to the undirected edge {u, v}, self loops ignored)
+   into nparts parts of sizes[k] vertices (NULL: n / nparts each). method 0:
+   TEMPI's partitioner, 1: the reference's random rule (partition.cpp:27-34,
+   one generator seeded 0 per process). Writes part[n] and returns the edge
+   cut, or -1 for bad input. */
+int64_t tempi_partition(int n, const int *xadj, const int *adjncy, const int *adjwgt, int nparts,
+                        const int *sizes, int method, int *part);
+/* the last placement this process took part in: out[0] 1 if any, [1] nodes,
+   [2] method (1 random, 2 partitioner), [3] this process's new rank, [4] the
+   edge cut of the library's rank order, [5] the placed edge cut (rank 0's
+   graph; 0 for random). Returns out[0]. */
+int tempi_placement_info(int64_t out[6]);
+
 #ifdef __cplusplus
 }
 #endif

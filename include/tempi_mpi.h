@@ -58,10 +58,14 @@
  *   MPI_Neighbor_alltoallv  src/neighbor_alltoallv.cpp:12-24 (passthrough
  *                    there)                          same route as alltoallw
  *   MPI_Dist_graph_create_adjacent  src/dist_graph_create_adjacent.cpp:55-470
+ *                    rank placement with reorder = 1 and TEMPI_PLACEMENT_
+ *                    {KAHIP,METIS,RANDOM} when the communicator spans several
+ *                    nodes (TEMPI's own partitioner for KAHIP/METIS); the new
+ *                    communicator is built in application rank order
  *   MPI_Dist_graph_neighbors        src/dist_graph_neighbors.cpp:13-49
- *   MPI_Comm_rank    src/comm_rank.cpp:13-27         these three forward
- *                    unchanged: they exist for KaHIP/METIS rank placement,
- *                    which is out of scope (a no-op on one node: SURVEY F12)
+ *   MPI_Comm_rank    src/comm_rank.cpp:13-27         these two forward
+ *                    unchanged: the placed communicator's library ranks are
+ *                    the application's, so there is nothing to translate
  *   MPI_Comm_free    src/comm_free.cpp:13-19         drop per-handle caches
  *
  * Error behaviour: return codes of the library pass through unchanged. Where

@@ -32,6 +32,10 @@ void read_environment() {
   if (has("TEMPI_DATATYPE_IPC")) e.datatype = DatatypeMethod::IPC;
   if (has("TEMPI_DATATYPE_AUTO")) e.datatype = DatatypeMethod::AUTO;
 
+  // the reference's order (env.cpp:51-69): the last one present wins
+  if (has("TEMPI_PLACEMENT_METIS") || has("TEMPI_PLACEMENT_KAHIP")) e.placement = PlacementMethod::PARTITION;
+  if (has("TEMPI_PLACEMENT_RANDOM")) e.placement = PlacementMethod::RANDOM;
+
   if (has("TEMPI_CONTIGUOUS_STAGED")) e.contiguous = ContiguousMethod::STAGED;
   if (has("TEMPI_CONTIGUOUS_AUTO")) e.contiguous = ContiguousMethod::AUTO;
 

@@ -4,6 +4,8 @@
 //   TEMPI_DATATYPE_STAGED  (the reference has the enum value but no variable)
 //   TEMPI_DATATYPE_IPC     (MI355X intra-node device-to-device transport)
 //   TEMPI_LOG_LEVEL=<level>
+// TEMPI_PLACEMENT_KAHIP and TEMPI_PLACEMENT_METIS both select TEMPI's own
+// partitioner (core/placement.hpp): neither library is in this image.
 #pragma once
 
 #include <string>
@@ -13,6 +15,7 @@ namespace tempi {
 enum class DatatypeMethod { AUTO, ONESHOT, DEVICE, STAGED, IPC };
 enum class ContiguousMethod { NONE, AUTO, STAGED };
 enum class AlltoallvMethod { NONE, AUTO, REMOTE_FIRST, STAGED, ISIR_STAGED, ISIR_REMOTE_STAGED };
+enum class PlacementMethod { NONE, RANDOM, PARTITION };
 
 struct Environment {
   bool noTempi = false;      // TEMPI_DISABLE
@@ -21,6 +24,7 @@ struct Environment {
   DatatypeMethod datatype = DatatypeMethod::AUTO;
   ContiguousMethod contiguous = ContiguousMethod::NONE;
   AlltoallvMethod alltoallv = AlltoallvMethod::AUTO;
+  PlacementMethod placement = PlacementMethod::NONE; // TEMPI_PLACEMENT_{KAHIP,METIS,RANDOM}
   std::string cacheDir;
 };
 

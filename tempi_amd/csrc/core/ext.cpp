@@ -6,6 +6,7 @@
 #include "gpu.hpp"
 #include "p2p.hpp"
 #include "perf_model.hpp"
+#include "placement.hpp"
 #include "state.hpp"
 #include "type_cache.hpp"
 
@@ -106,7 +107,7 @@ TEMPI_EXPORT int64_t tempi_mpi_constant(const char *name, int *found) {
       H(MPI_PROC_NULL), H(MPI_SUM), H(MPI_MAX), H(MPI_MIN), H(MPI_THREAD_SINGLE),
       H(MPI_THREAD_FUNNELED), H(MPI_THREAD_SERIALIZED), H(MPI_THREAD_MULTIPLE),
       H(MPI_MAX_PROCESSOR_NAME), H(MPI_UNDEFINED),
-      P(MPI_STATUS_IGNORE), P(MPI_STATUSES_IGNORE), P(MPI_IN_PLACE), P(MPI_UNWEIGHTED), H(MPI_INFO_NULL),
+      P(MPI_STATUS_IGNORE), P(MPI_STATUSES_IGNORE), P(MPI_IN_PLACE), P(MPI_UNWEIGHTED), P(MPI_WEIGHTS_EMPTY), H(MPI_INFO_NULL),
       H(MPI_ERRORS_RETURN), H(MPI_ERRORS_ARE_FATAL), H(MPI_MESSAGE_NULL), H(MPI_MESSAGE_NO_PROC),
       {"sizeof(MPI_Message)", int64_t(sizeof(MPI_Message))},
       {"sizeof(MPI_Status)", int64_t(sizeof(MPI_Status))},
@@ -175,4 +176,38 @@ TEMPI_EXPORT void tempi_set_datatype_method(int m) {
   static const DatatypeMethod map[] = {DatatypeMethod::AUTO, DatatypeMethod::ONESHOT, DatatypeMethod::DEVICE,
                                        DatatypeMethod::STAGED, DatatypeMethod::IPC};
   if (m >= 0 && m < 5) env.datatype = map[m];
+}
+
+// ---- rank placement (core/placement.hpp)
+
+TEMPI_EXPORT int64_t tempi_partition(int n, const int *xadj, const int *adjncy, const int *adjwgt, int nparts,
+                                     const int *sizes, int method, int *part) {
+  if (n < 0 || nparts < 1 || !part || (n > 0 && (!xadj || !adjncy))) return -1;
+  std::vector<int> sz(size_t(nparts), n / nparts);
+  if (sizes) {
+    sz.assign(sizes, sizes + nparts);
+  } else if (n % nparts) {
+    return -1;
+  }
+  int64_t total = 0;
+  for (int s : sz) total += s;
+  if (total != n) return -1;
+  std::vector<placement::Edge> edges;
+  for (int u = 0; u < n; ++u)
+    for (int e = xadj[u]; e < xadj[u + 1]; ++e) edges.push_back({u, adjncy[e], adjwgt ? int64_t(adjwgt[e]) : 1});
+  const placement::Graph g = placement::make_graph(n, edges);
+  const std::vector<int> p = method == 1 ? placement::random_parts(sz) : placement::partition(g, sz);
+  std::copy(p.begin(), p.end(), part);
+  return placement::edge_cut(g, p);
+}
+
+TEMPI_EXPORT int tempi_placement_info(int64_t out[6]) {
+  const placement::Info i = placement::last();
+  out[0] = i.placed;
+  out[1] = i.nodes;
+  out[2] = i.method;
+  out[3] = i.appRank;
+  out[4] = i.cutIdentity;
+  out[5] = i.cutPlaced;
+  return i.placed;
 }

@@ -12,12 +12,15 @@
 //                           reads device memory from the host). Here it takes
 //                           the same per-edge route as alltoallw when any block
 //                           is on the GPU.
-//   MPI_Dist_graph_create_adjacent, MPI_Dist_graph_neighbors, MPI_Comm_rank
-//                           reference: src/dist_graph_create_adjacent.cpp:55-470,
-//                           src/dist_graph_neighbors.cpp:13-49, src/comm_rank.cpp:13-27.
-//                           They exist there for KaHIP/METIS rank placement,
-//                           out of scope here (a no-op on one node: SURVEY F12),
-//                           so the application and library ranks coincide and
+//   MPI_Dist_graph_create_adjacent  reference: src/dist_graph_create_adjacent.cpp:55-470
+//                           -> placement::create (core/placement.hpp) when
+//                           reorder = 1, TEMPI_PLACEMENT_* is set and the
+//                           communicator spans several nodes.
+//   MPI_Dist_graph_neighbors, MPI_Comm_rank
+//                           reference: src/dist_graph_neighbors.cpp:13-49,
+//                           src/comm_rank.cpp:13-27 translate library ranks to
+//                           application ranks there. A placed communicator is
+//                           created in the application's rank order here, so
 //                           these forward unchanged.
 //   MPI_Comm_free           reference: src/comm_free.cpp:13-19 -- drop the
 //                           handle's cached state (world-rank map, private
@@ -35,6 +38,7 @@
 #include "gpu.hpp"
 #include "next_mpi.hpp"
 #include "p2p.hpp"
+#include "placement.hpp"
 #include "state.hpp"
 #include "type_cache.hpp"
 
@@ -200,6 +204,11 @@ TEMPI_EXPORT int MPI_Dist_graph_create_adjacent(MPI_Comm comm_old, int indegree,
                                                 const int destweights[], MPI_Info info, int reorder,
                                                 MPI_Comm *comm_dist_graph) {
   resolve_next();
+  TEMPI_RANGE("MPI_Dist_graph_create_adjacent");
+  int rc = MPI_SUCCESS;
+  if (state.active && placement::create(comm_old, indegree, sources, sourceweights, outdegree, destinations,
+                                        destweights, info, reorder, comm_dist_graph, &rc))
+    return rc;
   return next.MPI_Dist_graph_create_adjacent(comm_old, indegree, sources, sourceweights, outdegree, destinations,
                                              destweights, info, reorder, comm_dist_graph);
 }

@@ -85,6 +85,8 @@ bool colocated_world(int w) {
   return nodeOf[size_t(w)] == myNode;
 }
 
+int node_of_world(int w) { return w >= 0 && size_t(w) < nodeOf.size() ? nodeOf[size_t(w)] : -1; }
+
 bool colocated(MPI_Comm comm, int rank) { return colocated_world(world_rank(comm, rank)); }
 
 int node_local_rank() { return localRank; }

@@ -82,6 +82,10 @@ class MPI:
         L.tempi_get_stream.argtypes = [ctypes.c_int]
         L.tempi_version.restype = ctypes.c_char_p
         L.MPI_Wtime.restype = ctypes.c_double
+        L.tempi_partition.restype = ctypes.c_int64
+        I = ctypes.POINTER(ctypes.c_int)
+        L.tempi_partition.argtypes = [ctypes.c_int, I, I, I, ctypes.c_int, I, ctypes.c_int, I]
+        L.tempi_placement_info.argtypes = [ctypes.POINTER(ctypes.c_int64)]
         self.initialized = False
 
     # ------------------------------------------------------------- plumbing
@@ -424,23 +428,43 @@ class MPI:
                    self.h(self.COMM_WORLD if comm is None else comm))
 
     # ------------------------------------------------ topologies / neighbours
-    def Dist_graph_create_adjacent(self, sources, destinations, reorder=False, comm=None):
+    def Dist_graph_create_adjacent(self, sources, destinations, reorder=False, comm=None, sourceweights=None,
+                                   destweights=None):
+        """weights None: MPI_UNWEIGHTED (both or neither)"""
         A = ctypes.c_int * max(len(sources), 1)
         B = ctypes.c_int * max(len(destinations), 1)
         out = self.Handle()
         unweighted = ctypes.c_void_p(self.const("MPI_UNWEIGHTED"))
+        empty = ctypes.c_void_p(self.const("MPI_WEIGHTS_EMPTY"))
+        sw = unweighted if sourceweights is None else (A(*sourceweights) if sources else empty)
+        dw = unweighted if destweights is None else (B(*destweights) if destinations else empty)
         self._call("MPI_Dist_graph_create_adjacent", self.h(self.COMM_WORLD if comm is None else comm),
-                   len(sources), A(*sources), unweighted, len(destinations), B(*destinations), unweighted,
+                   len(sources), A(*sources), sw, len(destinations), B(*destinations), dw,
                    self.h(self.const("MPI_INFO_NULL")), int(reorder), ctypes.byref(out))
         return out.value
 
-    def Dist_graph_neighbors(self, comm, indeg, outdeg):
+    def Dist_graph_neighbors(self, comm, indeg, outdeg, weights=False):
+        """(sources, destinations), plus (sourceweights, destweights) when
+        weights is True"""
         A = ctypes.c_int * max(indeg, 1)
         B = ctypes.c_int * max(outdeg, 1)
         s, d = A(), B()
+        if weights:
+            sw, dw = A(), B()
+            self._call("MPI_Dist_graph_neighbors", self.h(comm), indeg, s, sw, outdeg, d, dw)
+            return list(s)[:indeg], list(d)[:outdeg], list(sw)[:indeg], list(dw)[:outdeg]
         unweighted = ctypes.c_void_p(self.const("MPI_UNWEIGHTED"))
         self._call("MPI_Dist_graph_neighbors", self.h(comm), indeg, s, unweighted, outdeg, d, unweighted)
         return list(s)[:indeg], list(d)[:outdeg]
+
+    def Allgather_int(self, value, comm=None):
+        """every rank's int, in rank order of `comm`"""
+        n = self.Comm_size(comm)
+        out = (ctypes.c_int * n)()
+        mine = ctypes.c_int(value)
+        self._call("MPI_Allgather", ctypes.byref(mine), 1, self.h(self.INT), out, 1, self.h(self.INT),
+                   self.h(self.COMM_WORLD if comm is None else comm))
+        return list(out)
 
     def Cart_create(self, dims, periods, reorder=False, comm=None):
         n = len(dims)
@@ -512,6 +536,23 @@ class MPI:
         k = KernelTimes()
         self.L.tempi_get_kernel_times(ctypes.byref(k))
         return {"pack_ms": k.pack_ms, "unpack_ms": k.unpack_ms, "packs": k.packs, "unpacks": k.unpacks}
+
+    def partition(self, xadj, adjncy, adjwgt, nparts, sizes=None, method=0):
+        """tempi_partition: (part list, edge cut); cut -1 for bad input"""
+        n = len(xadj) - 1
+        I = ctypes.c_int
+        part = (I * max(n, 1))()
+        w = (I * max(len(adjwgt), 1))(*adjwgt) if adjwgt is not None else None
+        sz = (I * nparts)(*sizes) if sizes is not None else None
+        cut = self.L.tempi_partition(n, (I * len(xadj))(*xadj), (I * max(len(adjncy), 1))(*adjncy), w, nparts, sz,
+                                     method, part)
+        return list(part)[:n], cut
+
+    def placement_info(self):
+        """the last rank placement of this process (tempi_placement_info)"""
+        out = (ctypes.c_int64 * 6)()
+        self.L.tempi_placement_info(out)
+        return dict(zip(("placed", "nodes", "method", "app_rank", "cut_identity", "cut_placed"), list(out)))
 
     def stream(self, device=0):
         return self.L.tempi_get_stream(device)

@@ -25,10 +25,14 @@ def _json(out):
 
 @pytest.mark.parametrize("mode", list(MODES))
 @pytest.mark.parametrize("ranks,grid,extra", [(1, "24", []), (2, "24", []), (4, "24", []), (8, "24", []),
-                                              (8, "24", ["--neighbor"]), (3, "18", [])])
+                                              (8, "24", ["--neighbor"]), (3, "18", []),
+                                              (8, "24", ["--reorder"]), (8, "24", ["--reorder", "--neighbor"])])
 def test_halo_host(mode, ranks, grid, extra):
+    env = dict(MODES[mode])
+    if "--reorder" in extra:  # placement over two fake nodes (the library ignores it: ranks unchanged)
+        env.update(TEMPI_PLACEMENT_KAHIP="", TEMPI_FAKE_NODE_SIZE="4")
     rc, out = mpi_launch.run(ranks, [os.path.join(LIB, "halo_exchange"), "2", grid, "--quants", "2", "--check"] + extra,
-                             env=MODES[mode], timeout=200)
+                             env=env, timeout=200)
     r = _json(out)
     assert rc == 0 and r["checked"] and r["errors"] == 0 and r["buffers"] == "host", out[-3000:]
     if ranks == 8:

@@ -74,3 +74,23 @@ def test_cache_dir(monkeypatch, env, expect):
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     assert bench.tempi_cache_dir() == expect
+
+
+def test_section_error_is_recorded():
+    sec = bench.Sections({"metric": "m"}, 0, 60.0)
+    try:
+        r = sec.run("halo", lambda: (_ for _ in ()).throw(RuntimeError("halo exchange failed rc=3")))
+    finally:
+        sec.done()
+    assert r == {"error": "RuntimeError: halo exchange failed rc=3"}
+
+
+def test_section_deadline_prints_the_line_so_far():
+    code = ("import sys, time; sys.path.insert(0, %r); import bench\n"
+            "rec = {'metric': 'm', 'value': 1.0, 'unit': 'GB/s', 'n_gpus': 1}\n"
+            "sec = bench.Sections(rec, 0, 0.5)\n"
+            "sec.run('halo', time.sleep, 30)\n") % ROOT
+    r = subprocess.run([sys.executable, "-c", code], stdout=subprocess.PIPE, text=True, timeout=60)
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert r.returncode == 0 and line["value"] == 1.0
+    assert line["incomplete"] == {"section": "halo", "deadline_s": 0.5}

@@ -79,7 +79,13 @@ def test_pingpong_nd(gpu, method, total, block):
     (4, "64 64 16", {"TEMPI_FAKE_FOREIGN_GPU": "1"}, []),
     (8, "64", {"TEMPI_FAKE_FOREIGN_GPU": "1", "TEMPI_STREAMS": "3"}, []),
     (2, "40", {"TEMPI_FAKE_FOREIGN_GPU": "1", "TEMPI_IPC_COPY_MIN_BYTES": "1", "TEMPI_IPC_COPY_MIN_BLOCK": "1"}, []),
-    (4, "64 64 16", {"TEMPI_FAKE_FOREIGN_GPU": "1", "TEMPI_FAULT_CANARY": "1"}, [])])
+    (4, "64 64 16", {"TEMPI_FAKE_FOREIGN_GPU": "1", "TEMPI_FAULT_CANARY": "1"}, []),
+    # rank placement (MPI_Dist_graph_create_adjacent, reorder = 1) over two
+    # fake nodes: every rank plays the rank it is given
+    (8, "48", {"TEMPI_PLACEMENT_KAHIP": "", "TEMPI_FAKE_NODE_SIZE": "4"}, ["--reorder"]),
+    (8, "48", {"TEMPI_PLACEMENT_KAHIP": "", "TEMPI_FAKE_NODE_SIZE": "4", "TEMPI_STREAMS": "3"},
+     ["--reorder", "--neighbor"]),
+    (4, "64 64 16", {"TEMPI_PLACEMENT_RANDOM": "", "TEMPI_FAKE_NODE_SIZE": "2"}, ["--reorder"])])
 def test_halo_exchange_content(gpu, ranks, grid, env, extra):
     rc, out = mpi_launch.run(ranks, [os.path.join(LIB, "halo_exchange"), "2"] + grid.split() + ["--quants", "2", "--check"] + extra,
                              env=env, timeout=300)
@@ -255,4 +261,13 @@ def test_transport_fuzz(gpu, n, seed, env):
     library-packed, host) between all pairs incl. self, tags reused so MPI
     order matters, random posting interleavings; every byte checked"""
     rc, out = mpi_launch.run(n, mpi_launch.py("fuzz.py", "5", str(seed)), env=env, timeout=200)
+    assert rc == 0 and "RESULT errors=0" in out, out[-3000:]
+
+
+@pytest.mark.parametrize("method", ["TEMPI_PLACEMENT_KAHIP", "TEMPI_PLACEMENT_RANDOM"])
+def test_placement_device(gpu, method):
+    """the placement program with a strided device type along every edge of
+    the placed communicator (TEMPI's transport), bytes against the oracle"""
+    rc, out = mpi_launch.run(8, mpi_launch.py("placement.py", "--device"),
+                             env={method: "", "TEMPI_FAKE_NODE_SIZE": "4"}, timeout=240)
     assert rc == 0 and "RESULT errors=0" in out, out[-3000:]
