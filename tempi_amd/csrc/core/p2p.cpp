@@ -123,12 +123,95 @@ int tagUb = 32767;
 bool gpuAwareLibrary = false;
 int64_t ipcMinBytes = 4 * 1024;
 
+// Acks between the ranks of one node go through shared memory: each rank
+// exposes `slots` 32-bit slots (MPI_Win_allocate_shared over its
+// MPI_COMM_TYPE_SHARED communicator). A sender takes a free slot of its own
+// board for each message whose ack it waits for (IPC slab, IPC COPY) and names
+// it as the descriptor's ackTag; the receiver stores code + 1 into that slot
+// (release) and the sender polls its outstanding slots on each progress pass
+// (acquire). No library message per ack, and no library request in the
+// sender's MPI_Testsome for it. Tags below `slots` are board slots; acks that
+// travel as library messages (a peer outside the node communicator, no free
+// slot, TEMPI_NO_SHM_ACKS) keep tags at or above it.
+struct AckBoard {
+  MPI_Comm node = MPI_COMM_NULL;
+  MPI_Win win = MPI_WIN_NULL;
+  std::vector<uint32_t *> of; // per world rank: its slots (nullptr: not on this board)
+  std::vector<int> freeSlots;
+  int slots = 0; // 0: off
+};
+AckBoard board;
+
+// a free slot of this rank's board for a message to world rank `peer`, or -1
+int board_take(int peer) {
+  if (!board.slots || peer < 0 || size_t(peer) >= board.of.size() || !board.of[size_t(peer)] ||
+      board.freeSlots.empty())
+    return -1;
+  const int s = board.freeSlots.back();
+  board.freeSlots.pop_back();
+  return s;
+}
+
+// the ack code in this rank's slot (and the slot freed), or -1 until it arrives
+int board_poll(int slot) {
+  uint32_t *p = board.of[size_t(state.worldRank)] + slot;
+  const uint32_t v = __atomic_load_n(p, __ATOMIC_ACQUIRE);
+  if (!v) return -1;
+  __atomic_store_n(p, 0u, __ATOMIC_RELAXED);
+  board.freeSlots.push_back(slot);
+  return int(v) - 1;
+}
+
+void board_init() {
+  board = AckBoard();
+  if (std::getenv("TEMPI_NO_SHM_ACKS")) return;
+  const int half = std::max(1, tagUb / 2);
+  const int slots = std::min(16384, half / 2); // (library-message ack tags stay above)
+  if (slots < 64) return;
+  MPI_Comm_split_type(MPI_COMM_WORLD, MPI_COMM_TYPE_SHARED, state.worldRank, MPI_INFO_NULL, &board.node);
+  uint32_t *mine = nullptr;
+  if (MPI_Win_allocate_shared(MPI_Aint(slots) * MPI_Aint(sizeof(uint32_t)), int(sizeof(uint32_t)), MPI_INFO_NULL,
+                              board.node, &mine, &board.win) != MPI_SUCCESS) {
+    next.MPI_Comm_free(&board.node);
+    return;
+  }
+  std::memset(mine, 0, size_t(slots) * sizeof(uint32_t));
+  int n = 0;
+  MPI_Comm_size(board.node, &n);
+  MPI_Group g, wg;
+  MPI_Comm_group(board.node, &g);
+  MPI_Comm_group(MPI_COMM_WORLD, &wg);
+  std::vector<int> local(static_cast<size_t>(n)), world(static_cast<size_t>(n));
+  for (int i = 0; i < n; ++i) local[size_t(i)] = i;
+  MPI_Group_translate_ranks(g, n, local.data(), wg, world.data());
+  MPI_Group_free(&g);
+  MPI_Group_free(&wg);
+  board.of.assign(size_t(state.worldSize), nullptr);
+  for (int i = 0; i < n; ++i) {
+    MPI_Aint size = 0;
+    int unit = 0;
+    uint32_t *base = nullptr;
+    MPI_Win_shared_query(board.win, i, &size, &unit, &base);
+    if (world[size_t(i)] >= 0) board.of[size_t(world[size_t(i)])] = base;
+  }
+  board.freeSlots.reserve(size_t(slots));
+  for (int i = slots - 1; i >= 0; --i) board.freeSlots.push_back(i);
+  board.slots = slots;
+  MPI_Barrier(board.node); // every board is zeroed before any rank writes to one
+}
+
+void board_finalize() {
+  if (board.win != MPI_WIN_NULL) MPI_Win_free(&board.win);
+  if (board.node != MPI_COMM_NULL) next.MPI_Comm_free(&board.node);
+  board = AckBoard();
+}
+
 // acks the sender is waiting for before reusing a device slab
 struct PendingAck {
-  MPI_Request req;
+  MPI_Request req; // the library receive of the ack (MPI_REQUEST_NULL: a board slot)
   Slab *slab;
   int peer;     // world rank of the receiver
-  int tag;      // ack tag
+  int tag;      // ack tag (a board slot when below board.slots)
   int64_t bytes;
   int code;     // received ack payload
 };
@@ -335,6 +418,10 @@ bool canary(int world, const void *peerBytes, int64_t n, int device) {
 int ackCodes[3] = {0, 1, 2};
 
 void send_ack(int world, int tag, int code) {
+  if (tag < board.slots && world >= 0 && size_t(world) < board.of.size() && board.of[size_t(world)]) {
+    __atomic_store_n(board.of[size_t(world)] + tag, uint32_t(code + 1), __ATOMIC_RELEASE);
+    return;
+  }
   MPI_Request r;
   next.MPI_Isend(&ackCodes[code], 1, MPI_INT, world, tag, ctrlComm, &r);
   next.MPI_Request_free(&r);
@@ -484,7 +571,12 @@ struct Op {
   bool done = false;
   int err = MPI_SUCCESS;                       // completed with this error (MPI_ERR_TRUNCATE, ...)
   MPI_Comm errComm = MPI_COMM_NULL;            // whose error handler the wait raises it on
+  int boardSlot = -1;                          // waiting for an ack in this board slot (boardOps)
+  virtual void acked(int) {}                   // that ack arrived with this code
 };
+
+// ops waiting for an ack on this rank's board (polled by progress())
+std::vector<Op *> boardOps;
 
 // ops with a library request outstanding (tested together by progress()).
 // Every post of Op::lib is followed by watch(op).
@@ -603,6 +695,7 @@ constexpr size_t kMaxPending = 512;
 size_t earlyFlush = 32; // TEMPI_EARLY_FLUSH
 size_t firstFlush = 16;  // TEMPI_FIRST_FLUSH: the same while no scatter batch is in flight
 int scattersInFlight = 0; // scatter / copy batches launched and not yet seen complete
+bool eagerFlush = false;  // TEMPI_EAGER_FLUSH (A/B): waits launch queued scatters even while every lane is busy
 
 template <typename T> const T *select(const std::vector<T> &v, const std::vector<int> &dev, int d, bool all,
                                       std::vector<T> &tmp) {
@@ -748,16 +841,19 @@ struct IsendOp : Op {
       desc.bytes = bytes;
       desc.senderWorld = state.worldRank;
       desc.senderPid = int32_t(getpid());
-      // slab acks take [0, tagUb/2); IPC COPY acks the upper half
-      desc.ackTag = int32_t(dslab->id % uint32_t(std::max(1, tagUb / 2)));
       desc.rawPtr = reinterpret_cast<uint64_t>(dslab->dev);
       desc.gpu = gpu::identity(device);
       std::memcpy(desc.handle, slab_ipc_handle(dslab), sizeof desc.handle);
-      // the slab is reused once the receiver acknowledges (private comm)
+      // the slab is reused once the receiver acknowledges: in a board slot,
+      // or as a library message on the private communicator (those tags take
+      // [board.slots, tagUb/2); IPC COPY's the upper half)
       const int peer = topology::world_rank(comm, dest);
+      const int slot = board_take(peer);
+      const uint32_t span = uint32_t(std::max(1, tagUb / 2 - board.slots));
+      desc.ackTag = slot >= 0 ? slot : board.slots + int32_t(dslab->id % span);
       pendingAcks.push_back(std::unique_ptr<PendingAck>(new PendingAck{MPI_REQUEST_NULL, dslab, peer, desc.ackTag, bytes, -1}));
       PendingAck &pa = *pendingAcks.back();
-      next.MPI_Irecv(&pa.code, 1, MPI_INT, peer, desc.ackTag, ctrlComm, &pa.req);
+      if (slot < 0) next.MPI_Irecv(&pa.code, 1, MPI_INT, peer, desc.ackTag, ctrlComm, &pa.req);
       dslab = nullptr;
       next.MPI_Isend(&desc, int(sizeof desc), MPI_PACKED, dest, tag, comm, &lib);
       watch(this);
@@ -901,7 +997,23 @@ struct IsendCopyOp : Op {
     ready = true;
     gate_advance(key);
   }
+  // With a board slot the library request is the descriptor's send (tested
+  // until it is delivered, which keeps the library progressing it) and the
+  // ack arrives on the board; the send completes once both have. Otherwise
+  // the library request is the ack's receive, and the descriptor's send is
+  // freed (the ack follows its delivery).
+  bool boardAck = false, descSent = false;
   void post() override {
+    const int slot = board_take(peer);
+    if (slot >= 0) {
+      desc.ackTag = slot;
+      boardSlot = slot;
+      boardAck = true;
+      boardOps.push_back(this);
+      next.MPI_Isend(&desc, int(sizeof desc), MPI_PACKED, dest, tag, comm, &lib);
+      watch(this);
+      return;
+    }
     next.MPI_Irecv(&ack, 1, MPI_INT, peer, desc.ackTag, ctrlComm, &lib);
     watch(this);
     MPI_Request r; // the descriptor lives in this op until the ack, which follows its delivery
@@ -909,6 +1021,18 @@ struct IsendCopyOp : Op {
     next.MPI_Request_free(&r);
   }
   void lib_done(const MPI_Status &) override {
+    if (boardAck) {
+      descSent = true;
+      if (ack >= 0) finish();
+      return;
+    }
+    finish();
+  }
+  void acked(int code) override {
+    ack = code;
+    if (descSent) finish();
+  }
+  void finish() {
     if (ack != kCopyDone) {
       if (ack == kCopyUnmapped) mark_ipc_broken(peer);
       counters.copy_resends++;
@@ -1787,6 +1911,7 @@ void init() {
   firstFlush = std::min<size_t>(16, earlyFlush);
   if (const char *s = std::getenv("TEMPI_FIRST_FLUSH")) firstFlush = size_t(std::max(1, std::atoi(s)));
   scattersInFlight = 0;
+  eagerFlush = std::getenv("TEMPI_EAGER_FLUSH") != nullptr;
   directShared.clear();
   directShared.reserve(512);
   active.reserve(2048);
@@ -1798,6 +1923,8 @@ void init() {
   int *ub = nullptr;
   MPI_Comm_get_attr(MPI_COMM_WORLD, MPI_TAG_UB, &ub, &flag);
   if (flag && ub) tagUb = *ub;
+  board_init();
+  boardOps.clear();
 }
 
 void reload_perf_model() {
@@ -1827,6 +1954,7 @@ void finalize() {
   gates.clear();
   gatedOps = 0;
   libWatch.clear();
+  boardOps.clear(); // (their ops died with `active`)
   for (auto &b : batches)
     if (b->event) tempi_hip_event_destroy(b->event);
   batches.clear();
@@ -1835,7 +1963,8 @@ void finalize() {
     progress();
     if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(30)) {
       LOG_WARN(pendingAcks.size() << " IPC slab(s) never acknowledged; abandoning");
-      for (auto &pa : pendingAcks) MPI_Cancel(&pa->req);
+      for (auto &pa : pendingAcks)
+        if (pa->req != MPI_REQUEST_NULL) MPI_Cancel(&pa->req);
       pendingAcks.clear();
     }
   }
@@ -1847,6 +1976,7 @@ void finalize() {
   ipcAllocOpen.clear();
   ipcExports.clear();
   if (ctrlComm != MPI_COMM_NULL) MPI_Comm_free(&ctrlComm);
+  board_finalize();
   device_pool().release_all();
   pinned_pool().release_all();
 }
@@ -2056,6 +2186,17 @@ int cancel(MPI_Request r) {
   return MPI_SUCCESS;
 }
 
+namespace {
+// Queued scatters / copies are launched by a waiting pass only while a
+// scatter lane is free, or once a launch's worth has queued: with every lane
+// busy the GPU has work either way, and messages arriving one at a time then
+// share a launch instead of each taking one (a cheap pass -- no library
+// request to test -- would otherwise launch every arrival on its own).
+bool scatter_flush_due() {
+  return eagerFlush || scattersInFlight < std::max(1, gpu::lanes() - 1) || pendingUnpack.size() >= earlyFlush;
+}
+} // namespace
+
 bool progress(bool full) {
   bool moved = false;
   counters.progress_passes++;
@@ -2065,7 +2206,7 @@ bool progress(bool full) {
     flush_list(pendingPack, true);
     moved = true;
   }
-  if (full && !pendingUnpack.empty()) {
+  if (full && !pendingUnpack.empty() && scatter_flush_due()) {
     flush_list(pendingUnpack, false);
     moved = true;
   }
@@ -2094,7 +2235,24 @@ bool progress(bool full) {
   while (!batches.empty() && batches.front()->complete) batches.pop_front();
   tock(counters.ns_events, t0);
   t0 = tick();
-  // 2. every outstanding library request in one MPI_Testsome
+  // 2. acks on this rank's board, then every outstanding library request in
+  //    one MPI_Testsome
+  std::vector<size_t> ackedSlots;
+  if (!boardOps.empty()) {
+    size_t w = 0;
+    for (size_t i = 0; i < boardOps.size(); ++i) {
+      Op *op = boardOps[i];
+      const int code = board_poll(op->boardSlot);
+      if (code < 0) {
+        boardOps[w++] = op;
+        continue;
+      }
+      op->boardSlot = -1;
+      op->acked(code);
+      moved = true;
+    }
+    boardOps.resize(w);
+  }
   pollReqs.clear();
   pollOps.clear();
   pollAck.clear();
@@ -2104,9 +2262,15 @@ bool progress(bool full) {
     pollAck.push_back(0);
   }
   for (size_t i = 0; i < pendingAcks.size(); ++i) {
-    pollReqs.push_back(pendingAcks[i]->req);
-    pollOps.push_back(nullptr);
-    pollAck.push_back(i);
+    PendingAck &pa = *pendingAcks[i];
+    if (pa.req != MPI_REQUEST_NULL) {
+      pollReqs.push_back(pa.req);
+      pollOps.push_back(nullptr);
+      pollAck.push_back(i);
+    } else if ((pa.code = board_poll(pa.tag)) >= 0) {
+      ackedSlots.push_back(i);
+      moved = true;
+    }
   }
   if (!pollReqs.empty()) {
     const int n = int(pollReqs.size());
@@ -2117,7 +2281,6 @@ bool progress(bool full) {
     if (outcount == MPI_UNDEFINED) outcount = 0;
     if (trc != MPI_ERR_IN_STATUS) // the statuses' MPI_ERROR fields are set only with this code
       for (int k = 0; k < outcount; ++k) pollSt[size_t(k)].MPI_ERROR = MPI_SUCCESS;
-    std::vector<size_t> ackedSlots;
     for (int k = 0; k < outcount; ++k) {
       const size_t i = size_t(pollIdx[size_t(k)]);
       if (Op *op = pollOps[i]) {
@@ -2138,28 +2301,29 @@ bool progress(bool full) {
       }
       libWatch.resize(w);
     }
-    // release acknowledged slabs (highest index first keeps indices valid)
-    std::sort(ackedSlots.rbegin(), ackedSlots.rend());
-    for (size_t a : ackedSlots) {
-      PendingAck &pa = *pendingAcks[a];
-      pa.req = MPI_REQUEST_NULL;
-      if (pa.code == 1) { // the receiver could not map the slab: send the bytes through the host
-        mark_ipc_broken(pa.peer);
-        Slab *h = pinned_pool().get(size_t(pa.bytes), pa.slab->device);
-        gpu::check(tempi_hip_memcpy(h->host, pa.slab->dev, size_t(pa.bytes)), "ipc fallback D2H");
-        next.MPI_Send(h->host, int(pa.bytes), MPI_PACKED, pa.peer, pa.tag, ctrlComm); // receive already posted
-        pinned_pool().put(h);
-      }
-      device_pool().put(pa.slab);
-      pendingAcks[a] = std::move(pendingAcks.back());
-      pendingAcks.pop_back();
+  }
+  // release acknowledged slabs (highest index first keeps indices valid)
+  std::sort(ackedSlots.rbegin(), ackedSlots.rend());
+  for (size_t a : ackedSlots) {
+    PendingAck &pa = *pendingAcks[a];
+    pa.req = MPI_REQUEST_NULL;
+    if (pa.code == 1) { // the receiver could not map the slab: send the bytes through the host
+      mark_ipc_broken(pa.peer);
+      Slab *h = pinned_pool().get(size_t(pa.bytes), pa.slab->device);
+      gpu::check(tempi_hip_memcpy(h->host, pa.slab->dev, size_t(pa.bytes)), "ipc fallback D2H");
+      next.MPI_Send(h->host, int(pa.bytes), MPI_PACKED, pa.peer, pa.tag, ctrlComm); // receive already posted
+      pinned_pool().put(h);
     }
+    device_pool().put(pa.slab);
+    pendingAcks[a] = std::move(pendingAcks.back());
+    pendingAcks.pop_back();
   }
   tock(counters.ns_testsome, t0);
   // 3. unpacks of messages that arrived: launched together when the caller
   //    is about to wait for them (light passes from MPI_Isend / MPI_Irecv
   //    only queue them, so a burst of receives shares one launch)
-  if (!pendingUnpack.empty() && (full || pendingUnpack.size() >= kMaxPending)) flush_list(pendingUnpack, false);
+  if (!pendingUnpack.empty() && (full || pendingUnpack.size() >= kMaxPending) && scatter_flush_due())
+    flush_list(pendingUnpack, false);
   // 4. operations the application freed with MPI_Request_free
   if (!detachedOps.empty()) {
     size_t w = 0;
