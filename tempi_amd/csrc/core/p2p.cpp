@@ -208,12 +208,13 @@ void board_finalize() {
 
 // acks the sender is waiting for before reusing a device slab
 struct PendingAck {
-  MPI_Request req; // the library receive of the ack (MPI_REQUEST_NULL: a board slot)
-  Slab *slab;
+  MPI_Request req; // the library receive of the ack (not on the board)
+  Slab *slab;   // nullptr once released
   int peer;     // world rank of the receiver
-  int tag;      // ack tag (a board slot when below board.slots)
+  int tag;      // ack tag (a board slot when onBoard)
   int64_t bytes;
   int code;     // received ack payload
+  bool onBoard; // the ack arrives in board slot `tag`
 };
 std::vector<std::unique_ptr<PendingAck>> pendingAcks; // stable addresses: Irecv targets
 
@@ -587,6 +588,11 @@ void watch(Op *op) {
     libWatch.push_back(op);
   }
 }
+void unwatch(Op *op) {
+  if (!op->watched) return;
+  libWatch.erase(std::find(libWatch.begin(), libWatch.end(), op));
+  op->watched = false;
+}
 
 // MPI's non-overtaking rule: sends from this process to one (comm, dest) reach
 // the library in call order. An IsendOp reaches it only when its gather has
@@ -851,7 +857,8 @@ struct IsendOp : Op {
       const int slot = board_take(peer);
       const uint32_t span = uint32_t(std::max(1, tagUb / 2 - board.slots));
       desc.ackTag = slot >= 0 ? slot : board.slots + int32_t(dslab->id % span);
-      pendingAcks.push_back(std::unique_ptr<PendingAck>(new PendingAck{MPI_REQUEST_NULL, dslab, peer, desc.ackTag, bytes, -1}));
+      pendingAcks.push_back(
+          std::unique_ptr<PendingAck>(new PendingAck{MPI_REQUEST_NULL, dslab, peer, desc.ackTag, bytes, -1, slot >= 0}));
       PendingAck &pa = *pendingAcks.back();
       if (slot < 0) next.MPI_Irecv(&pa.code, 1, MPI_INT, peer, desc.ackTag, ctrlComm, &pa.req);
       dslab = nullptr;
@@ -1023,14 +1030,22 @@ struct IsendCopyOp : Op {
   void lib_done(const MPI_Status &) override {
     if (boardAck) {
       descSent = true;
-      if (ack >= 0) finish();
+      if (ack >= 0 && !done) finish();
       return;
     }
     finish();
   }
   void acked(int code) override {
     ack = code;
-    if (descSent) finish();
+    // the receiver has the descriptor, so the library is done with this
+    // op's copy of it: a send still under test is let go (its completion may
+    // also be recorded already, with the callback still to come)
+    if (!descSent && lib != MPI_REQUEST_NULL) {
+      unwatch(this);
+      next.MPI_Request_free(&lib);
+    }
+    descSent = true;
+    finish();
   }
   void finish() {
     if (ack != kCopyDone) {
@@ -1885,7 +1900,8 @@ MPI_Request add(std::unique_ptr<Op> op) {
 // scratch for progress()
 std::vector<MPI_Request> pollReqs;
 std::vector<Op *> pollOps;   // nullptr: a pending ack
-std::vector<size_t> pollAck; // index into pendingAcks
+std::vector<PendingAck *> pollAck; // the pending ack of each request (nullptr: an op's)
+int progressDepth = 0;             // progress() passes on the stack
 std::vector<int> pollIdx;
 std::vector<MPI_Status> pollSt;
 
@@ -2200,6 +2216,14 @@ bool scatter_flush_due() {
 bool progress(bool full) {
   bool moved = false;
   counters.progress_passes++;
+  // a pass run from inside a callback of an outer pass (a wait inside it)
+  // leaves finished detached operations to the outer pass, whose recorded
+  // completions may still name them
+  struct Depth {
+    int &d;
+    explicit Depth(int &x) : d(++x) {}
+    ~Depth() { --d; }
+  } depth(progressDepth);
   // 0. launch queued gathers (one launch per batch group); scatters too when
   //    the caller is about to wait
   if (!pendingPack.empty()) {
@@ -2236,8 +2260,12 @@ bool progress(bool full) {
   tock(counters.ns_events, t0);
   t0 = tick();
   // 2. acks on this rank's board, then every outstanding library request in
-  //    one MPI_Testsome
-  std::vector<size_t> ackedSlots;
+  //    one MPI_Testsome. Completions are recorded -- requests cleared, the
+  //    watch list compacted, acknowledged slabs released -- before any
+  //    operation's callback runs: a callback may wait for something (a
+  //    descriptor landing in a host buffer does), and so run a nested pass,
+  //    which must not test a request the library has already completed and
+  //    freed.
   if (!boardOps.empty()) {
     size_t w = 0;
     for (size_t i = 0; i < boardOps.size(); ++i) {
@@ -2253,25 +2281,26 @@ bool progress(bool full) {
     }
     boardOps.resize(w);
   }
+  std::vector<PendingAck *> acked;
   pollReqs.clear();
   pollOps.clear();
   pollAck.clear();
   for (Op *op : libWatch) {
     pollReqs.push_back(op->lib);
     pollOps.push_back(op);
-    pollAck.push_back(0);
+    pollAck.push_back(nullptr);
   }
-  for (size_t i = 0; i < pendingAcks.size(); ++i) {
-    PendingAck &pa = *pendingAcks[i];
-    if (pa.req != MPI_REQUEST_NULL) {
+  for (auto &p : pendingAcks) {
+    PendingAck &pa = *p;
+    if (!pa.onBoard) {
       pollReqs.push_back(pa.req);
       pollOps.push_back(nullptr);
-      pollAck.push_back(i);
+      pollAck.push_back(&pa);
     } else if ((pa.code = board_poll(pa.tag)) >= 0) {
-      ackedSlots.push_back(i);
-      moved = true;
+      acked.push_back(&pa);
     }
   }
+  std::vector<std::pair<Op *, MPI_Status>> completed;
   if (!pollReqs.empty()) {
     const int n = int(pollReqs.size());
     pollIdx.resize(size_t(n));
@@ -2285,13 +2314,13 @@ bool progress(bool full) {
       const size_t i = size_t(pollIdx[size_t(k)]);
       if (Op *op = pollOps[i]) {
         op->lib = MPI_REQUEST_NULL;
-        op->lib_done(pollSt[size_t(k)]);
+        completed.emplace_back(op, pollSt[size_t(k)]);
       } else {
-        ackedSlots.push_back(pollAck[i]);
+        pollAck[i]->req = MPI_REQUEST_NULL;
+        acked.push_back(pollAck[i]);
       }
-      moved = true;
     }
-    if (outcount) { // drop completed requests from the watch list (re-posted ones stay)
+    if (!completed.empty()) { // drop completed requests from the watch list
       size_t w = 0;
       for (Op *op : libWatch) {
         if (op->lib != MPI_REQUEST_NULL)
@@ -2302,22 +2331,27 @@ bool progress(bool full) {
       libWatch.resize(w);
     }
   }
-  // release acknowledged slabs (highest index first keeps indices valid)
-  std::sort(ackedSlots.rbegin(), ackedSlots.rend());
-  for (size_t a : ackedSlots) {
-    PendingAck &pa = *pendingAcks[a];
-    pa.req = MPI_REQUEST_NULL;
-    if (pa.code == 1) { // the receiver could not map the slab: send the bytes through the host
-      mark_ipc_broken(pa.peer);
-      Slab *h = pinned_pool().get(size_t(pa.bytes), pa.slab->device);
-      gpu::check(tempi_hip_memcpy(h->host, pa.slab->dev, size_t(pa.bytes)), "ipc fallback D2H");
-      next.MPI_Send(h->host, int(pa.bytes), MPI_PACKED, pa.peer, pa.tag, ctrlComm); // receive already posted
+  // release acknowledged slabs
+  for (PendingAck *pa : acked) {
+    if (pa->code == 1) { // the receiver could not map the slab: send the bytes through the host
+      mark_ipc_broken(pa->peer);
+      Slab *h = pinned_pool().get(size_t(pa->bytes), pa->slab->device);
+      gpu::check(tempi_hip_memcpy(h->host, pa->slab->dev, size_t(pa->bytes)), "ipc fallback D2H");
+      next.MPI_Send(h->host, int(pa->bytes), MPI_PACKED, pa->peer, pa->tag, ctrlComm); // receive already posted
       pinned_pool().put(h);
     }
-    device_pool().put(pa.slab);
-    pendingAcks[a] = std::move(pendingAcks.back());
-    pendingAcks.pop_back();
+    device_pool().put(pa->slab);
+    pa->slab = nullptr;
   }
+  if (!acked.empty()) {
+    pendingAcks.erase(std::remove_if(pendingAcks.begin(), pendingAcks.end(),
+                                     [](const std::unique_ptr<PendingAck> &p) { return !p->slab; }),
+                      pendingAcks.end());
+    moved = true;
+  }
+  // the callbacks of the completed library requests, last
+  for (auto &c : completed) c.first->lib_done(c.second);
+  if (!completed.empty()) moved = true;
   tock(counters.ns_testsome, t0);
   // 3. unpacks of messages that arrived: launched together when the caller
   //    is about to wait for them (light passes from MPI_Isend / MPI_Irecv
@@ -2325,7 +2359,7 @@ bool progress(bool full) {
   if (!pendingUnpack.empty() && (full || pendingUnpack.size() >= kMaxPending) && scatter_flush_due())
     flush_list(pendingUnpack, false);
   // 4. operations the application freed with MPI_Request_free
-  if (!detachedOps.empty()) {
+  if (!detachedOps.empty() && progressDepth == 1) {
     size_t w = 0;
     for (uint32_t h : detachedOps) {
       auto it = active.find(h);
