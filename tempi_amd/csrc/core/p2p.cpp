@@ -169,6 +169,7 @@ void board_init() {
   const int slots = std::min(16384, half / 2); // (library-message ack tags stay above)
   if (slots < 64) return;
   MPI_Comm_split_type(MPI_COMM_WORLD, MPI_COMM_TYPE_SHARED, state.worldRank, MPI_INFO_NULL, &board.node);
+  MPI_Comm_set_errhandler(board.node, MPI_ERRORS_RETURN); // no shared window: library acks, not an abort
   uint32_t *mine = nullptr;
   if (MPI_Win_allocate_shared(MPI_Aint(slots) * MPI_Aint(sizeof(uint32_t)), int(sizeof(uint32_t)), MPI_INFO_NULL,
                               board.node, &mine, &board.win) != MPI_SUCCESS) {
