@@ -633,6 +633,55 @@ def alltoallv(args, world):
             "points": out}
 
 
+def _line_classes(bl, st, n, first):
+    """Per 128-B line of the strided side of n rows of bl bytes at stride st
+    (first row at byte `first`): (lines touched, lines with a partly written
+    64-B sector, lines written whole, lines with one whole sector and one
+    untouched). Counted exactly on a sample of whole periods of the row
+    pattern (>= 64 KiB of address span) and scaled to n rows."""
+    import numpy as np
+
+    p = 128 // math.gcd(st, 128)  # rows after which the pattern repeats modulo a line
+    m = min(n, max(p, -(-65536 // st)))
+    m = min(n, -(-m // p) * p)
+    lo = first - first % 128
+    span = (m - 1) * st + bl + (first - lo)
+    cov = np.zeros(-(-span // 128) * 128, dtype=np.uint8)
+    starts = first - lo + np.arange(m, dtype=np.int64) * st
+    for b in range(bl):  # bl <= 4096; vectorised over rows
+        cov[starts + b] = 1
+    sec = cov.reshape(-1, 2, 64).sum(axis=2)  # bytes covered per sector
+    touched = (sec > 0).any(axis=1)
+    partial = ((sec > 0) & (sec < 64)).any(axis=1)
+    whole = (sec == 64).all(axis=1)
+    half = touched & ~partial & ~whole
+    s = n / m
+    return touched.sum() * s, partial.sum() * s, whole.sum() * s, half.sum() * s
+
+
+# Write cost per line, in bytes of full-line streaming, from the box's
+# calibration (profiles/r02/counter_calibration.txt: whole lines 5.6-5.7 TB/s,
+# one whole sector per line 7.5-7.6 TB/s of lines, lines with a partly
+# written sector 2.3-2.7 TB/s of lines: a DRAM read-modify-write)
+LINE_WRITE_WHOLE, LINE_WRITE_HALF, LINE_WRITE_PARTIAL = 128.0, 96.0, 292.0
+
+
+def touched_model(bl, st, nplanes, rows, plane_stride, first):
+    """Bytes-equivalent one pack and one unpack of this config-2 shape must
+    move at the memory side, to be divided by the achievable streaming rate:
+    pack = every 128-B line the strided side touches (a read fetches whole
+    lines, any load flavour) + the packed bytes written whole; unpack = the
+    packed bytes read + each strided-side line at its calibrated write cost
+    (whole, one whole sector, or a partly written sector). Planes of a 3D
+    shape are counted at the first plane's alignment (their offsets differ by
+    less than a line per plane)."""
+    payload = nplanes * rows * bl
+    touched, partial, whole, half = _line_classes(bl, st, rows, first)
+    return {"pack_bytes": nplanes * touched * 128.0 + payload,
+            "unpack_bytes": payload + nplanes * (whole * LINE_WRITE_WHOLE + half * LINE_WRITE_HALF +
+                                                 partial * LINE_WRITE_PARTIAL)}
+
+
 def sweep(args, mpi, torch, dev, path, sizes=(1 << 20, 16 << 20, 256 << 20, 1 << 30), quiet=False):
     """Config-2 sweep: 2D subarray and 3D subarray, block 1 B - 4 KiB.
     Returns the records (also written to `path` when given)."""
@@ -648,6 +697,7 @@ def sweep(args, mpi, torch, dev, path, sizes=(1 << 20, 16 << 20, 256 << 20, 1 <<
                         t = mpi.Type_create_subarray([rows, st], [rows, bl], [0, 0], mpi.ORDER_C, mpi.BYTE)
                         extent = rows * st
                         shape = f"2d rows={rows} stride={st}"
+                        planes = (1, rows, 0, 0)  # (planes, rows per plane, plane stride, first byte)
                     else:
                         y = max(1, int(rows ** 0.5))
                         z = max(1, rows // y)
@@ -656,6 +706,7 @@ def sweep(args, mpi, torch, dev, path, sizes=(1 << 20, 16 << 20, 256 << 20, 1 <<
                         t = mpi.Type_create_subarray([z + 2, Y, st], [z, y, bl], [1, 2, 0], mpi.ORDER_C, mpi.BYTE)
                         extent = (z + 2) * Y * st
                         shape = f"3d {z}x{y} rows pitch={st} ypad=3"
+                        planes = (z, y, Y * st, Y * st + 2 * st)
                     if extent > (12 << 30):
                         mpi.Type_free(t)
                         continue
@@ -685,6 +736,10 @@ def sweep(args, mpi, torch, dev, path, sizes=(1 << 20, 16 << 20, 256 << 20, 1 <<
                            "pack_api_ms": (t1 - t0) / reps * 1e3, "unpack_api_ms": (t2 - t1) / reps * 1e3,
                            "pack_alg_gbs": 2 * payload / (pk_ms * 1e-3) / 1e9,
                            "unpack_alg_gbs": 2 * payload / (up_ms * 1e-3) / 1e9}
+                    tb = touched_model(bl, st, *planes)
+                    rec.update({"pack_touched_bytes": tb["pack_bytes"], "unpack_touched_bytes": tb["unpack_bytes"],
+                                "pack_frac_touched": tb["pack_bytes"] / (HBM_ACHIEVABLE_GBS * 1e9) / (pk_ms * 1e-3),
+                                "unpack_frac_touched": tb["unpack_bytes"] / (HBM_ACHIEVABLE_GBS * 1e9) / (up_ms * 1e-3)})
                     recs.append(rec)
                     if not quiet:
                         print(json.dumps(rec), flush=True)
@@ -709,7 +764,10 @@ def sweep_geomean(args, mpi, torch, dev):
 
     pk = [r["pack_alg_gbs"] for r in recs]
     up = [r["unpack_alg_gbs"] for r in recs]
+    pkt = [r["pack_frac_touched"] for r in recs]
+    upt = [r["unpack_frac_touched"] for r in recs]
     worst = sorted(recs, key=lambda r: min(r["pack_alg_gbs"], r["unpack_alg_gbs"]))[:3]
+    worst_t = sorted(recs, key=lambda r: min(r["pack_frac_touched"], r["unpack_frac_touched"]))[:3]
     return {"points": len(recs), "packed_bytes": 1 << 30,
             "pack_GBps": round(gm(pk), 1), "unpack_GBps": round(gm(up), 1),
             "pack_frac": round(gm(pk) / HBM_PEAK_GBS, 4), "unpack_frac": round(gm(up) / HBM_PEAK_GBS, 4),
@@ -718,6 +776,17 @@ def sweep_geomean(args, mpi, torch, dev):
             "worst": [{"shape": r["shape"], "block": r["block"], "stride": r["stride"],
                        "pack_GBps": round(r["pack_alg_gbs"], 1), "unpack_GBps": round(r["unpack_alg_gbs"], 1)}
                       for r in worst],
+            # the same points against the bytes the memory side must move
+            # (touched_model: whole lines read, partial sectors read-modify-
+            # written) at the 6.3 TB/s achievable rate
+            "pack_frac_touched": round(gm(pkt), 4), "unpack_frac_touched": round(gm(upt), 4),
+            "worst_touched": [{"shape": r["shape"], "block": r["block"], "stride": r["stride"],
+                               "pack_frac_touched": round(r["pack_frac_touched"], 3),
+                               "unpack_frac_touched": round(r["unpack_frac_touched"], 3)} for r in worst_t],
+            "touched_model": ("pack: 128-B lines touched on the strided side + packed bytes; unpack: packed bytes + "
+                              "each strided-side line at its calibrated write cost (whole 128, one whole sector 96, "
+                              "a partly written sector 292 bytes-equivalent: DRAM read-modify-write), all at 6.3 TB/s; "
+                              "profiles/r02/counter_calibration.txt"),
             "workload": "config 2 at 1 GiB packed: MPI_Type_create_subarray 2D {rows, S} and 3D {z+2, y+3, S}, "
                         "block 1 B - 4 KiB, S in {2*bl, bl+16, 512 (bl <= 256)}; kernel time per MPI_Pack / "
                         "MPI_Unpack from HIP events on TEMPI's stream"}

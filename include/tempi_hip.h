@@ -106,6 +106,9 @@ int tempi_hip_device_count(int *n);
 int tempi_hip_device_uuid(int device, unsigned char uuid[16]);
 int tempi_hip_get_device(int *dev);
 int tempi_hip_set_device(int dev);
+/* 1 when kernels on `device` can load from memory of `peer` (always 1 for
+   device == peer), 0 otherwise */
+int tempi_hip_can_access_peer(int device, int peer);
 int tempi_hip_device_synchronize(void);
 
 /* pointer classification (reference semantics: "device-accessible" means

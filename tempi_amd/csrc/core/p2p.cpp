@@ -365,11 +365,14 @@ void *peer_pointer(const IpcDesc &d) {
 // First contact with a peer on ANOTHER GPU. This pool's boxes have one GPU,
 // so the cross-GPU IPC path is first met on the driver's 8-GPU node: before
 // the transport trusts a mapping of that peer's memory, the first bytes a
-// descriptor names are read twice -- by the remote-load copy kernel the
-// receiver uses (TEMPI_HIP_ITEM_REMOTE, system-scope loads) and by a DMA copy
-// (hipMemcpy) -- and compared on the host. A failed read or a mismatch turns
-// IPC with that peer off: this message and every later one go through the
-// host (the NACK path). Once per peer; at most 64 KiB.
+// descriptor names are read twice -- by a DMA copy (hipMemcpy) and by the
+// remote-load copy kernel the receiver uses (TEMPI_HIP_ITEM_REMOTE,
+// system-scope loads) -- and compared on the host. The kernel runs only after
+// the DMA read succeeded and when HIP reports that this GPU can load from the
+// mapping's GPU, so a mapping the fabric cannot serve fails as a HIP error,
+// never as a faulting kernel. A failed read or a mismatch turns IPC with that
+// peer off: this message and every later one go through the host (the NACK
+// path). Once per peer; at most 64 KiB.
 std::vector<signed char> canaryVerdict; // per world rank: 0 untested, 1 passed, -1 failed
 bool faultCanary = false;               // TEMPI_FAULT_CANARY: the comparison fails (tests)
 
@@ -384,8 +387,17 @@ bool canary(int world, const void *peerBytes, int64_t n, int device) {
   tempi_hip_get_device(&cur);
   if (cur != device) tempi_hip_set_device(device);
   std::vector<unsigned char> viaKernel(size_t(n), 0), viaDma(size_t(n), 1);
+  bool ok = tempi_hip_memcpy(viaDma.data(), peerBytes, size_t(n)) == 0;
+  if (ok) {
+    tempi_hip_ptrinfo info;
+    if (tempi_hip_pointer_info(peerBytes, &info) == 0 && info.device >= 0 &&
+        !tempi_hip_can_access_peer(device, info.device)) {
+      LOG_WARN("canary: GPU " << device << " cannot load from GPU " << info.device << " (rank " << world << ")");
+      ok = false;
+    }
+  }
   void *scratch = nullptr;
-  bool ok = tempi_hip_malloc(&scratch, size_t(n)) == 0;
+  ok = ok && tempi_hip_malloc(&scratch, size_t(n)) == 0;
   if (ok) {
     tempi_hip_copy_item c{};
     c.dst_first = scratch;
@@ -396,10 +408,9 @@ bool canary(int world, const void *peerBytes, int64_t n, int device) {
     c.flags = TEMPI_HIP_ITEM_REMOTE;
     void *s = gpu::stream(device);
     ok = tempi_hip_copy_batch(&c, 1, s) == 0 && tempi_hip_stream_synchronize(s) == 0 &&
-         tempi_hip_memcpy(viaKernel.data(), scratch, size_t(n)) == 0 &&
-         tempi_hip_memcpy(viaDma.data(), peerBytes, size_t(n)) == 0;
-    tempi_hip_free(scratch);
+         tempi_hip_memcpy(viaKernel.data(), scratch, size_t(n)) == 0;
   }
+  if (scratch) tempi_hip_free(scratch);
   if (cur != device) tempi_hip_set_device(cur);
   if (ok && faultCanary) viaDma[0] ^= 0xFF;
   ok = ok && viaKernel == viaDma;

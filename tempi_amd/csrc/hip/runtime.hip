@@ -46,6 +46,15 @@ int tempi_hip_device_uuid(int device, unsigned char uuid[16]) {
   return 0;
 }
 int tempi_hip_set_device(int dev) { RET(hipSetDevice(dev)); }
+int tempi_hip_can_access_peer(int device, int peer) {
+  if (device == peer) return 1;
+  int can = 0;
+  if (hipDeviceCanAccessPeer(&can, device, peer) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return can ? 1 : 0;
+}
 int tempi_hip_device_synchronize(void) { RET(hipDeviceSynchronize()); }
 
 int tempi_hip_pointer_info(const void *p, tempi_hip_ptrinfo *out) {

@@ -94,3 +94,39 @@ def test_section_deadline_prints_the_line_so_far():
     line = json.loads(r.stdout.strip().splitlines()[-1])
     assert r.returncode == 0 and line["value"] == 1.0
     assert line["incomplete"] == {"section": "halo", "deadline_s": 0.5}
+
+
+def _brute_classes(bl, st, n, first):
+    """line classes of n rows, byte by byte (small cases only)"""
+    lines = {}
+    for r in range(n):
+        for b in range(first + r * st, first + r * st + bl):
+            lines.setdefault(b // 128, [0, 0])[(b % 128) // 64] += 1
+    touched = len(lines)
+    partial = sum(any(0 < s < 64 for s in v) for v in lines.values())
+    whole = sum(v == [64, 64] for v in lines.values())
+    return touched, partial, whole, touched - partial - whole
+
+
+@pytest.mark.parametrize("bl,st,n,first", [(512, 1024, 64, 0), (8, 16, 4096, 0), (128, 144, 256, 0),
+                                           (64, 512, 128, 0), (3, 19, 2000, 38), (24, 4608, 40, 24),
+                                           (1, 2, 9000, 5), (2048, 2064, 40, 0)])
+def test_touched_line_classes_exact(bl, st, n, first):
+    """the sampled, period-scaled count equals a byte-by-byte count when the
+    sample covers every row"""
+    got = bench._line_classes(bl, st, n, first)
+    assert tuple(round(x, 6) for x in got) == _brute_classes(bl, st, n, first)
+
+
+def test_touched_model_headline_and_narrow_rows():
+    # headline: 512-B rows at 1024: reads 4 whole lines per row, writes whole lines
+    m = bench.touched_model(512, 1024, 1, 1 << 21, 0, 0)
+    assert m["pack_bytes"] == m["unpack_bytes"] == 2 * (1 << 30)
+    # 8 : 16, 1 GiB: every line read whole (2x the payload), every line has partly written sectors
+    m = bench.touched_model(8, 16, 1, 1 << 27, 0, 0)
+    lines = (1 << 31) // 128
+    assert m["pack_bytes"] == pytest.approx(lines * 128 + (1 << 30))
+    assert m["unpack_bytes"] == pytest.approx((1 << 30) + lines * bench.LINE_WRITE_PARTIAL)
+    # 64 : 512: one whole sector per touched line
+    m = bench.touched_model(64, 512, 1, 1 << 24, 0, 0)
+    assert m["unpack_bytes"] == pytest.approx((1 << 30) + (1 << 24) * bench.LINE_WRITE_HALF)
