@@ -17,6 +17,16 @@
 //   the same srand/rand and std::shuffle(default_random_engine) calls, so the
 //   matrix is the reference's own); time = max over ranks, min over
 //   iterations, as there. check: every received byte is the sender's pattern.
+//
+// tempi_bench_nbr_alltoallv: the reference's bench_nbr_alltoallv_random_sparse
+//   (/root/reference/bin/bench_nbr_alltoallv_random_sparse.cpp:100-330): the
+//   same matrix as a distributed graph (MPI_Dist_graph_create_adjacent over
+//   the nonzeros, weights = bytes, reorder = 1 as there, so TEMPI_PLACEMENT_*
+//   places the ranks), then MPI_BYTE MPI_Neighbor_alltoallv of device buffers
+//   with graph rank q sending row q of the matrix. Reported as there: setup
+//   (graph creation) and teardown (MPI_Comm_free) times, min over iterations
+//   of the max over ranks, and the pattern's bytes between and within nodes
+//   (:40-97) under the placement that was made.
 #include <hip/hip_runtime.h>
 #include <mpi.h>
 
@@ -177,11 +187,75 @@ EXPORT int tempi_bench_pingpong(int iters, long total, long bl, long stride, int
   return errors ? 3 : 0;
 }
 
-__global__ void a2av_fill(unsigned char *buf, const int64_t *displ, const int64_t *count, int n, int src) {
+// block d of buf (displ[d], count[d] bytes) gets the pattern of src -> dst[d]
+// (dst == nullptr: d itself)
+__global__ void a2av_fill(unsigned char *buf, const int64_t *displ, const int64_t *count, const int *dst, int n,
+                          int src) {
   for (int d = 0; d < n; ++d)
     for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < count[d]; i += int64_t(gridDim.x) * blockDim.x)
-      buf[displ[d] + i] = a2av_byte(i, src, d);
+      buf[displ[d] + i] = a2av_byte(i, src, dst ? dst[d] : d);
 }
+
+namespace {
+// blocks (displ, count) of a benchmark buffer get the patterns src -> dst[d]
+void fill_blocks(unsigned char *buf, const std::vector<int> &displ, const std::vector<int> &count,
+                 const std::vector<int> &dst, int src) {
+  const size_t n = displ.size();
+  if (host_buffers()) {
+    for (size_t d = 0; d < n; ++d)
+      for (int64_t i = 0; i < count[d]; ++i) buf[displ[d] + i] = a2av_byte(i, src, dst[d]);
+    return;
+  }
+  if (!n) return;
+  std::vector<int64_t> hd(displ.begin(), displ.end()), hc(count.begin(), count.end());
+  int64_t *dd, *dc;
+  int *dr;
+  HIPCHECK(hipMalloc(&dd, sizeof(int64_t) * n));
+  HIPCHECK(hipMalloc(&dc, sizeof(int64_t) * n));
+  HIPCHECK(hipMalloc(&dr, sizeof(int) * n));
+  HIPCHECK(hipMemcpy(dd, hd.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice));
+  HIPCHECK(hipMemcpy(dc, hc.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice));
+  HIPCHECK(hipMemcpy(dr, dst.data(), sizeof(int) * n, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(a2av_fill, dim3(256), dim3(256), 0, 0, buf, dd, dc, dr, int(n), src);
+  HIPCHECK(hipDeviceSynchronize());
+  HIPCHECK(hipFree(dd));
+  HIPCHECK(hipFree(dc));
+  HIPCHECK(hipFree(dr));
+}
+
+void fill_byte(void *buf, int v, size_t n) {
+  if (host_buffers())
+    std::memset(buf, v, n);
+  else
+    HIPCHECK(hipMemset(buf, v, n));
+}
+
+// node of every rank of comm, by world rank: TEMPI_FAKE_NODE_SIZE groups of
+// consecutive world ranks (the nodes TEMPI's placement sees in tests), else
+// the ranks sharing memory with it
+std::vector<int> node_of_ranks(MPI_Comm comm) {
+  int wr = 0, size = 0;
+  MPI_Comm_rank(MPI_COMM_WORLD, &wr);
+  MPI_Comm_size(comm, &size);
+  int node = wr;
+  const char *f = std::getenv("TEMPI_FAKE_NODE_SIZE");
+  if (f && std::atoi(f) > 0) {
+    node = wr / std::atoi(f);
+  } else {
+    MPI_Comm shm;
+    MPI_Comm_split_type(MPI_COMM_WORLD, MPI_COMM_TYPE_SHARED, 0, MPI_INFO_NULL, &shm);
+    MPI_Allreduce(MPI_IN_PLACE, &node, 1, MPI_INT, MPI_MIN, shm);
+    MPI_Comm_free(&shm);
+  }
+  std::vector<int> ids(static_cast<size_t>(size));
+  MPI_Allgather(&node, 1, MPI_INT, ids.data(), 1, MPI_INT, comm);
+  std::vector<int> distinct(ids);
+  std::sort(distinct.begin(), distinct.end());
+  distinct.erase(std::unique(distinct.begin(), distinct.end()), distinct.end());
+  for (int &i : ids) i = int(std::lower_bound(distinct.begin(), distinct.end(), i) - distinct.begin());
+  return ids; // 0 .. nodes - 1
+}
+} // namespace
 
 EXPORT int tempi_bench_alltoallv(int iters, int scale, double density, int seed, int check, int setDevice,
                                  char *json, int jsonCap) {
@@ -239,7 +313,7 @@ EXPORT int tempi_bench_alltoallv(int iters, int scale, double density, int seed,
     HIPCHECK(hipMalloc(&dc, sizeof(int64_t) * size_t(size)));
     HIPCHECK(hipMemcpy(dd, hd.data(), sizeof(int64_t) * size_t(size), hipMemcpyHostToDevice));
     HIPCHECK(hipMemcpy(dc, hc.data(), sizeof(int64_t) * size_t(size), hipMemcpyHostToDevice));
-    hipLaunchKernelGGL(a2av_fill, dim3(256), dim3(256), 0, 0, sbuf, dd, dc, size, rank);
+    hipLaunchKernelGGL(a2av_fill, dim3(256), dim3(256), 0, 0, sbuf, dd, dc, nullptr, size, rank);
     HIPCHECK(hipMemset(rbuf, 0xEE, size_t(std::max<int64_t>(rbytes, 1))));
     HIPCHECK(hipDeviceSynchronize());
     HIPCHECK(hipFree(dd));
@@ -271,6 +345,131 @@ EXPORT int tempi_bench_alltoallv(int iters, int scale, double density, int seed,
                   "\"max_gpu_out_or_in_bytes\": %lld, \"checked\": %s, \"errors\": %ld, \"buffers\": \"%s\"}",
                   size, scale, density, rowNnz, seed, iters, tmin * 1e6, trimean(times) * 1e6, (long long)total,
                   (long long)maxPair, (long long)maxOut, check ? "true" : "false", errors,
+                  host_buffers() ? "host" : "device");
+  }
+  buf_free(sbuf);
+  buf_free(rbuf);
+  return errors ? 3 : 0;
+}
+
+EXPORT int tempi_bench_nbr_alltoallv(int iters, int scale, double density, int seed, int reorder, int check,
+                                     int setDevice, char *json, int jsonCap) {
+  int wrank, size;
+  MPI_Comm_rank(MPI_COMM_WORLD, &wrank);
+  MPI_Comm_size(MPI_COMM_WORLD, &size);
+  if (setDevice) {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess) ndev = 0; // (host buffers need no GPU)
+    if (ndev > 0) HIPCHECK(hipSetDevice(wrank % ndev));
+  }
+  const int rowNnz = int(density * size + 0.5);
+  const std::vector<int64_t> mat = random_sparse(size, rowNnz, 1, 10, scale, seed);
+  auto M = [&](int r, int c) { return mat[size_t(r) * size_t(size) + size_t(c)]; };
+  // the graph: this process's row and column of the matrix
+  // (bench_nbr_alltoallv_random_sparse.cpp:143-152)
+  std::vector<int> sources, sourceweights, destinations, destweights;
+  for (int i = 0; i < size; ++i) {
+    if (M(wrank, i)) {
+      destinations.push_back(i);
+      destweights.push_back(int(M(wrank, i)));
+    }
+    if (M(i, wrank)) {
+      sources.push_back(i);
+      sourceweights.push_back(int(M(i, wrank)));
+    }
+  }
+  MPI_Comm graph;
+  MPI_Barrier(MPI_COMM_WORLD);
+  double t0 = MPI_Wtime();
+  MPI_Dist_graph_create_adjacent(MPI_COMM_WORLD, int(sources.size()), sources.data(), sourceweights.data(),
+                                 int(destinations.size()), destinations.data(), destweights.data(), MPI_INFO_NULL,
+                                 reorder, &graph);
+  double setup = MPI_Wtime() - t0;
+  MPI_Allreduce(MPI_IN_PLACE, &setup, 1, MPI_DOUBLE, MPI_MAX, MPI_COMM_WORLD);
+  // after placement this process is graph rank q and plays row q
+  // (:232-259): its neighbours as the graph reports them
+  int q = 0;
+  MPI_Comm_rank(graph, &q);
+  int indeg = 0, outdeg = 0, weighted = 0;
+  MPI_Dist_graph_neighbors_count(graph, &indeg, &outdeg, &weighted);
+  std::vector<int> in(static_cast<size_t>(indeg)), out(static_cast<size_t>(outdeg));
+  std::vector<int> iw(size_t(indeg) + 1), ow(size_t(outdeg) + 1);
+  MPI_Dist_graph_neighbors(graph, indeg, in.data(), iw.data(), outdeg, out.data(), ow.data());
+  std::vector<int> sc, sd, rc, rd;
+  int64_t sbytes = 0, rbytes = 0;
+  for (int d : out) {
+    sc.push_back(int(M(q, d)));
+    sd.push_back(int(sbytes));
+    sbytes += M(q, d);
+  }
+  for (int s : in) {
+    rc.push_back(int(M(s, q)));
+    rd.push_back(int(rbytes));
+    rbytes += M(s, q);
+  }
+  // the pattern's bytes between and within nodes under this placement (:40-97)
+  const std::vector<int> node = node_of_ranks(graph);
+  const int nodes = *std::max_element(node.begin(), node.end()) + 1;
+  std::vector<int64_t> nodeMat(size_t(nodes) * size_t(nodes), 0);
+  int64_t maxPair = 0;
+  for (int r = 0; r < size; ++r)
+    for (int c = 0; c < size; ++c) {
+      maxPair = std::max(maxPair, M(r, c));
+      nodeMat[size_t(node[size_t(r)]) * size_t(nodes) + size_t(node[size_t(c)])] += M(r, c);
+    }
+  int64_t maxOn = 0, maxOff = 0, totOn = 0, totOff = 0;
+  for (int i = 0; i < nodes; ++i) {
+    int64_t off = 0;
+    for (int j = 0; j < nodes; ++j) {
+      const int64_t v = nodeMat[size_t(i) * size_t(nodes) + size_t(j)];
+      if (i == j) {
+        totOn += v;
+        maxOn = std::max(maxOn, v);
+      } else {
+        off += v;
+      }
+    }
+    totOff += off;
+    maxOff = std::max(maxOff, off);
+  }
+  unsigned char *sbuf = static_cast<unsigned char *>(buf_alloc(size_t(sbytes)));
+  unsigned char *rbuf = static_cast<unsigned char *>(buf_alloc(size_t(rbytes)));
+  fill_blocks(sbuf, sd, sc, out, q);
+  fill_byte(rbuf, 0xEE, size_t(std::max<int64_t>(rbytes, 1)));
+  std::vector<double> times;
+  for (int i = 0; i < iters + 1; ++i) {
+    MPI_Barrier(MPI_COMM_WORLD);
+    const double ts = MPI_Wtime();
+    MPI_Neighbor_alltoallv(sbuf, sc.data(), sd.data(), MPI_BYTE, rbuf, rc.data(), rd.data(), MPI_BYTE, graph);
+    double el = MPI_Wtime() - ts;
+    MPI_Allreduce(MPI_IN_PLACE, &el, 1, MPI_DOUBLE, MPI_MAX, MPI_COMM_WORLD);
+    if (i >= 1) times.push_back(el);
+  }
+  long errors = 0;
+  if (check) {
+    std::vector<unsigned char> h(size_t(std::max<int64_t>(rbytes, 1)));
+    buf_copy(h.data(), rbuf, h.size());
+    for (size_t k = 0; k < in.size(); ++k)
+      for (int64_t i = 0; i < rc[k]; ++i)
+        if (h[size_t(rd[k] + i)] != a2av_byte(i, in[k], q)) ++errors;
+    MPI_Allreduce(MPI_IN_PLACE, &errors, 1, MPI_LONG, MPI_SUM, MPI_COMM_WORLD);
+  }
+  MPI_Barrier(MPI_COMM_WORLD);
+  t0 = MPI_Wtime();
+  MPI_Comm_free(&graph);
+  double teardown = MPI_Wtime() - t0;
+  MPI_Allreduce(MPI_IN_PLACE, &teardown, 1, MPI_DOUBLE, MPI_MAX, MPI_COMM_WORLD);
+  if (wrank == 0 && json && jsonCap > 0) {
+    const double tmin = times.empty() ? 0 : *std::min_element(times.begin(), times.end());
+    std::snprintf(json, size_t(jsonCap),
+                  "{\"ranks\": %d, \"scale\": %d, \"density\": %.4f, \"row_nnz\": %d, \"seed\": %d, "
+                  "\"iters\": %d, \"reorder\": %s, \"setup_us\": %.2f, \"min_us\": %.2f, \"trimean_us\": %.2f, "
+                  "\"teardown_us\": %.2f, \"max_pairwise_bytes\": %lld, \"nodes\": %d, \"max_on_node_bytes\": %lld, "
+                  "\"max_off_node_bytes\": %lld, \"total_on_node_bytes\": %lld, \"total_off_node_bytes\": %lld, "
+                  "\"checked\": %s, \"errors\": %ld, \"buffers\": \"%s\", \"api\": \"MPI_Neighbor_alltoallv\"}",
+                  size, scale, density, rowNnz, seed, iters, reorder ? "true" : "false", setup * 1e6, tmin * 1e6,
+                  trimean(times) * 1e6, teardown * 1e6, (long long)maxPair, nodes, (long long)maxOn,
+                  (long long)maxOff, (long long)totOn, (long long)totOff, check ? "true" : "false", errors,
                   host_buffers() ? "host" : "device");
   }
   buf_free(sbuf);

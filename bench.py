@@ -20,8 +20,9 @@ iteration) run through MPI_Isend/MPI_Irecv/MPI_Wait on the same ranks
 (strong scaling of the fixed grid), with its xGMI roofline. Under torchrun
 the ranks are wired into one MPI job by tempi_amd.pmi.
 
-At N > 1 the line also carries "pingpong" (config 3, ranks 0 <-> 1) and
-"alltoallv" (config 5, all ranks), each with its xGMI fraction.
+At N > 1 the line also carries "pingpong" (config 3, ranks 0 <-> 1),
+"alltoallv" (config 5, all ranks) and "nbr_alltoallv" (config 5's
+neighbourhood form), each with its xGMI fraction.
 
 Other modes (not the driver's line):
   --sweep FILE   the config-2 sweep (block 1 B - 4 KiB, 2D and 3D, 1 MiB -
@@ -582,6 +583,8 @@ def apps_lib():
                                        ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
     L.tempi_bench_alltoallv.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_int, ctypes.c_int,
                                         ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
+    L.tempi_bench_nbr_alltoallv.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_int, ctypes.c_int,
+                                            ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
     return L
 
 
@@ -680,6 +683,32 @@ def touched_model(bl, st, nplanes, rows, plane_stride, first):
     return {"pack_bytes": nplanes * touched * 128.0 + payload,
             "unpack_bytes": payload + nplanes * (whole * LINE_WRITE_WHOLE + half * LINE_WRITE_HALF +
                                                  partial * LINE_WRITE_PARTIAL)}
+
+
+def nbr_alltoallv(args, world):
+    """Config 5's neighbourhood form (bench_nbr_alltoallv_random_sparse.cpp):
+    the same matrices as a distributed graph created with reorder = 1 (the
+    reference's KaHIP remapping is a no-op on one node, F12), then MPI_BYTE
+    MPI_Neighbor_alltoallv of device buffers; min over iterations of the max
+    over ranks."""
+    import ctypes
+
+    L = apps_lib()
+    out = []
+    for scale, density in ((100000, 1.0), (100000, 0.5), (1000, 1.0)):
+        buf = ctypes.create_string_buffer(2048)
+        rc = L.tempi_bench_nbr_alltoallv(args.a2av_iters, scale, density, 101, 1, 0, 0, buf, 2048)
+        if rc != 0:
+            raise RuntimeError(f"neighbor alltoallv failed rc={rc}")
+        if buf.value:
+            r = json.loads(buf.value.decode())
+            lb = r["max_pairwise_bytes"] / (XGMI_LINK_GBS * 1e9)
+            r["lower_bound_us"] = round(lb * 1e6, 2)
+            r["xgmi_frac"] = round(lb / (r["min_us"] * 1e-6), 4) if r["min_us"] > 0 else None
+            out.append(r)
+    return {"workload": ("config 5, neighbourhood form: bench-nbr-alltoallv-random-sparse, the same matrices as "
+                         "MPI_Dist_graph_create_adjacent(reorder = 1) + MPI_Neighbor_alltoallv, device buffers"),
+            "points": out}
 
 
 def sweep(args, mpi, torch, dev, path, sizes=(1 << 20, 16 << 20, 256 << 20, 1 << 30), quiet=False):
@@ -891,9 +920,12 @@ def main():
             pp = sec.run("pingpong", pingpong, args, world)
             barrier(pg)
             a2 = sec.run("alltoallv", alltoallv, args, world)
+            barrier(pg)
+            na = sec.run("nbr_alltoallv", nbr_alltoallv, args, world)
             if rank == 0:
                 rec["pingpong"] = pp
                 rec["alltoallv"] = a2
+                rec["nbr_alltoallv"] = na
         if rank == 0 and world == 1:
             if not args.no_traffic:
                 tr = sec.run("traffic", run_traffic_passes, args, "pack_kernel")

@@ -1,7 +1,8 @@
 """Under torch.distributed.run (gloo, CPU): bench.py's own multi-rank
 plumbing -- dist_setup (gloo group + one MPI job wired over the torch
 ranks), barrier, the max / sum reductions of the timing -- and an MPI
-exchange through libtempi.so between the wired ranks."""
+exchange through libtempi.so between the wired ranks, and the line's
+config-5 sections (alltoallv, nbr_alltoallv) on host buffers."""
 import os
 import sys
 
@@ -26,6 +27,19 @@ got = mpi.Sendrecv(src.ctypes.data, 4096, mpi.BYTE, (rank + 1) % world, 9, dst.c
                    (rank - 1) % world, 9)
 assert got == ((rank - 1) % world, 9, 4096), got
 assert (dst == (rank - 1) % world).all()
+# the N > 1 line's config-5 sections, on host buffers (no GPU here)
+os.environ["TEMPI_BENCH_HOST"] = "1"
+
+
+class Args:
+    a2av_iters = 2
+
+
+for fn in (bench.alltoallv, bench.nbr_alltoallv):
+    sec = fn(Args, world)
+    if rank == 0:
+        assert len(sec["points"]) == 3 and all(p["errors"] == 0 and p["buffers"] == "host" for p in sec["points"]), sec
+        assert all(p["min_us"] > 0 and p["xgmi_frac"] is not None for p in sec["points"]), sec
 mpi.Finalize()
 print(f"RESULT ok rank={rank}", flush=True)
 pg.destroy_process_group()

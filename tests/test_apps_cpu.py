@@ -61,3 +61,38 @@ def test_alltoallv_host(mode, ranks, scale, density):
                                      str(density), "--check"], env=MODES[mode], timeout=120)
     r = _json(out)
     assert rc == 0 and r["checked"] and r["errors"] == 0 and r["buffers"] == "host", out[-3000:]
+
+
+@pytest.mark.parametrize("mode", list(MODES))
+@pytest.mark.parametrize("ranks,scale,density,extra", [
+    (8, 1000, 0.5, []), (8, 100000, 0.125, []), (3, 100, 1.0, []), (8, 10, 1.0, ["--no-reorder"]),
+    (8, 1000, 0.5, ["placed"])])
+def test_nbr_alltoallv_host(mode, ranks, scale, density, extra):
+    """config 5's neighbourhood form (bench_nbr_alltoallv_random_sparse): the
+    matrix as a distributed graph created with reorder = 1, then
+    MPI_Neighbor_alltoallv; "placed": TEMPI_PLACEMENT_KAHIP over two fake
+    nodes of 4 ranks (the library ignores it)"""
+    env = dict(MODES[mode])
+    if "placed" in extra:
+        env.update(TEMPI_PLACEMENT_KAHIP="", TEMPI_FAKE_NODE_SIZE="4")
+        extra = []
+    rc, out = mpi_launch.run(ranks, [os.path.join(LIB, "alltoallv_sparse"), "2", "--scale", str(scale), "--density",
+                                     str(density), "--check", "--neighbor"] + extra, env=env, timeout=120)
+    r = _json(out)
+    assert rc == 0 and r["checked"] and r["errors"] == 0 and r["buffers"] == "host", out[-3000:]
+    assert r["api"] == "MPI_Neighbor_alltoallv" and r["reorder"] == ("--no-reorder" not in extra)
+    assert r["total_on_node_bytes"] + r["total_off_node_bytes"] > 0
+
+
+def test_nbr_alltoallv_placement_cuts_off_node_bytes():
+    """with two fake nodes, TEMPI's placement of the reference's matrix moves
+    fewer bytes between nodes than the identity placement (reorder = 0)"""
+    env = dict(MODES["interposed"], TEMPI_PLACEMENT_KAHIP="", TEMPI_FAKE_NODE_SIZE="4")
+    off = {}
+    for extra in ([], ["--no-reorder"]):
+        rc, out = mpi_launch.run(8, [os.path.join(LIB, "alltoallv_sparse"), "1", "--scale", "1000", "--density",
+                                     "0.5", "--check", "--neighbor"] + extra, env=env, timeout=120)
+        r = _json(out)
+        assert rc == 0 and r["errors"] == 0 and r["nodes"] == 2, out[-3000:]
+        off[bool(extra)] = r["total_off_node_bytes"]
+    assert off[False] < off[True], off

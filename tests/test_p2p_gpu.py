@@ -192,6 +192,22 @@ def test_alltoallv_sparse_app(gpu, ranks, scale, density, env):
     assert rc == 0 and r["checked"] and r["errors"] == 0, out[-3000:]
 
 
+@pytest.mark.parametrize("ranks,scale,density,env", [
+    (2, 100000, 1.0, {}), (4, 1000, 0.5, {}), (3, 10, 1.0, {"TEMPI_DATATYPE_ONESHOT": "1"}),
+    (8, 1, 1.0, {}), (8, 100000, 0.5, {}), (8, 1000000, 0.125, {"TEMPI_STREAMS": "3"}),
+    # the reference's KaHIP remapping, over two fake nodes of 4 ranks
+    (8, 1000, 0.5, {"TEMPI_PLACEMENT_KAHIP": "", "TEMPI_FAKE_NODE_SIZE": "4"}),
+    (8, 100000, 1.0, {"TEMPI_PLACEMENT_METIS": "", "TEMPI_FAKE_NODE_SIZE": "2", "TEMPI_FAKE_FOREIGN_GPU": "1"})])
+def test_nbr_alltoallv_sparse_app(gpu, ranks, scale, density, env):
+    """config 5's neighbourhood form (bench_nbr_alltoallv_random_sparse.cpp:
+    distributed graph with reorder = 1, MPI_Neighbor_alltoallv of device
+    buffers), every byte checked"""
+    rc, out = mpi_launch.run(ranks, [os.path.join(LIB, "alltoallv_sparse"), "3", "--scale", str(scale), "--density",
+                                     str(density), "--check", "--neighbor"], env=env, timeout=240)
+    r = _json_line(out)
+    assert rc == 0 and r["checked"] and r["errors"] == 0 and r["buffers"] == "device", out[-3000:]
+
+
 @pytest.mark.parametrize("method", ["AUTO", "ONESHOT", "IPC", "STAGED", "XCOPY"])
 def test_completion_family_device(gpu, method):
     """TEMPI device requests mixed with library requests through
