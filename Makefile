@@ -18,7 +18,8 @@ HIPFLAGS := --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Iinclude -Wall
 CXXFLAGS := -std=c++17 -O2 -g -fPIC -fvisibility=hidden -Wall -Wextra -Wno-unused-parameter \
             -Iinclude -I$(MPI_HOME)/include
 
-APPS := $(LIB)/libtempi_apps.so $(LIB)/halo_exchange $(LIB)/pingpong_nd $(LIB)/alltoallv_sparse $(LIB)/measure_system
+APPS := $(LIB)/libtempi_apps.so $(LIB)/halo_exchange $(LIB)/pingpong_nd $(LIB)/alltoallv_sparse $(LIB)/measure_system \
+        $(LIB)/type_commit
 
 all: $(LIB)/libtempi.so $(APPS) oracle
 

@@ -221,6 +221,33 @@ def library_path_baselines(args):
     return out
 
 
+def type_commit_cost():
+    """MPI_Type_commit through libtempi (commit + canonical
+    descriptor) against the library's own commit (TEMPI_DISABLE=1), the
+    reference's bench_type_commit shapes and constructions (apps/
+    type_commit.cpp), each a one-rank child job on this host."""
+    import tempi_amd
+
+    env = {k: v for k, v in os.environ.items() if not k.startswith(("PMI_", "MPI_LOCAL", "HYDRA_"))}
+    env["HYDRA_LAUNCHER"] = "fork"
+    out = {}
+    for name, extra in (("tempi", {}), ("library", {"TEMPI_DISABLE": "1"})):
+        r = subprocess.run(["timeout", "-k", "10", "120", "/opt/conda/bin/mpiexec", "-n", "1",
+                            os.path.join(tempi_amd.LIBDIR, "type_commit"), "300"], stdout=subprocess.PIPE,
+                           stderr=subprocess.STDOUT, text=True, env=dict(env, **extra))
+        line = next((l for l in r.stdout.splitlines() if l.startswith("{")), None)
+        if r.returncode != 0 or line is None:
+            raise RuntimeError(f"type_commit ({name}) rc={r.returncode}: {r.stdout[-300:]}")
+        d = json.loads(line)
+        out[name] = {"commit_us_median": d["commit_us_median"], "commit_us_max": d["commit_us_max"],
+                     "per_factory_median_us": {k: sorted(v["commit_us"])[len(v["commit_us"]) // 2]
+                                               for k, v in d["factories"].items()}}
+    out["workload"] = ("bench_type_commit: 24 copy extents in a 1024^3-byte allocation x 5 constructions "
+                       "(subarray, byte_v_hv, byte_v1_hv_hv, byte_vn_hv_hv, subarray_v), create + commit + free "
+                       "300 times each, trimean; host only, one core")
+    return out
+
+
 def run_traffic_passes(args, kernel_substr):
     """rocprofv3 PMC passes (one counter group per run, child processes),
     gfx950 correction: FETCH_SIZE reads half of a wide streaming read
@@ -957,6 +984,7 @@ def main():
             if not args.no_cpu_baseline:
                 rec["cpu_baseline"] = sec.run("cpu_baseline", cpu_baseline, mpi, args.pitch, args.block,
                                               args.cpu_seconds)
+                rec["type_commit"] = sec.run("type_commit", type_commit_cost)
                 lb = sec.run("cpu_baselines_configs_3_5", library_path_baselines, args)
                 if lb:
                     rec["cpu_baselines_configs_3_5"] = lb

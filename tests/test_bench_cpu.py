@@ -130,3 +130,13 @@ def test_touched_model_headline_and_narrow_rows():
     # 64 : 512: one whole sector per touched line
     m = bench.touched_model(64, 512, 1, 1 << 24, 0, 0)
     assert m["unpack_bytes"] == pytest.approx((1 << 30) + (1 << 24) * bench.LINE_WRITE_HALF)
+
+
+def test_type_commit_cost_section():
+    """the line's type_commit section: the reference's bench_type_commit
+    shapes through libtempi and through the library alone"""
+    r = bench.type_commit_cost()
+    for k in ("tempi", "library"):
+        assert 0 < r[k]["commit_us_median"] <= r[k]["commit_us_max"]
+        assert set(r[k]["per_factory_median_us"]) == {"subarray", "byte_v_hv", "byte_v1_hv_hv", "byte_vn_hv_hv",
+                                                      "subarray_v"}
