@@ -1,14 +1,15 @@
 """Busy / idle time of the GPU over a halo kernel trace (tools/gpu_halo_trace.sh):
 per kernel name the total time, and over the timed window the union of
-kernel intervals (busy) against the window (busy + gaps)."""
+kernel intervals (busy) against the window (busy + gaps). Several trace
+files (one per process of a multi-rank run on one GPU) are merged."""
 import csv
 import glob
 import sys
 from collections import defaultdict
 
-path = glob.glob((sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/halo_trace") + "/**/*kernel_trace.csv",
-                 recursive=True)[0]
-rows = list(csv.DictReader(open(path)))
+paths = glob.glob((sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/halo_trace") + "/**/*kernel_trace.csv",
+                  recursive=True)
+rows = [r for p in paths for r in csv.DictReader(open(p))]
 ks = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows)
 copies = [k for k in ks if "copy" in k[2] or "pack" in k[2]]
 # skip the warm-up iteration: the first 1/11 of the copy launches
