@@ -524,17 +524,21 @@ def node_perf_model(args, mpi, pg, rank, world, shared_gpu):
     path = os.path.join(tempi_cache_dir(), "perf.json")
     info = {"perf_json": path, "measured_here": False}
     if rank == 0 and not os.path.exists(path) and not args.no_measure_system:
-        os.makedirs(os.path.dirname(path), exist_ok=True)
-        env = {k: v for k, v in os.environ.items() if not k.startswith(("PMI_", "MPI_LOCAL", "HYDRA_"))}
-        env["HYDRA_LAUNCHER"] = "fork"
-        exe = os.path.join(tempi_amd.LIBDIR, "measure_system")
-        t0 = time.perf_counter()
-        r = subprocess.run(["timeout", "-k", "10", "120", "/opt/conda/bin/mpiexec", "-n", "2", exe, "--quick", "--out",
-                            path], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env)
-        info["measure_seconds"] = round(time.perf_counter() - t0, 1)
-        info["measured_here"] = r.returncode == 0 and os.path.exists(path)
-        if not info["measured_here"]:
-            info["measure_error"] = (r.stdout or "")[-400:]
+        # (a failure here must not skip the barrier below: every rank waits there)
+        try:
+            os.makedirs(os.path.dirname(path), exist_ok=True)
+            env = {k: v for k, v in os.environ.items() if not k.startswith(("PMI_", "MPI_LOCAL", "HYDRA_"))}
+            env["HYDRA_LAUNCHER"] = "fork"
+            exe = os.path.join(tempi_amd.LIBDIR, "measure_system")
+            t0 = time.perf_counter()
+            r = subprocess.run(["timeout", "-k", "10", "120", "/opt/conda/bin/mpiexec", "-n", "2", exe, "--quick",
+                                "--out", path], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env)
+            info["measure_seconds"] = round(time.perf_counter() - t0, 1)
+            info["measured_here"] = r.returncode == 0 and os.path.exists(path)
+            if not info["measured_here"]:
+                info["measure_error"] = (r.stdout or "")[-400:]
+        except Exception as e:
+            info["measure_error"] = f"{type(e).__name__}: {e}"
     barrier(pg)
     mpi.L.tempi_perf_reload()
     buf = ctypes.create_string_buffer(4096)
