@@ -1069,36 +1069,26 @@ struct CArgs {
   uint32_t flags; // TEMPI_HIP_ITEM_REMOTE: the source is another process's memory
 };
 
-// A system-scope (sc0 sc1) load through the flat global path, complete on
-// return: the source side of a copy may have any stride sign, so the
-// wave-uniform buffer base of ld_remote cannot be used. One load in flight
-// per lane is enough here: these reads cross xGMI, whose link rate, not the
-// latency, bounds them (256 CUs x 8 waves x 64 lanes x 8 B in flight / ~2 us
-// is well over a link's bandwidth).
+// A system-scope load through the flat global path: a relaxed atomic load at
+// system scope, which gfx950 issues as global_load_* sc0 sc1 (the same cache
+// policy as ld_remote's) and which the compiler tracks like any other load,
+// so every load of a lane's words is in flight at once. (The source side of a
+// copy may have any stride sign, so the wave-uniform buffer base of ld_remote
+// cannot be used.) A 16-byte word is two 8-byte loads.
 template <typename T> __device__ __forceinline__ T ld_sys(const T *p) {
   T v;
   if constexpr (sizeof(T) == 16) {
-    u32x4 x;
-    asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=v"(x) : "v"(p) : "memory");
-    __builtin_memcpy(&v, &x, 16);
-  } else if constexpr (sizeof(T) == 8) {
-    u32x2 x;
-    asm volatile("global_load_dwordx2 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=v"(x) : "v"(p) : "memory");
-    __builtin_memcpy(&v, &x, 8);
-  } else if constexpr (sizeof(T) == 4) {
-    uint32_t x;
-    asm volatile("global_load_dword %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=v"(x) : "v"(p) : "memory");
-    __builtin_memcpy(&v, &x, 4);
-  } else if constexpr (sizeof(T) == 2) {
-    uint32_t x;
-    asm volatile("global_load_ushort %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=v"(x) : "v"(p) : "memory");
-    const uint16_t h = uint16_t(x);
-    __builtin_memcpy(&v, &h, 2);
+    const uint64_t *q = reinterpret_cast<const uint64_t *>(p);
+    const uint64_t x[2] = {__hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM),
+                           __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)};
+    __builtin_memcpy(&v, x, 16);
   } else {
-    uint32_t x;
-    asm volatile("global_load_ubyte %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=v"(x) : "v"(p) : "memory");
-    const uint8_t b = uint8_t(x);
-    __builtin_memcpy(&v, &b, 1);
+    typedef typename std::conditional<
+        sizeof(T) == 8, uint64_t,
+        typename std::conditional<sizeof(T) == 4, uint32_t,
+                                  typename std::conditional<sizeof(T) == 2, uint16_t, uint8_t>::type>::type>::type U;
+    const U x = __hip_atomic_load(reinterpret_cast<const U *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __builtin_memcpy(&v, &x, sizeof(T));
   }
   return v;
 }

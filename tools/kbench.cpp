@@ -2,9 +2,12 @@
 //
 // usage: kbench LIB.so REPS SHAPE...   where SHAPE = block:count1:stride1[:count2:stride2]
 //   (dims outermost first after the block, e.g. 512:2097152:1024)
-// Also times hipMemcpyAsync D2D of the same payload (achievable-copy peak).
+// Also times hipMemcpyAsync D2D of the same payload (achievable-copy peak), and
+// the strided -> strided copy kernel between two objects of this shape, with
+// plain loads and with the source flagged TEMPI_HIP_ITEM_REMOTE (the
+// system-scope loads a reader on another GPU uses; here on local memory).
 // Prints one JSON line per shape: kernel ms (HIP events, back-to-back
-// launches) and algorithmic GB/s (2 x payload per pack or unpack).
+// launches) and algorithmic GB/s (2 x payload per pack, unpack or copy).
 #include "tempi_hip.h"
 
 #include <cstdio>
@@ -32,6 +35,7 @@ int main(int argc, char **argv) {
   SYM(tempi_hip_stream_create) SYM(tempi_hip_event_create) SYM(tempi_hip_event_record)
   SYM(tempi_hip_event_synchronize) SYM(tempi_hip_event_elapsed_ms) SYM(tempi_hip_memcpy_async)
   SYM(tempi_hip_memset_async) SYM(tempi_hip_stream_synchronize) SYM(tempi_hip_desc_bytes)
+  SYM(tempi_hip_copy_batch)
   const int reps = std::atoi(argv[2]);
   void *s, *e0, *e1;
   CK(tempi_hip_stream_create(&s));
@@ -58,23 +62,29 @@ int main(int argc, char **argv) {
     // extent: outermost count * stride (enough for positive strides)
     extent = d.ndims ? d.counts[0] * d.strides[0] : d.block;
     const long long payload = tempi_hip_desc_bytes(&d);
-    void *strided, *packed;
+    void *strided, *packed, *other = nullptr;
     CK(tempi_hip_malloc(&strided, size_t(extent)));
     CK(tempi_hip_malloc(&packed, size_t(payload)));
     CK(tempi_hip_memset_async(strided, 1, size_t(extent), s));
-    float ms[3];
-    for (int mode = 0; mode < 3; ++mode) {
-      for (int w = 0; w < 2; ++w) { // warm-up
-        if (mode == 0) CK(tempi_hip_pack(packed, strided, &d, s));
-        if (mode == 1) CK(tempi_hip_unpack(strided, packed, &d, s));
-        if (mode == 2) CK(tempi_hip_memcpy_async(packed, strided, size_t(payload), s));
-      }
+    const bool copies = std::getenv("KBENCH_NO_COPY") == nullptr;
+    if (copies) CK(tempi_hip_malloc(&other, size_t(extent)));
+    tempi_hip_copy_item ci{};
+    ci.dst_first = other;
+    ci.src_first = strided;
+    ci.dst = d;
+    ci.src = d;
+    float ms[5] = {0, 0, 0, 0, 0};
+    for (int mode = 0; mode < (copies ? 5 : 3); ++mode) {
+      ci.flags = mode == 4 ? TEMPI_HIP_ITEM_REMOTE : 0;
+      auto run = [&]() -> int {
+        if (mode == 0) return tempi_hip_pack(packed, strided, &d, s);
+        if (mode == 1) return tempi_hip_unpack(strided, packed, &d, s);
+        if (mode == 2) return tempi_hip_memcpy_async(packed, strided, size_t(payload), s);
+        return tempi_hip_copy_batch(&ci, 1, s);
+      };
+      for (int w = 0; w < 2; ++w) CK(run()); // warm-up
       CK(tempi_hip_event_record(e0, s));
-      for (int r = 0; r < reps; ++r) {
-        if (mode == 0) CK(tempi_hip_pack(packed, strided, &d, s));
-        if (mode == 1) CK(tempi_hip_unpack(strided, packed, &d, s));
-        if (mode == 2) CK(tempi_hip_memcpy_async(packed, strided, size_t(payload), s));
-      }
+      for (int r = 0; r < reps; ++r) CK(run());
       CK(tempi_hip_event_record(e1, s));
       CK(tempi_hip_event_synchronize(e1));
       CK(tempi_hip_event_elapsed_ms(&ms[mode], e0, e1));
@@ -82,11 +92,14 @@ int main(int argc, char **argv) {
     }
     auto gbs = [&](float m) { return 2.0 * double(payload) / (double(m) * 1e-3) / 1e9; };
     std::printf("{\"lib\": \"%s\", \"shape\": \"%s\", \"payload\": %lld, \"pack_ms\": %.4f, \"unpack_ms\": %.4f, "
-                "\"memcpy_ms\": %.4f, \"pack_gbs\": %.1f, \"unpack_gbs\": %.1f, \"memcpy_gbs\": %.1f}\n",
-                argv[1], argv[a], payload, ms[0], ms[1], ms[2], gbs(ms[0]), gbs(ms[1]), gbs(ms[2]));
+                "\"memcpy_ms\": %.4f, \"pack_gbs\": %.1f, \"unpack_gbs\": %.1f, \"memcpy_gbs\": %.1f, "
+                "\"copy_gbs\": %.1f, \"copy_remote_gbs\": %.1f}\n",
+                argv[1], argv[a], payload, ms[0], ms[1], ms[2], gbs(ms[0]), gbs(ms[1]), gbs(ms[2]),
+                copies ? gbs(ms[3]) : 0.0, copies ? gbs(ms[4]) : 0.0);
     std::fflush(stdout);
     tempi_hip_free(strided);
     tempi_hip_free(packed);
+    if (other) tempi_hip_free(other);
   }
   return 0;
 }
