@@ -19,7 +19,7 @@ CXXFLAGS := -std=c++17 -O2 -g -fPIC -fvisibility=hidden -Wall -Wextra -Wno-unuse
             -Iinclude -I$(MPI_HOME)/include
 
 APPS := $(LIB)/libtempi_apps.so $(LIB)/halo_exchange $(LIB)/pingpong_nd $(LIB)/alltoallv_sparse $(LIB)/measure_system \
-        $(LIB)/type_commit
+        $(LIB)/type_commit $(LIB)/mpi_pack
 
 all: $(LIB)/libtempi.so $(APPS) oracle
 

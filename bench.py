@@ -248,6 +248,57 @@ def type_commit_cost():
     return out
 
 
+def mpi_pack_bench():
+    """The reference's own headline benchmark, bench_mpi_pack
+    (/root/reference/bin/bench_mpi_pack.cpp; its README chart is MPI_Pack
+    speedup over the library): 2D byte objects of 1 KiB / 1 MiB / 4 MiB per
+    element, count 1 and 2, rows of 1-512 B at a 512-B stride, vector /
+    hvector / subarray, API-level MiB/s (MPI_Wtime per call, trimean).
+    Through libtempi on device buffers (100 calls), and the library's CPU
+    path on host buffers (TEMPI_DISABLE=1, 3 calls as the reference's
+    no-TEMPI runs use few; subarray only, the library packs all three the
+    same way), each a one-rank child job (apps/mpi_pack.cpp)."""
+    import tempi_amd
+
+    env = {k: v for k, v in os.environ.items() if not k.startswith(("PMI_", "MPI_LOCAL", "HYDRA_"))}
+    env["HYDRA_LAUNCHER"] = "fork"
+    exe = os.path.join(tempi_amd.LIBDIR, "mpi_pack")
+
+    def run(argv, extra, timeout):
+        r = subprocess.run(["timeout", "-k", "10", str(timeout), "/opt/conda/bin/mpiexec", "-n", "1", exe] + argv,
+                           stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=dict(env, **extra))
+        recs = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+        if r.returncode != 0 or not recs:
+            raise RuntimeError(f"mpi_pack rc={r.returncode}: {r.stdout[-300:]}")
+        return recs
+
+    gpu = run(["100"], {}, 240)
+    lib = {(p["target"], p["count"], p["block"]): p
+           for p in run(["3", "--host", "--factory", "subarray"], {"TEMPI_DISABLE": "1"}, 240)}
+    points, speedups = [], {}
+    for p in gpu:
+        key = (p["target"], p["count"], p["block"])
+        q = {"target": p["target"], "count": p["count"], "block": p["block"], "factory": p["factory"],
+             "pack_MiBps": p["pack_MiBps"], "unpack_MiBps": p["unpack_MiBps"], "errors": p["errors"]}
+        if key in lib and lib[key]["pack_us"] > 0.01 and p["pack_us"] > 0:  # (below the library's timer tick)
+            s = lib[key]["pack_us"] / p["pack_us"]
+            q["library_pack_MiBps"] = lib[key]["pack_MiBps"]
+            q["pack_speedup"] = float(f"{s:.3g}")
+            speedups.setdefault(p["target"], []).append(s)
+        points.append(q)
+
+    def gm(xs):
+        return math.exp(sum(math.log(x) for x in xs) / len(xs))
+
+    return {"workload": ("bench_mpi_pack: MPI_Pack / MPI_Unpack of 2D byte vector / hvector / subarray objects, "
+                         "1 KiB / 1 MiB / 4 MiB per element, count 1-2, rows 1-512 B at stride 512, one rank; "
+                         "MiB/s of packed bytes per API call (trimean)"),
+            "errors": sum(p["errors"] for p in gpu),
+            "pack_speedup_geomean_by_target": {str(t): float(f"{gm(v):.3g}") for t, v in sorted(speedups.items())},
+            "library": "MPICH 3.3.2 MPI_Pack on pageable host buffers, TEMPI_DISABLE=1, one core of " + _cpu_model(),
+            "points": points}
+
+
 def run_traffic_passes(args, kernel_substr):
     """rocprofv3 PMC passes (one counter group per run, child processes),
     gfx950 correction: FETCH_SIZE reads half of a wide streaming read
@@ -989,6 +1040,7 @@ def main():
                 rec["cpu_baseline"] = sec.run("cpu_baseline", cpu_baseline, mpi, args.pitch, args.block,
                                               args.cpu_seconds)
                 rec["type_commit"] = sec.run("type_commit", type_commit_cost)
+                rec["mpi_pack"] = sec.run("mpi_pack", mpi_pack_bench)
                 lb = sec.run("cpu_baselines_configs_3_5", library_path_baselines, args)
                 if lb:
                     rec["cpu_baselines_configs_3_5"] = lb

@@ -96,3 +96,14 @@ def test_nbr_alltoallv_placement_cuts_off_node_bytes():
         assert rc == 0 and r["errors"] == 0 and r["nodes"] == 2, out[-3000:]
         off[bool(extra)] = r["total_off_node_bytes"]
     assert off[False] < off[True], off
+
+
+@pytest.mark.parametrize("mode", list(MODES))
+def test_mpi_pack_host(mode):
+    """the reference's bench_mpi_pack shapes (1 KiB per element here) on host
+    buffers: every point's packed bytes checked against the type map"""
+    rc, out = mpi_launch.run(1, [os.path.join(LIB, "mpi_pack"), "2", "--host", "--max-target", "1024"],
+                             env=MODES[mode], timeout=120)
+    recs = [json.loads(l) for l in out.splitlines() if l.startswith("{")]
+    assert rc == 0 and len(recs) == 2 * 9 * 3, out[-3000:]
+    assert all(r["errors"] == 0 and r["buffers"] == "host" and r["pack_MiBps"] > 0 for r in recs)
