@@ -46,6 +46,8 @@ typedef struct tempi_counters_t {
   uint64_t canary_ok;   /* peers on another GPU whose mapped memory read back right at first contact */
   uint64_t canary_fail; /* ... and those that did not (IPC with them off: host-staged transfers) */
   uint64_t self_matched; /* messages to this same process matched inside TEMPI (no library message) */
+  uint64_t staged_packs;   /* MPI_Pack of a GPU object into pageable host memory (through a pinned slab) */
+  uint64_t staged_unpacks; /* MPI_Unpack into a GPU object from pageable host memory */
 } tempi_counters_t;
 void tempi_get_counters(tempi_counters_t *out);
 void tempi_reset_counters(void);

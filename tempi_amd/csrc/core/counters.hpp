@@ -14,6 +14,8 @@ struct Counters {
   uint64_t pack_bytes = 0, unpack_bytes = 0;
   uint64_t launches = 0;
   uint64_t lib_packs = 0, lib_unpacks = 0; // handed to the library
+  // GPU packs into / unpacks from pageable host memory through a pinned slab
+  uint64_t staged_packs = 0, staged_unpacks = 0;
   uint64_t sends = 0, recvs = 0, isends = 0, irecvs = 0;
   uint64_t send_device = 0, send_oneshot = 0, send_staged = 0, send_ipc = 0;
   uint64_t lib_sends = 0, lib_recvs = 0;

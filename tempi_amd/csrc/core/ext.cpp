@@ -71,6 +71,8 @@ TEMPI_EXPORT void tempi_get_counters(tempi_counters_t *o) {
   o->canary_ok = c.canary_ok;
   o->canary_fail = c.canary_fail;
   o->self_matched = c.self_matched;
+  o->staged_packs = c.staged_packs;
+  o->staged_unpacks = c.staged_unpacks;
 }
 
 TEMPI_EXPORT void tempi_reset_counters(void) { counters = Counters(); }

@@ -29,6 +29,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #define TEMPI_EXPORT extern "C" __attribute__((visibility("default")))
@@ -271,17 +272,29 @@ int pack(const void *inbuf, int incount, MPI_Datatype datatype, void *outbuf, in
     return library_pack(inbuf, incount, datatype, outbuf, outsize, position, comm);
   const char *first = static_cast<const char *>(inbuf) + rec->desc.start;
   const gpu::Ptr src = gpu::classify(first);
-  const gpu::Ptr dst = gpu::classify(static_cast<char *>(outbuf) + *position);
-  if (!src.device_accessible || !dst.device_accessible)
+  if (!src.device_accessible)
     return library_pack(inbuf, incount, datatype, outbuf, outsize, position, comm);
+  const gpu::Ptr dst = gpu::classify(static_cast<char *>(outbuf) + *position);
   const int64_t bytes = rec->packer->packed_bytes(incount);
   if (*position < 0 || int64_t(*position) + bytes > int64_t(outsize))
     return raise_error(comm, MPI_ERR_TRUNCATE);
   const char *origin = static_cast<const char *>(src.dptr) - rec->desc.start;
+  // a GPU object packed into pageable host memory: the kernel gathers into a
+  // pinned, mapped slab (as the ONESHOT sender does) and the packed bytes are
+  // copied out on the host -- only the payload crosses the host link, where
+  // the library route would copy the object's whole span and pack on the CPU
+  Slab *stage = dst.device_accessible ? nullptr : pinned_pool().get(size_t(std::max<int64_t>(bytes, 1)), src.device);
+  if (!dst.device_accessible && !stage)
+    return library_pack(inbuf, incount, datatype, outbuf, outsize, position, comm);
   const int e = on_device(src.device, true, [&](void *s) {
-    return rec->packer->pack_async(dst.dptr, origin, incount, s);
+    return rec->packer->pack_async(stage ? stage->dev : dst.dptr, origin, incount, s);
   });
   gpu::check(e, "MPI_Pack");
+  if (stage) {
+    counters.staged_packs++;
+    std::memcpy(static_cast<char *>(outbuf) + *position, stage->host, size_t(bytes));
+    pinned_pool().put(stage);
+  }
   *position += int(bytes);
   return MPI_SUCCESS;
 }
@@ -295,17 +308,27 @@ int unpack(const void *inbuf, int insize, int *position, void *outbuf, int outco
     return library_unpack(inbuf, insize, position, outbuf, outcount, datatype, comm);
   char *first = static_cast<char *>(outbuf) + rec->desc.start;
   const gpu::Ptr dst = gpu::classify(first);
-  const gpu::Ptr src = gpu::classify(static_cast<const char *>(inbuf) + *position);
-  if (!src.device_accessible || !dst.device_accessible)
+  if (!dst.device_accessible)
     return library_unpack(inbuf, insize, position, outbuf, outcount, datatype, comm);
+  const gpu::Ptr src = gpu::classify(static_cast<const char *>(inbuf) + *position);
   const int64_t bytes = rec->packer->packed_bytes(outcount);
   if (*position < 0 || int64_t(*position) + bytes > int64_t(insize))
     return raise_error(comm, MPI_ERR_TRUNCATE);
   char *origin = static_cast<char *>(dst.dptr) - rec->desc.start;
+  // packed bytes in pageable host memory: copied into a pinned, mapped slab
+  // on the host, scattered from there by the kernel (the ONESHOT receive)
+  Slab *stage = src.device_accessible ? nullptr : pinned_pool().get(size_t(std::max<int64_t>(bytes, 1)), dst.device);
+  if (!src.device_accessible && !stage)
+    return library_unpack(inbuf, insize, position, outbuf, outcount, datatype, comm);
+  if (stage) {
+    counters.staged_unpacks++;
+    std::memcpy(stage->host, static_cast<const char *>(inbuf) + *position, size_t(bytes));
+  }
   const int e = on_device(dst.device, false, [&](void *s) {
-    return rec->packer->unpack_async(origin, src.dptr, outcount, s);
+    return rec->packer->unpack_async(origin, stage ? stage->dev : src.dptr, outcount, s);
   });
   gpu::check(e, "MPI_Unpack");
+  if (stage) pinned_pool().put(stage);
   *position += int(bytes);
   return MPI_SUCCESS;
 }

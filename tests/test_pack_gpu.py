@@ -263,17 +263,48 @@ def test_pinned_host_output(mpi, gpu):
         mpi.Type_free(t)
 
 
-def test_device_to_pageable_host(mpi, gpu):
-    """Device source, pageable host destination: handled (library with host
-    staging), bit-exact."""
+@pytest.mark.parametrize("count,prefix", [(1, 0), (2, 5), (3, 13)])
+def test_device_to_pageable_host(mpi, gpu, count, prefix):
+    """Device object, pageable host packed buffer (both directions): the GPU
+    kernel gathers into / scatters from a pinned slab (no library pack, no
+    copy of the object's span), bit-exact, at odd positions; bytes before the
+    position and gap bytes untouched"""
     torch = _torch()
     t = mpi.Type_commit(mpi.Type_vector(1000, 12, 40, mpi.BYTE))
     try:
-        src = torch.randint(0, 256, (40000,), dtype=torch.uint8, device=gpu)
-        out = np.zeros(12000, dtype=np.uint8)
+        ext = 999 * 40 + 12
+        src = torch.randint(0, 256, (ext * count,), dtype=torch.uint8, device=gpu)
+        n = 12000 * count
+        out = np.full(prefix + n + 7, 0xA5, dtype=np.uint8)
         torch.cuda.synchronize()
-        mpi.Pack(src.data_ptr(), 1, t, out.ctypes.data, 12000, 0)
-        assert np.array_equal(out, to_np(src.view(1000, 40)[:, :12]).reshape(-1))
+        before = mpi.counters()
+        pos = mpi.Pack(src.data_ptr(), count, t, out.ctypes.data, prefix + n, prefix)
+        after = mpi.counters()
+        assert pos == prefix + n
+        assert after["staged_packs"] == before["staged_packs"] + 1 and after["lib_packs"] == before["lib_packs"]
+        hs = to_np(src)
+        exp = np.concatenate([hs[e * ext + r * 40:e * ext + r * 40 + 12] for e in range(count) for r in range(1000)])
+        assert np.array_equal(out[prefix:prefix + n], exp)
+        assert (out[:prefix] == 0xA5).all() and (out[prefix + n:] == 0xA5).all()
+        # and back into a device object whose gaps must keep their bytes
+        dst = torch.full((ext * count,), 0x3C, dtype=torch.uint8, device=gpu)
+        torch.cuda.synchronize()
+        upos = mpi.Unpack(out.ctypes.data, prefix + n, prefix, dst.data_ptr(), count, t)
+        assert upos == prefix + n and mpi.counters()["staged_unpacks"] == after["staged_unpacks"] + 1
+        hd = to_np(dst)
+        ref = np.full(ext * count, 0x3C, dtype=np.uint8)
+        for e in range(count):
+            for r in range(1000):
+                ref[e * ext + r * 40:e * ext + r * 40 + 12] = hs[e * ext + r * 40:e * ext + r * 40 + 12]
+        assert np.array_equal(hd, ref)
+        # a packed buffer too small: MPI_ERR_TRUNCATE, nothing written
+        assert mpi.L.MPI_Comm_set_errhandler(mpi.COMM_WORLD, mpi.const("MPI_ERRORS_RETURN")) == 0
+        try:
+            out[:] = 0xA5
+            rc, p2 = mpi.Pack_rc(src.data_ptr(), count, t, out.ctypes.data, prefix + n - 1, prefix)
+            assert rc == mpi.ERR_TRUNCATE and p2 == prefix and (out == 0xA5).all()
+        finally:
+            mpi.L.MPI_Comm_set_errhandler(mpi.COMM_WORLD, mpi.const("MPI_ERRORS_ARE_FATAL"))
     finally:
         mpi.Type_free(t)
 
