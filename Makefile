@@ -18,7 +18,8 @@ HIPFLAGS := --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Iinclude -Wall
 CXXFLAGS := -std=c++17 -O2 -g -fPIC -fvisibility=hidden -Wall -Wextra -Wno-unused-parameter \
             -Iinclude -I$(MPI_HOME)/include
 
-APPS := $(LIB)/libtempi_apps.so $(LIB)/halo_exchange $(LIB)/pingpong_nd $(LIB)/alltoallv_sparse $(LIB)/measure_system \
+APPS := $(LIB)/libtempi_apps.so $(LIB)/halo_exchange $(LIB)/pingpong_nd $(LIB)/pingpong_1d $(LIB)/alltoallv_sparse \
+        $(LIB)/measure_system \
         $(LIB)/type_commit $(LIB)/mpi_pack
 
 all: $(LIB)/libtempi.so $(APPS) oracle
@@ -52,6 +53,10 @@ $(LIB)/halo_exchange: apps/halo_exchange_main.cpp $(LIB)/libtempi_apps.so
 	    -ltempi -L$(MPI_HOME)/lib -lmpi -static-libstdc++ -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,$(MPI_HOME)/lib
 
 $(LIB)/pingpong_nd: apps/pingpong_nd.cpp $(LIB)/libtempi_apps.so
+	$(HIPCC) --offload-arch=gfx950 -O2 -std=c++17 -Iinclude -I$(MPI_HOME)/include -o $@ $< -L$(LIB) -ltempi_apps \
+	    -ltempi -L$(MPI_HOME)/lib -lmpi -static-libstdc++ -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,$(MPI_HOME)/lib
+
+$(LIB)/pingpong_1d: apps/pingpong_1d.cpp $(LIB)/libtempi_apps.so
 	$(HIPCC) --offload-arch=gfx950 -O2 -std=c++17 -Iinclude -I$(MPI_HOME)/include -o $@ $< -L$(LIB) -ltempi_apps \
 	    -ltempi -L$(MPI_HOME)/lib -lmpi -static-libstdc++ -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,$(MPI_HOME)/lib
 

@@ -9,6 +9,13 @@
 //   round trips / 2. Ranks other than 0 and 1 only take part in the barriers.
 //   check: every block holds rank 0's bytes afterwards, every gap its owner's.
 //
+// tempi_bench_pingpong_1d: the reference's bench_mpi_pingpong_1d
+//   (/root/reference/bin/bench_mpi_pingpong_1d.cpp:29-100, 119-165): MPI_BYTE
+//   count = total, device buffers, every rank r < size/2 paired with
+//   r + size/2 (all pairs at once), MPI_Send then MPI_Recv (the partner
+//   Recv then Send); time = max over ranks per iteration, trimean, one-way =
+//   half of it. check: every rank's receive buffer holds its partner's bytes.
+//
 // tempi_bench_alltoallv: the reference's bench_alltoallv_random_sparse
 //   (/root/reference/bin/bench_alltoallv_random_sparse.cpp:100-222): an
 //   MPI_BYTE MPI_Alltoallv of device buffers whose counts are the matrix of
@@ -189,6 +196,60 @@ EXPORT int tempi_bench_pingpong(int iters, long total, long bl, long stride, int
 
 // block d of buf (displ[d], count[d] bytes) gets the pattern of src -> dst[d]
 // (dst == nullptr: d itself)
+EXPORT int tempi_bench_pingpong_1d(int iters, long total, int check, int setDevice, char *json, int jsonCap) {
+  int rank, size;
+  MPI_Comm_rank(MPI_COMM_WORLD, &rank);
+  MPI_Comm_size(MPI_COMM_WORLD, &size);
+  if (size < 2 || total <= 0 || total > (1L << 30)) return 2;
+  if (setDevice) {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess) ndev = 0; // (host buffers need no GPU)
+    if (ndev > 0) HIPCHECK(hipSetDevice(rank % ndev));
+  }
+  const int half = size / 2;
+  const int partner = rank < half ? rank + half : (rank < 2 * half ? rank - half : -1); // odd size: the last idles
+  char *src = static_cast<char *>(buf_alloc(size_t(total)));
+  char *dst = static_cast<char *>(buf_alloc(size_t(total)));
+  std::vector<unsigned char> h(static_cast<size_t>(total));
+  for (size_t i = 0; i < h.size(); ++i) h[i] = (unsigned char)((i * 7 + size_t(rank) * 31) & 0xFF);
+  buf_copy(src, h.data(), h.size());
+  std::vector<double> times;
+  for (int i = 0; i < iters + 2; ++i) {
+    MPI_Barrier(MPI_COMM_WORLD);
+    const double t0 = MPI_Wtime();
+    if (partner >= 0 && rank < half) {
+      MPI_Send(src, int(total), MPI_BYTE, partner, 0, MPI_COMM_WORLD);
+      MPI_Recv(dst, int(total), MPI_BYTE, partner, 0, MPI_COMM_WORLD, MPI_STATUS_IGNORE);
+    } else if (partner >= 0) {
+      MPI_Recv(dst, int(total), MPI_BYTE, partner, 0, MPI_COMM_WORLD, MPI_STATUS_IGNORE);
+      MPI_Send(src, int(total), MPI_BYTE, partner, 0, MPI_COMM_WORLD);
+    }
+    double el = MPI_Wtime() - t0;
+    MPI_Allreduce(MPI_IN_PLACE, &el, 1, MPI_DOUBLE, MPI_MAX, MPI_COMM_WORLD);
+    if (i >= 2) times.push_back(el);
+  }
+  long errors = 0;
+  if (check && partner >= 0) {
+    std::vector<unsigned char> g(static_cast<size_t>(total));
+    buf_copy(g.data(), dst, g.size());
+    for (size_t i = 0; i < g.size(); ++i) errors += g[i] != (unsigned char)((i * 7 + size_t(partner) * 31) & 0xFF);
+  }
+  MPI_Allreduce(MPI_IN_PLACE, &errors, 1, MPI_LONG, MPI_SUM, MPI_COMM_WORLD);
+  if (rank == 0 && json && jsonCap > 0) {
+    const double oneway = trimean(times) / 2;
+    std::snprintf(json, size_t(jsonCap),
+                  "{\"total\": %ld, \"pairs\": %d, \"iters\": %d, \"oneway_us\": %.2f, \"pair_GBps\": %.3f, "
+                  "\"aggregate_GBps\": %.3f, \"checked\": %s, \"errors\": %ld, \"method\": \"%s\", "
+                  "\"buffers\": \"%s\"}",
+                  total, half, iters, oneway * 1e6, double(total) / oneway / 1e9,
+                  double(half) * double(total) / oneway / 1e9, check ? "true" : "false", errors, method_name(),
+                  host_buffers() ? "host" : "device");
+  }
+  buf_free(src);
+  buf_free(dst);
+  return errors ? 3 : 0;
+}
+
 __global__ void a2av_fill(unsigned char *buf, const int64_t *displ, const int64_t *count, const int *dst, int n,
                           int src) {
   for (int d = 0; d < n; ++d)

@@ -21,6 +21,7 @@ iteration) run through MPI_Isend/MPI_Irecv/MPI_Wait on the same ranks
 the ranks are wired into one MPI job by tempi_amd.pmi.
 
 At N > 1 the line also carries "pingpong" (config 3, ranks 0 <-> 1),
+"pingpong_1d" (the contiguous ping-pong, all pairs),
 "alltoallv" (config 5, all ranks) and "nbr_alltoallv" (config 5's
 neighbourhood form), each with its xGMI fraction.
 
@@ -665,6 +666,8 @@ def apps_lib():
                                        ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
     L.tempi_bench_alltoallv.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_int, ctypes.c_int,
                                         ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
+    L.tempi_bench_pingpong_1d.argtypes = [ctypes.c_int, ctypes.c_long, ctypes.c_int, ctypes.c_int, ctypes.c_char_p,
+                                          ctypes.c_int]
     L.tempi_bench_nbr_alltoallv.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_int, ctypes.c_int,
                                             ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
     return L
@@ -690,6 +693,28 @@ def pingpong(args, world):
     return {"workload": ("config 3: MPI_Type_vector(total/bl, bl, 512, MPI_BYTE) MPI_Send/MPI_Recv ping-pong "
                          "rank 0 <-> 1, device buffers, one-way = trimean(round trip)/2"),
             "link_peak_GBps": XGMI_LINK_GBS, "points": out}
+
+
+def pingpong_1d(args, world):
+    """The reference's bench_mpi_pingpong_1d (contiguous
+    senders): MPI_BYTE count = 2 MiB and 16 MiB of device buffers, ranks r and
+    r + N/2 paired, all pairs at once, one-way = trimean(max over ranks of the
+    round trip) / 2; aggregate = the pairs' bytes in flight per one-way time."""
+    import ctypes
+
+    L = apps_lib()
+    out = []
+    for total in (1 << 21, 1 << 24):
+        buf = ctypes.create_string_buffer(1024)
+        rc = L.tempi_bench_pingpong_1d(args.pp_iters, total, 0, 0, buf, 1024)
+        if rc != 0:
+            raise RuntimeError(f"pingpong_1d failed rc={rc}")
+        if buf.value:
+            r = json.loads(buf.value.decode())
+            r["xgmi_frac"] = round(r["pair_GBps"] / XGMI_LINK_GBS, 4)
+            out.append(r)
+    return {"workload": ("bench_mpi_pingpong_1d: MPI_BYTE MPI_Send/MPI_Recv of device buffers, ranks r <-> r + N/2, "
+                         "all pairs at once"), "link_peak_GBps": XGMI_LINK_GBS, "points": out}
 
 
 def alltoallv(args, world):
@@ -1001,11 +1026,14 @@ def main():
             barrier(pg)
             pp = sec.run("pingpong", pingpong, args, world)
             barrier(pg)
+            p1 = sec.run("pingpong_1d", pingpong_1d, args, world)
+            barrier(pg)
             a2 = sec.run("alltoallv", alltoallv, args, world)
             barrier(pg)
             na = sec.run("nbr_alltoallv", nbr_alltoallv, args, world)
             if rank == 0:
                 rec["pingpong"] = pp
+                rec["pingpong_1d"] = p1
                 rec["alltoallv"] = a2
                 rec["nbr_alltoallv"] = na
         if rank == 0 and world == 1:

@@ -2,7 +2,8 @@
 plumbing -- dist_setup (gloo group + one MPI job wired over the torch
 ranks), barrier, the max / sum reductions of the timing -- and an MPI
 exchange through libtempi.so between the wired ranks, and the line's
-config-5 sections (alltoallv, nbr_alltoallv) on host buffers."""
+config-5 sections (alltoallv, nbr_alltoallv) and the contiguous ping-pong
+on host buffers."""
 import os
 import sys
 
@@ -33,6 +34,7 @@ os.environ["TEMPI_BENCH_HOST"] = "1"
 
 class Args:
     a2av_iters = 2
+    pp_iters = 2
 
 
 for fn in (bench.alltoallv, bench.nbr_alltoallv):
@@ -40,6 +42,9 @@ for fn in (bench.alltoallv, bench.nbr_alltoallv):
     if rank == 0:
         assert len(sec["points"]) == 3 and all(p["errors"] == 0 and p["buffers"] == "host" for p in sec["points"]), sec
         assert all(p["min_us"] > 0 and p["xgmi_frac"] is not None for p in sec["points"]), sec
+sec = bench.pingpong_1d(Args, world)
+if rank == 0:
+    assert [p["total"] for p in sec["points"]] == [1 << 21, 1 << 24] and all(p["oneway_us"] > 0 for p in sec["points"])
 mpi.Finalize()
 print(f"RESULT ok rank={rank}", flush=True)
 pg.destroy_process_group()

@@ -107,3 +107,15 @@ def test_mpi_pack_host(mode):
     recs = [json.loads(l) for l in out.splitlines() if l.startswith("{")]
     assert rc == 0 and len(recs) == 2 * 9 * 3, out[-3000:]
     assert all(r["errors"] == 0 and r["buffers"] == "host" and r["pack_MiBps"] > 0 for r in recs)
+
+
+@pytest.mark.parametrize("mode", list(MODES))
+@pytest.mark.parametrize("ranks", [2, 4, 3])
+def test_pingpong_1d_host(mode, ranks):
+    """the reference's bench_mpi_pingpong_1d (MPI_BYTE, all pairs r <-> r + N/2;
+    an odd rank out idles) on host buffers, every byte checked"""
+    rc, out = mpi_launch.run(ranks, [os.path.join(LIB, "pingpong_1d"), "2", "65536", str(1 << 21), "--check"],
+                             env=MODES[mode], timeout=120)
+    recs = [json.loads(l) for l in out.splitlines() if l.startswith("{")]
+    assert rc == 0 and len(recs) == 2 and all(r["errors"] == 0 and r["checked"] for r in recs), out[-3000:]
+    assert recs[0]["pairs"] == ranks // 2

@@ -192,6 +192,17 @@ def test_alltoallv_sparse_app(gpu, ranks, scale, density, env):
     assert rc == 0 and r["checked"] and r["errors"] == 0, out[-3000:]
 
 
+@pytest.mark.parametrize("ranks,env", [(2, {}), (4, {}), (2, {"TEMPI_CONTIGUOUS_STAGED": "1"}), (4, METHODS["XCOPY"]),
+                                       (2, {"TEMPI_DATATYPE_ONESHOT": "1"}), (8, {"TEMPI_STREAMS": "3"})])
+def test_pingpong_1d_app(gpu, ranks, env):
+    """the reference's bench_mpi_pingpong_1d on device buffers (MPI_BYTE,
+    all pairs at once), every byte checked, small and large"""
+    rc, out = mpi_launch.run(ranks, [os.path.join(LIB, "pingpong_1d"), "3", "1", "4096", str(1 << 21), str(1 << 24),
+                                     "--check"], env=env, timeout=240)
+    recs = [json.loads(l) for l in out.splitlines() if l.startswith("{")]
+    assert rc == 0 and len(recs) == 4 and all(r["errors"] == 0 and r["buffers"] == "device" for r in recs), out[-3000:]
+
+
 @pytest.mark.parametrize("ranks,scale,density,env", [
     (2, 100000, 1.0, {}), (4, 1000, 0.5, {}), (3, 10, 1.0, {"TEMPI_DATATYPE_ONESHOT": "1"}),
     (8, 1, 1.0, {}), (8, 100000, 0.5, {}), (8, 1000000, 0.125, {"TEMPI_STREAMS": "3"}),
