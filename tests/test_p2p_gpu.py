@@ -93,12 +93,17 @@ def test_halo_exchange_content(gpu, ranks, grid, env, extra):
     assert rc == 0 and r["checked"] and r["errors"] == 0, out[-3000:]
 
 
-def test_halo_exchange_512_full_check(gpu):
-    """config 4 at its full size, 1 rank, 8 quantities: every cell of every
-    quantity checked (on the GPU)"""
-    rc, out = mpi_launch.run(1, [os.path.join(LIB, "halo_exchange"), "2", "512", "--check"], timeout=240)
+@pytest.mark.parametrize("ranks,env", [(1, {}), (2, {}), (4, {"TEMPI_FAKE_FOREIGN_GPU": "1"}),
+                                       (8, {"TEMPI_STREAMS": "3"})])
+def test_halo_exchange_512_full_check(gpu, ranks, env):
+    """config 4 at its full size, 8 quantities: every cell of every quantity
+    checked (on the GPU), at 1 rank and in the 2-, 4- and 8-rank
+    decompositions (the full-size faces through IPC COPY, slabs and the
+    cross-GPU load path)"""
+    rc, out = mpi_launch.run(ranks, [os.path.join(LIB, "halo_exchange"), "2", "512", "--check"], env=env,
+                             timeout=240)
     r = _json_line(out)
-    assert rc == 0 and r["checked"] and r["errors"] == 0 and r["lcr"] == [512, 512, 512], out[-3000:]
+    assert rc == 0 and r["checked"] and r["errors"] == 0 and r["global"] == [512, 512, 512], out[-3000:]
 
 
 def test_halo_check_finds_a_planted_error(gpu):
