@@ -104,6 +104,10 @@ int main(int argc, char **argv) {
           if (host) {
             src = static_cast<char *>(std::malloc(span));
             dst = static_cast<char *>(std::malloc(size_t(psize)));
+            if (!src || !dst) {
+              std::fprintf(stderr, "mpi_pack: cannot allocate %zu host bytes\n", span);
+              MPI_Abort(MPI_COMM_WORLD, 1);
+            }
             for (size_t i = 0; i < span; ++i) src[i] = char(i & 0xFF);
           } else {
             HIPCHECK(hipMalloc(&src, span));
