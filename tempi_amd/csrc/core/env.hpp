@@ -21,6 +21,7 @@ struct Environment {
   bool noTempi = false;      // TEMPI_DISABLE
   bool noPack = false;       // TEMPI_NO_PACK
   bool noTypeCommit = false; // TEMPI_NO_TYPE_COMMIT
+  bool faultPack = false;    // TEMPI_FAULT_PACK (tests): every MPI_Pack / MPI_Unpack kernel launch "fails"
   DatatypeMethod datatype = DatatypeMethod::AUTO;
   ContiguousMethod contiguous = ContiguousMethod::NONE;
   AlltoallvMethod alltoallv = AlltoallvMethod::AUTO;

@@ -286,10 +286,14 @@ int pack(const void *inbuf, int incount, MPI_Datatype datatype, void *outbuf, in
   Slab *stage = dst.device_accessible ? nullptr : pinned_pool().get(size_t(std::max<int64_t>(bytes, 1)), src.device);
   if (!dst.device_accessible && !stage)
     return library_pack(inbuf, incount, datatype, outbuf, outsize, position, comm);
-  const int e = on_device(src.device, true, [&](void *s) {
+  const int e = env.faultPack ? 1 : on_device(src.device, true, [&](void *s) {
     return rec->packer->pack_async(stage ? stage->dev : dst.dptr, origin, incount, s);
   });
-  gpu::check(e, "MPI_Pack");
+  if (e != 0) { // (a GPU error falls back to the library instead of exiting)
+    LOG_WARN("MPI_Pack: the GPU pack failed (" << tempi_hip_error_string(e) << "); the library packs it");
+    if (stage) pinned_pool().put(stage);
+    return library_pack(inbuf, incount, datatype, outbuf, outsize, position, comm);
+  }
   if (stage) {
     counters.staged_packs++;
     std::memcpy(static_cast<char *>(outbuf) + *position, stage->host, size_t(bytes));
@@ -324,11 +328,14 @@ int unpack(const void *inbuf, int insize, int *position, void *outbuf, int outco
     counters.staged_unpacks++;
     std::memcpy(stage->host, static_cast<const char *>(inbuf) + *position, size_t(bytes));
   }
-  const int e = on_device(dst.device, false, [&](void *s) {
+  const int e = env.faultPack ? 1 : on_device(dst.device, false, [&](void *s) {
     return rec->packer->unpack_async(origin, stage ? stage->dev : src.dptr, outcount, s);
   });
-  gpu::check(e, "MPI_Unpack");
   if (stage) pinned_pool().put(stage);
+  if (e != 0) {
+    LOG_WARN("MPI_Unpack: the GPU unpack failed (" << tempi_hip_error_string(e) << "); the library unpacks it");
+    return library_unpack(inbuf, insize, position, outbuf, outcount, datatype, comm);
+  }
   *position += int(bytes);
   return MPI_SUCCESS;
 }

@@ -8,6 +8,7 @@ torch views and pack -> unpack round trips. Bit-exact everywhere.
 """
 import ctypes
 import hashlib
+import os
 import random
 
 import numpy as np
@@ -512,3 +513,32 @@ def test_pinned_slab_reuse_coarse_grained_contrast(gpu, capsys):
             print(f"\n[coarse-grained slab] stale bytes over 64 rounds: host read {bad[0]}, kernel read {bad[1]}")
     finally:
         hip.hipHostFree(host)
+
+
+def test_gpu_failure_falls_back_to_the_library(gpu):
+    """a failed GPU pack / unpack (TEMPI_FAULT_PACK makes every launch fail)
+    is redone by the library through host staging, bit-exact, instead of
+    exiting"""
+    import subprocess
+    import sys
+
+    code = (
+        "import numpy as np, torch, tempi_amd\n"
+        "mpi = tempi_amd.get_mpi(); mpi.Init()\n"
+        "t = mpi.Type_commit(mpi.Type_vector(1000, 12, 40, mpi.BYTE))\n"
+        "src = torch.randint(0, 256, (40000,), dtype=torch.uint8, device='cuda')\n"
+        "out = torch.zeros(12000, dtype=torch.uint8, device='cuda')\n"
+        "torch.cuda.synchronize()\n"
+        "assert mpi.Pack(src.data_ptr(), 1, t, out.data_ptr(), 12000, 0) == 12000\n"
+        "assert torch.equal(out.cpu(), src.view(1000, 40)[:, :12].reshape(-1).cpu())\n"
+        "dst = torch.full((40000,), 7, dtype=torch.uint8, device='cuda'); torch.cuda.synchronize()\n"
+        "assert mpi.Unpack(out.data_ptr(), 12000, 0, dst.data_ptr(), 1, t) == 12000\n"
+        "ref = torch.full((40000,), 7, dtype=torch.uint8); ref.view(1000, 40)[:, :12] = src.view(1000, 40)[:, :12].cpu()\n"
+        "assert torch.equal(dst.cpu(), ref)\n"
+        "c = mpi.counters(); assert c['lib_packs'] == 1 and c['lib_unpacks'] == 1 and c['packs'] == 0, c\n"
+        "mpi.Finalize(); print('RESULT ok')\n")
+    env = dict(os.environ, TEMPI_FAULT_PACK="1")
+    root = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, stdout=subprocess.PIPE,
+                       stderr=subprocess.STDOUT, text=True, timeout=200)
+    assert r.returncode == 0 and "RESULT ok" in r.stdout, r.stdout[-3000:]
