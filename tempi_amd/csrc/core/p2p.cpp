@@ -23,6 +23,7 @@
 #include <tuple>
 #include <unordered_map>
 #include <memory>
+#include <memory_resource>
 #include <unistd.h>
 #include <vector>
 
@@ -103,6 +104,16 @@ struct IpcCopyDesc {
   uint32_t pad;
 };
 static_assert(sizeof(IpcCopyDesc) == 232, "descriptor size");
+
+// Operation objects, the shared state of direct sends and the request table
+// are carved from one unsynchronised pool (the transport runs on the MPI
+// thread only), so a message's bookkeeping costs no malloc / free. The pool
+// is never destroyed: objects that outlive MPI_Finalize (statics torn down at
+// exit) still return their memory to it.
+std::pmr::unsynchronized_pool_resource &op_pool() {
+  static auto *pool = new std::pmr::unsynchronized_pool_resource();
+  return *pool;
+}
 
 struct Op;
 struct DirectShared {
@@ -567,6 +578,9 @@ std::deque<std::shared_ptr<GpuBatch>> batches; // launch order
 
 struct Op {
   virtual ~Op() {}
+  static void *operator new(size_t n) { return op_pool().allocate(n, alignof(std::max_align_t)); }
+  // (virtual destructor: `n` is the size of the object's dynamic type)
+  static void operator delete(void *p, size_t n) { op_pool().deallocate(p, n, alignof(std::max_align_t)); }
   virtual void gpu_done() {}                   // its GPU work completed
   virtual void lib_done(const MPI_Status &) {} // library request completed
   virtual void status(MPI_Status *s) const = 0;
@@ -917,7 +931,7 @@ struct IsendDirectOp : Op {
                 int dev, int64_t b, const tempi_hip_desc &flat)
       : rec(r->ref()), origin(o), count(c), dt(d), bytes(b) {
     device = dev;
-    sh = std::make_shared<DirectShared>();
+    sh = std::allocate_shared<DirectShared>(std::pmr::polymorphic_allocator<DirectShared>(&op_pool()));
     sh->device = dev;
     sh->sender = this;
     const uint64_t token = nextDirectToken++;
@@ -1891,7 +1905,7 @@ struct LocalCopyOp : Op {
 // (the reference uses a plain counter that can collide: SURVEY F9)
 constexpr uint32_t kHandleSpace = 1u << 26;
 uint32_t nextHandle = 1;
-std::unordered_map<uint32_t, std::unique_ptr<Op>> active;
+std::pmr::unordered_map<uint32_t, std::unique_ptr<Op>> active{&op_pool()};
 std::vector<uint32_t> detachedOps; // freed by the application, still running
 
 bool handlesWrapped = false; // once the counter has wrapped, skip handles still in use
