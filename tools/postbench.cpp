@@ -3,8 +3,9 @@
 // burst, then MPI_Waitall, as the halo's substep does, with small strided
 // device objects so the GPU work stays negligible. Prints per-call µs of each
 // phase (median over ROUNDS bursts).
-//   hipcc --offload-arch=gfx950 -O2 -std=c++17 -Iinclude -I/opt/conda/include -o tempi_amd/lib/postbench \
-//     tools/postbench.cpp -Ltempi_amd/lib -ltempi -L/opt/conda/lib -lmpi -Wl,-rpath,'$ORIGIN' \
+// build (one command):
+//   hipcc --offload-arch=gfx950 -O2 -std=c++17 -Iinclude -I/opt/conda/include -o tempi_amd/lib/postbench
+//     tools/postbench.cpp -Ltempi_amd/lib -ltempi -L/opt/conda/lib -lmpi -Wl,-rpath,'$ORIGIN'
 //     -Wl,-rpath,/opt/conda/lib
 //   mpiexec -n 1 tempi_amd/lib/postbench ROUNDS BURST
 #include <hip/hip_runtime.h>
