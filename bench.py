@@ -167,6 +167,58 @@ def cpu_baseline(mpi, pitch, block, seconds):
     }
 
 
+def config1(mpi, torch, dev, iters=300):
+    """BASELINE config 1 exactly: the reference's bench-mpi-pack object
+    MPI_Type_vector(1024, 512, 1024, MPI_BYTE) (512 KiB packed, extent
+    1 MiB), one MPI_Pack per call, trimean over `iters` calls: through the
+    host MPI on host buffers (the reference's CPU path, one pinned core) and
+    through libtempi on device buffers (synchronous GPU pack)."""
+    import numpy as np
+
+    t = mpi.Type_commit(mpi.Type_vector(1024, 512, 1024, mpi.BYTE))
+    n = 1023 * 1024 + 512
+    out = {}
+
+    def trimean(v):
+        v = sorted(v)
+        q = lambda p: v[int(round(p * (len(v) - 1)))]  # noqa: E731
+        return (q(0.25) + 2 * q(0.5) + q(0.75)) / 4
+
+    try:
+        src = (np.arange(n, dtype=np.int64) & 0xFF).astype(np.uint8)
+        packed = np.zeros(512 * 1024, dtype=np.uint8)
+        old = os.sched_getaffinity(0)
+        os.sched_setaffinity(0, {sorted(old)[0]})
+        try:
+            ts = []
+            for _ in range(iters + 5):
+                t0 = time.perf_counter()
+                mpi.Pack(src.ctypes.data, 1, t, packed.ctypes.data, packed.size, 0)
+                ts.append(time.perf_counter() - t0)
+        finally:
+            os.sched_setaffinity(0, old)
+        cpu = trimean(ts[5:])
+        dsrc = torch.from_numpy(src).to(dev)
+        dpk = torch.zeros(512 * 1024, dtype=torch.uint8, device=dev)
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(iters + 5):
+            t0 = time.perf_counter()
+            mpi.Pack(dsrc.data_ptr(), 1, t, dpk.data_ptr(), dpk.numel(), 0)
+            ts.append(time.perf_counter() - t0)
+        gpu = trimean(ts[5:])
+        ok = bool(np.array_equal(dpk.cpu().numpy(), packed))
+        out = {"workload": "BASELINE config 1: MPI_Pack of MPI_Type_vector(1024, 512, 1024, MPI_BYTE), 512 KiB packed, "
+                           "API time per call (trimean)",
+               "cpu_us": round(cpu * 1e6, 2), "cpu_payload_GBps": round(512 * 1024 / cpu / 1e9, 2),
+               "cpu": "host MPICH 3.3.2 on host buffers, one pinned core of " + _cpu_model(),
+               "gpu_us": round(gpu * 1e6, 2), "gpu_payload_GBps": round(512 * 1024 / gpu / 1e9, 2),
+               "speedup": round(cpu / gpu, 2), "gpu_matches_cpu": ok}
+    finally:
+        mpi.Type_free(t)
+    return out
+
+
 def _cpu_model():
     try:
         return [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
@@ -1067,6 +1119,7 @@ def main():
             if not args.no_cpu_baseline:
                 rec["cpu_baseline"] = sec.run("cpu_baseline", cpu_baseline, mpi, args.pitch, args.block,
                                               args.cpu_seconds)
+                rec["config1"] = sec.run("config1", config1, mpi, torch, dev)
                 rec["type_commit"] = sec.run("type_commit", type_commit_cost)
                 rec["mpi_pack"] = sec.run("mpi_pack", mpi_pack_bench)
                 lb = sec.run("cpu_baselines_configs_3_5", library_path_baselines, args)
