@@ -119,6 +119,29 @@ template <int W> struct Unroll {
   static constexpr int U = W == 16 ? TEMPI_UNROLL_16 : W == 8 ? TEMPI_UNROLL_WIDE : (W == 4 ? 2 : TEMPI_UNROLL_NARROW);
 };
 
+#ifndef TEMPI_XCD_MAP
+#define TEMPI_XCD_MAP 1
+#endif
+// Workgroup -> tile for scatters that write sectors in part. The dispatcher
+// deals workgroups round-robin over the 8 XCDs, so blocks b and b + 8 share
+// an XCD and its L2 (MI355X_MICROARCH.md, "Workgroup dispatch, XCD
+// placement"). With kXcdRange in the launch's flags, XCD slot b % 8 owns one
+// contiguous eighth of the tiles and walks it in order, so neighbouring tiles
+// meet in one L2: a strided-side line two tiles both write in part (a row or
+// an unaligned plane crossing the tile edge) is merged there instead of
+// reaching DRAM as two masked writes from two XCDs, each a read-modify-write
+// (1 B : 2 B 3D unpack +10 %, 128 B : 144 +26 %, 24-B rows +8 %). Streams of
+// whole lines keep the dealt order: eight streams an eighth of the object
+// apart cost the headline unpack 6 % (profiles/r02/xcd_group_ab_s12.jsonl),
+// as do shorter runs per XCD (16 tiles: -14 %). Placement is only a speed
+// hint: the map is a bijection of [0, n) whatever the hardware does.
+constexpr uint32_t kXcdRange = 1u << 31; // internal flag bit (never a TEMPI_HIP_ITEM_*)
+__device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t n, uint32_t flags) {
+  if (!(flags & kXcdRange)) return b;
+  const uint32_t x = b & 7, q = n >> 3, r = n & 7;
+  return x * q + (x < r ? x : r) + (b >> 3);
+}
+
 constexpr int kBlock = TEMPI_BLOCK;
 // the interleaved tiles index whole 64-lane waves (tile + wave * 64, j * 64 + lane over kBlock entries)
 static_assert(kBlock % 64 == 0 && kBlock >= 64 && kBlock <= 1024, "packer workgroups are whole 64-lane waves");
@@ -420,12 +443,12 @@ __device__ __forceinline__ void unpack_body(const KArgs<ND> &a, uint32_t blk, ui
 
 template <int W, int ND>
 __global__ __launch_bounds__(kBlock) void pack_kernel(const KArgs<ND> a) {
-  pack_body<W, ND>(a, blockIdx.x, gridDim.x);
+  pack_body<W, ND>(a, xcd_tile(blockIdx.x, gridDim.x, a.flags), gridDim.x);
 }
 
 template <int W, int ND>
 __global__ __launch_bounds__(kBlock) void unpack_kernel(const KArgs<ND> a) {
-  unpack_body<W, ND>(a, blockIdx.x, gridDim.x);
+  unpack_body<W, ND>(a, xcd_tile(blockIdx.x, gridDim.x, a.flags), gridDim.x);
 }
 
 // ------------------------------------------- wave-interleaved scatter (unpack)
@@ -537,10 +560,10 @@ __device__ __forceinline__ void pack_il_tile(const KArgs<ND> &a, uint32_t tileId
 }
 
 template <int W, int ND> __global__ __launch_bounds__(kBlock) void pack_il_kernel(const KArgs<ND> a) {
-  pack_il_tile<W, ND>(a, blockIdx.x, gridDim.x);
+  pack_il_tile<W, ND>(a, xcd_tile(blockIdx.x, gridDim.x, a.flags), gridDim.x);
 }
 template <int W, int ND> __global__ __launch_bounds__(kBlock) void unpack_il_kernel(const KArgs<ND> a) {
-  unpack_il_tile<W, ND>(a, blockIdx.x, gridDim.x);
+  unpack_il_tile<W, ND>(a, xcd_tile(blockIdx.x, gridDim.x, a.flags), gridDim.x);
 }
 
 // ------------------------------------------------- dense-window gather (pack)
@@ -570,7 +593,7 @@ static_assert(kDenseLds <= 64 * 1024, "dense window too large for LDS");
 template <int ND>
 __global__ __launch_bounds__(kBlock) void pack_dense_kernel(const KArgs<ND> a) {
   __shared__ uint4 win[kDenseLds / 16];
-  const uint32_t blk = blockIdx.x;
+  const uint32_t blk = xcd_tile(blockIdx.x, gridDim.x, a.flags);
   const uint32_t c0 = blk * kBlock; // first chunk of this tile
   const uint32_t c1 = min(c0 + uint32_t(kBlock), a.nchunks);
   // packed bytes of the tile (W = 1: words are bytes)
@@ -656,23 +679,27 @@ template <int ND> __device__ __forceinline__ uint32_t find_item(const BatchArgs<
 
 template <int W, int ND>
 __global__ __launch_bounds__(kBlock) void pack_batch_kernel(const BatchArgs<ND> b) {
-  const uint32_t i = find_item<ND>(b, blockIdx.x);
-  pack_body<W, ND>(b.item[i], blockIdx.x - b.first[i], b.first[i + 1] - b.first[i]);
+  const uint32_t i = find_item<ND>(b, blockIdx.x), n = b.first[i + 1] - b.first[i];
+  const uint32_t blk = xcd_tile(blockIdx.x - b.first[i], n, b.item[i].flags); // (within the item: balanced)
+  pack_body<W, ND>(b.item[i], blk, n);
 }
 
 template <int W, int ND> __global__ __launch_bounds__(kBlock) void pack_il_batch_kernel(const BatchArgs<ND> b) {
-  const uint32_t i = find_item<ND>(b, blockIdx.x);
-  pack_il_tile<W, ND>(b.item[i], blockIdx.x - b.first[i], b.first[i + 1] - b.first[i]);
+  const uint32_t i = find_item<ND>(b, blockIdx.x), n = b.first[i + 1] - b.first[i];
+  const uint32_t blk = xcd_tile(blockIdx.x - b.first[i], n, b.item[i].flags); // (within the item: balanced)
+  pack_il_tile<W, ND>(b.item[i], blk, n);
 }
 template <int W, int ND> __global__ __launch_bounds__(kBlock) void unpack_il_batch_kernel(const BatchArgs<ND> b) {
-  const uint32_t i = find_item<ND>(b, blockIdx.x);
-  unpack_il_tile<W, ND>(b.item[i], blockIdx.x - b.first[i], b.first[i + 1] - b.first[i]);
+  const uint32_t i = find_item<ND>(b, blockIdx.x), n = b.first[i + 1] - b.first[i];
+  const uint32_t blk = xcd_tile(blockIdx.x - b.first[i], n, b.item[i].flags); // (within the item: balanced)
+  unpack_il_tile<W, ND>(b.item[i], blk, n);
 }
 
 template <int W, int ND>
 __global__ __launch_bounds__(kBlock) void unpack_batch_kernel(const BatchArgs<ND> b) {
-  const uint32_t i = find_item<ND>(b, blockIdx.x);
-  unpack_body<W, ND>(b.item[i], blockIdx.x - b.first[i], b.first[i + 1] - b.first[i]);
+  const uint32_t i = find_item<ND>(b, blockIdx.x), n = b.first[i + 1] - b.first[i];
+  const uint32_t blk = xcd_tile(blockIdx.x - b.first[i], n, b.item[i].flags); // (within the item: balanced)
+  unpack_body<W, ND>(b.item[i], blk, n);
 }
 
 // ---------------------------------------------------------------- host side
@@ -738,6 +765,25 @@ int word_width(uintptr_t packed, uintptr_t first, const Norm &n) {
   return int(g & (~g + 1));
 }
 
+// kXcdRange when a scatter onto this strided side writes sectors in part
+// (block, a stride or the base not a multiple of the 32-byte sector) AND
+// neighbouring rows share lines (gap < 128 B), with rows below kXcdMaxBlock:
+// isolated rows (the halo's x faces) have nothing to merge, and long rows
+// are whole-line streams, which the dealt order serves better.
+// (TEMPI_NO_XCD_MAP set: never, for A/B runs)
+#ifndef TEMPI_XCD_MAX_BLOCK
+#define TEMPI_XCD_MAX_BLOCK 1024
+#endif
+uint32_t xcd_flag(const char *first, const Norm &n) {
+  static const bool off = std::getenv("TEMPI_NO_XCD_MAP") != nullptr;
+  if (!TEMPI_XCD_MAP || off || n.nd == 0 || n.block >= TEMPI_XCD_MAX_BLOCK) return 0;
+  const int64_t inner = n.str[n.nd - 1];
+  if (inner < n.block || inner - n.block >= 128) return 0;
+  uint64_t g = reinterpret_cast<uintptr_t>(first) | uint64_t(n.block);
+  for (int k = 0; k < n.nd; ++k) g |= uint64_t(n.str[k] < 0 ? -n.str[k] : n.str[k]);
+  return (g & 31) ? kXcdRange : 0;
+}
+
 // TEMPI_HIP_ITEM_* of the object make_args is describing (set around each
 // item by run_batch; 0 for the single-object entry points)
 thread_local uint32_t gItemFlags = 0;
@@ -777,6 +823,7 @@ int launch_nd(bool pack, char *packed, char *first, const Norm &n, hipStream_t s
   uint32_t blocks;
   make_args<W, ND>(packed, first, n, &a, &blocks);
   if (blocks == 0) return 0;
+  if (!pack) a.flags |= xcd_flag(first, n);
   if (pack)
     hipLaunchKernelGGL((pack_kernel<W, ND>), dim3(blocks), dim3(kBlock), 0, s, a);
   else
@@ -819,6 +866,7 @@ template <int W, int ND> int launch_batch_nd(bool pack, const std::vector<Job> &
     gItemFlags = j.flags;
     make_args<W, ND>(j.packed, j.first, j.n, &a, &blocks);
     gItemFlags = 0;
+    if (!pack) a.flags |= xcd_flag(j.first, j.n);
     if (il) blocks = (a.nchunks + kBlock - 1) / kBlock;
     if (!blocks) continue;
     if (uint64_t(total) + blocks >= (uint64_t(1) << 31))
@@ -899,6 +947,7 @@ template <int W, int ND> int launch_il_nd(bool pack, char *packed, char *first, 
   make_args<W, ND>(packed, first, n, &a, &blocks);
   blocks = (a.nchunks + kBlock - 1) / kBlock; // one tile per workgroup, no grid-stride
   if (blocks == 0) return 0;
+  if (!pack) a.flags |= xcd_flag(first, n);
   if (pack)
     hipLaunchKernelGGL((pack_il_kernel<W, ND>), dim3(blocks), dim3(kBlock), 0, s, a);
   else
@@ -989,7 +1038,7 @@ int run_batch(bool pack, const tempi_hip_batch_item *items, int n, hipStream_t s
     Job j;
     j.packed = static_cast<char *>(items[i].packed);
     j.first = static_cast<char *>(items[i].first);
-    j.flags = pack ? 0u : items[i].flags; // (gathers read the strided side only)
+    j.flags = pack ? 0u : items[i].flags & TEMPI_HIP_ITEM_REMOTE; // (gathers read the strided side only)
     if (!normalise(&items[i].desc, &j.n)) return int(hipErrorInvalidValue);
     const int64_t bytes = norm_bytes(j.n);
     if (bytes == 0) continue;
@@ -1158,7 +1207,7 @@ template <int W> __device__ __forceinline__ void copy_body(const CArgs &a, uint3
 }
 
 template <int W> __global__ __launch_bounds__(kCopyBlock) void copy_kernel(const CArgs a) {
-  copy_body<W>(a, blockIdx.x, gridDim.x);
+  copy_body<W>(a, xcd_tile(blockIdx.x, gridDim.x, a.flags), gridDim.x);
 }
 
 constexpr int kCopyMax = int((kBatchBytes - 8) / (sizeof(CArgs) + 4));
@@ -1177,7 +1226,8 @@ template <int W> __global__ __launch_bounds__(kCopyBlock) void copy_batch_kernel
     else
       hi = mid;
   }
-  copy_body<W>(b.item[lo], blockIdx.x - b.first[lo], b.first[lo + 1] - b.first[lo]);
+  const uint32_t n = b.first[lo + 1] - b.first[lo];
+  copy_body<W>(b.item[lo], xcd_tile(blockIdx.x - b.first[lo], n, b.item[lo].flags), n); // (within the item)
 }
 
 bool make_side(char *first, const Norm &n, int W, CSide *c) {
@@ -1222,7 +1272,7 @@ bool plan_copy(void *dst, const void *src, const tempi_hip_desc *dd, const tempi
   if (!make_side(const_cast<char *>(static_cast<const char *>(src)), ns, w, &job->a.s)) return false;
   if (!make_side(static_cast<char *>(dst), nd, w, &job->a.d)) return false;
   job->a.nwords = uint32_t(bytes / w);
-  job->a.flags = 0;
+  job->a.flags = xcd_flag(static_cast<char *>(dst), nd);
   job->a.s2 = job->a.d2 = nullptr;
   job->w = w;
   return true;
@@ -1315,7 +1365,7 @@ int tempi_hip_copy_batch(const tempi_hip_copy_item *items, int n, void *stream) 
     CopyJob j;
     if (!plan_copy(items[i].dst_first, items[i].src_first, &items[i].dst, &items[i].src, &j))
       return int(hipErrorInvalidValue);
-    j.a.flags = items[i].flags;
+    j.a.flags |= items[i].flags & TEMPI_HIP_ITEM_REMOTE;
     if (j.a.nwords == 0) continue;
     const int wi = j.w == 1 ? 0 : j.w == 2 ? 1 : j.w == 4 ? 2 : j.w == 8 ? 3 : 4;
     groups[wi].push_back(j);

@@ -201,6 +201,36 @@ def test_full_size_2d_exact(mpi, gpu, rows, pitch, bl):
         mpi.Type_free(t)
 
 
+@pytest.mark.parametrize("z,y,pitch,bl", [(4000, 4000, 8, 4),       # 3D, planes 24 B off line alignment
+                                          (3001, 3000, 18, 2),       # 3D, 2-byte words
+                                          (1, 1000003, 144, 128)])   # 2D, 16-byte gap
+def test_xcd_mapped_scatter_exact(mpi, gpu, z, y, pitch, bl):
+    """Shapes whose unpack takes the XCD-range tile map (partial sectors,
+    neighbouring rows sharing lines), with tile counts that are not multiples
+    of 8: pack against torch views, then unpack into zeros restores exactly
+    the type map and leaves every gap byte untouched."""
+    torch = _torch()
+    t = mpi.Type_commit(mpi.Type_create_subarray([z, y + 3, pitch], [z, y, bl], [0, 0, 0], mpi.ORDER_C, mpi.BYTE))
+    try:
+        n = z * (y + 3) * pitch
+        size = z * y * bl
+        src = torch.randint(0, 256, (n,), dtype=torch.uint8, device=gpu)
+        out = torch.empty(size, dtype=torch.uint8, device=gpu)
+        torch.cuda.synchronize()
+        assert mpi.Pack(src.data_ptr(), 1, t, out.data_ptr(), size, 0) == size
+        view = src.view(z, y + 3, pitch)[:, :y, :bl]
+        assert torch.equal(out.view(z, y, bl), view)
+        dst = torch.zeros(n, dtype=torch.uint8, device=gpu)
+        torch.cuda.synchronize()
+        mpi.Unpack(out.data_ptr(), size, 0, dst.data_ptr(), 1, t)
+        torch.cuda.synchronize()
+        d3 = dst.view(z, y + 3, pitch)
+        assert torch.equal(d3[:, :y, :bl], view)
+        assert int(d3[:, :y, bl:].count_nonzero()) == 0 and int(d3[:, y:, :].count_nonzero()) == 0
+    finally:
+        mpi.Type_free(t)
+
+
 def test_halo_faces_512(mpi, gpu):
     """Halo-exchange face/edge/corner types of the 512^3 bench (radius 3,
     8-byte quantities, pitch 4608), against torch 3-D views."""
