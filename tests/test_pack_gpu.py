@@ -572,3 +572,21 @@ def test_gpu_failure_falls_back_to_the_library(gpu):
     r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, stdout=subprocess.PIPE,
                        stderr=subprocess.STDOUT, text=True, timeout=200)
     assert r.returncode == 0 and "RESULT ok" in r.stdout, r.stdout[-3000:]
+
+
+def test_pack_bench_app(gpu):
+    """the reference's bench_pack and bench_pack_kernels at the C-ABI (apps/
+    pack_bench.cpp): every point's first pack and unpack checked byte for
+    byte, packed side in pinned host memory (oneshot) and in device memory"""
+    import json
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([os.path.join(root, "tempi_amd", "lib", "pack_bench"), "3", "--max-target", str(1 << 20)],
+                       capture_output=True, text=True, timeout=200)
+    recs = [json.loads(l) for l in p.stdout.splitlines() if l.startswith("{")]
+    assert p.returncode == 0, p.stderr[-2000:]
+    # bench_pack: 2 destinations x 8 targets <= 1 MiB x 12 rows x {pack, unpack};
+    # bench_pack_kernels: 2 destinations x 2 targets x 2 counts x (7 + 15) rows
+    assert sum(r["bench"] == "bench_pack" for r in recs) == 2 * 8 * 12 * 2
+    assert sum(r["bench"] == "bench_pack_kernels" for r in recs) == 2 * 2 * 2 * 22
+    assert all(r["errors"] == 0 and r["us"] > 0 for r in recs)
