@@ -375,3 +375,45 @@ def test_copy_paired_halo_faces(mpi, gpu, l, nq, remote):
     for k in range(nq + 1):
         got = devs[k].cpu().numpy().reshape(zsz, ysz, pitch)
         assert np.array_equal(got, exps[k]), f"quantity {k}"
+
+
+def _desc2d(rows, block, stride):
+    d = HipDesc()
+    d.block, d.ndims = block, 1
+    d.counts[0], d.strides[0] = rows, stride
+    return d
+
+
+def test_copy_xcd_mapped_large(gpu):
+    """copies whose destination takes the XCD-range tile map (rows sharing
+    lines, sectors written in part), two such items of one word width in one
+    launch with tile counts that are not multiples of 8, next to an unmapped
+    item: every destination byte against torch views, gaps untouched"""
+    import torch
+
+    H = _hip()
+    g = torch.Generator().manual_seed(7)
+    specs = [  # rows, block, src stride, dst stride, dst offset
+        (2000003, 8, 24, 40, 8),
+        (1000001, 8, 16, 48, 24),
+        (3000001, 1, 2, 3, 1),
+        (262147, 512, 1024, 1024, 0),
+    ]
+    cases = []
+    for rows, bl, ss, ds, off in specs:
+        src = torch.randint(0, 256, (rows * ss,), dtype=torch.uint8, generator=g).to(gpu)
+        dst = torch.zeros(rows * ds + off, dtype=torch.uint8, device=gpu)
+        it = CopyItem()
+        it.src_first, it.dst_first = src.data_ptr(), dst.data_ptr() + off
+        it.src, it.dst = _desc2d(rows, bl, ss), _desc2d(rows, bl, ds)
+        it.flags = 0
+        assert H.tempi_hip_copy_supported(it.dst_first, it.src_first, ctypes.byref(it.dst), ctypes.byref(it.src))
+        cases.append((it, src, dst, rows, bl, ss, ds, off))
+    items = (CopyItem * len(cases))(*[c[0] for c in cases])
+    torch.cuda.synchronize()
+    assert H.tempi_hip_copy_batch(items, len(cases), None) == 0
+    torch.cuda.synchronize()
+    for it, src, dst, rows, bl, ss, ds, off in cases:
+        got = dst[off:].view(rows, ds)
+        assert torch.equal(got[:, :bl], src.view(rows, ss)[:, :bl]), (rows, bl, ss, ds)
+        assert int(got[:, bl:].count_nonzero()) == 0 and int(dst[:off].count_nonzero()) == 0

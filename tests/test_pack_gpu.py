@@ -590,3 +590,34 @@ def test_pack_bench_app(gpu):
     assert sum(r["bench"] == "bench_pack" for r in recs) == 2 * 8 * 12 * 2
     assert sum(r["bench"] == "bench_pack_kernels" for r in recs) == 2 * 2 * 2 * 22
     assert all(r["errors"] == 0 and r["us"] > 0 for r in recs)
+
+
+def test_unpack_batch_xcd_mapped_large(gpu):
+    """tempi_hip_unpack_batch with large items whose scatter takes the
+    XCD-range tile map (per item within one launch: 4-byte rows at strides 8
+    and 12, 2-byte rows at 18) beside an unmapped one (512-byte rows): every
+    row against torch views, the gaps untouched"""
+    import tempi_amd
+    import torch
+
+    H = ctypes.CDLL(tempi_amd.LIBTEMPI_HIP)
+    H.tempi_hip_unpack_batch.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+    g = torch.Generator().manual_seed(11)
+    specs = [(4000003, 4, 8), (2500001, 4, 12), (3000017, 2, 18), (131075, 512, 1024)]  # rows, block, stride
+    items = (HipItem * len(specs))()
+    bufs = []
+    for k, (rows, bl, st) in enumerate(specs):
+        packed = torch.randint(0, 256, (rows * bl,), dtype=torch.uint8, generator=g).to(gpu)
+        dst = torch.zeros(rows * st, dtype=torch.uint8, device=gpu)
+        it = items[k]
+        it.packed, it.first, it.flags = packed.data_ptr(), dst.data_ptr(), 0
+        it.desc.block, it.desc.ndims = bl, 1
+        it.desc.counts[0], it.desc.strides[0] = rows, st
+        bufs.append((packed, dst, rows, bl, st))
+    torch.cuda.synchronize()
+    assert H.tempi_hip_unpack_batch(items, len(specs), None) == 0
+    torch.cuda.synchronize()
+    for packed, dst, rows, bl, st in bufs:
+        got = dst.view(rows, st)
+        assert torch.equal(got[:, :bl], packed.view(rows, bl)), (rows, bl, st)
+        assert int(got[:, bl:].count_nonzero()) == 0
