@@ -2,7 +2,9 @@
 // hipStreamSynchronize, against the host spinning on a flag in pinned memory
 // written (system-scope release) by a one-lane kernel queued behind it, or by
 // the last workgroup of the kernel itself (each workgroup fencing at system
-// scope first). profiles/r02/completion_flag_bench_s11.jsonl; DESIGN §6.
+// scope first); and HIP's own completion polled instead of waited for:
+// hipStreamQuery / hipEventQuery in a spin loop, hipEventSynchronize.
+// profiles/r02/completion_flag_bench_s11.jsonl, _s13.jsonl; DESIGN §6.
 //   hipcc --offload-arch=gfx950 -O2 -o flagbench tools/flagbench.hip
 #include <hip/hip_runtime.h>
 #include <chrono>
@@ -29,9 +31,10 @@ int main() {
   unsigned *flag; hipHostMalloc(&flag, 64, hipHostMallocMapped | hipHostMallocCoherent); *flag = 0;
   unsigned *dflag; hipHostGetDevicePointer((void**)&dflag, flag, 0);
   hipStream_t s; hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+  hipEvent_t ev; hipEventCreateWithFlags(&ev, hipEventDisableTiming);
   for (int blocks : {1, 64, 512}) {
     int n = blocks * 256;
-    std::vector<double> a, b, c;
+    std::vector<double> a, b, c, q, eq, es;
     unsigned ticket = 1;
     for (int it = 0; it < 300; ++it) {
       double t0 = now_us(); hipLaunchKernelGGL(work, dim3(blocks), dim3(256), 0, s, d, n); hipStreamSynchronize(s); a.push_back(now_us() - t0);
@@ -42,9 +45,17 @@ int main() {
       ++ticket; t0 = now_us(); hipLaunchKernelGGL(work_flag, dim3(blocks), dim3(256), 0, s, d, n, cnt, dflag, ticket);
       while (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != ticket) __builtin_ia32_pause(); c.push_back(now_us() - t0);
       hipStreamSynchronize(s);
+      t0 = now_us(); hipLaunchKernelGGL(work, dim3(blocks), dim3(256), 0, s, d, n);
+      while (hipStreamQuery(s) == hipErrorNotReady) __builtin_ia32_pause(); q.push_back(now_us() - t0);
+      t0 = now_us(); hipLaunchKernelGGL(work, dim3(blocks), dim3(256), 0, s, d, n); hipEventRecord(ev, s);
+      while (hipEventQuery(ev) == hipErrorNotReady) __builtin_ia32_pause(); eq.push_back(now_us() - t0);
+      t0 = now_us(); hipLaunchKernelGGL(work, dim3(blocks), dim3(256), 0, s, d, n); hipEventRecord(ev, s);
+      hipEventSynchronize(ev); es.push_back(now_us() - t0);
     }
     auto med = [](std::vector<double> v) { std::sort(v.begin(), v.end()); return v[v.size() / 2]; };
-    printf("{\"blocks\": %d, \"sync_us\": %.2f, \"signal_kernel_flag_us\": %.2f, \"last_wg_flag_us\": %.2f}\n", blocks, med(a), med(b), med(c));
+    printf("{\"blocks\": %d, \"sync_us\": %.2f, \"signal_kernel_flag_us\": %.2f, \"last_wg_flag_us\": %.2f, "
+           "\"stream_query_poll_us\": %.2f, \"event_query_poll_us\": %.2f, \"event_sync_us\": %.2f}\n",
+           blocks, med(a), med(b), med(c), med(q), med(eq), med(es));
   }
   return 0;
 }
