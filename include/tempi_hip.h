@@ -133,6 +133,9 @@ int tempi_hip_stream_create(void **stream); /* non-blocking stream */
 int tempi_hip_stream_create_priority(void **stream, int high);
 int tempi_hip_stream_destroy(void *stream);
 int tempi_hip_stream_synchronize(void *stream);
+/* wait for `stream` by a ticket a kernel queued behind its work stores to
+   pinned memory (faster than tempi_hip_stream_synchronize for small work) */
+int tempi_hip_stream_signal_wait(void *stream);
 int tempi_hip_stream_wait_event(void *stream, void *event);
 /* flags: bit 0 = timing enabled, bit 1 = blocking sync, bit 2 = interprocess */
 int tempi_hip_event_create(void **event, int flags);

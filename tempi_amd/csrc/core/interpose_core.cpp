@@ -118,7 +118,10 @@ template <typename F> int on_device(int device, bool pack, F &&fn) {
   if (ev0) tempi_hip_event_record(ev0, s);
   int e = fn(s);
   if (ev1) tempi_hip_event_record(ev1, s);
-  if (e == 0) e = tempi_hip_stream_synchronize(s);
+  if (e == 0) e = env.streamSync ? tempi_hip_stream_synchronize(s) : tempi_hip_stream_signal_wait(s);
+  // (the ticket can be seen before HIP has noted ev1 complete, which it
+  // already is on the GPU: wait for it before reading the elapsed time)
+  if (e == 0 && ev1 && !env.streamSync) e = tempi_hip_event_synchronize(ev1);
   if (e == 0 && ev0 && ev1) {
     float ms = 0;
     if (tempi_hip_event_elapsed_ms(&ms, ev0, ev1) == 0) {

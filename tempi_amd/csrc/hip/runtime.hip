@@ -15,6 +15,8 @@
 
 #include <algorithm>
 #include <cstring>
+#include <mutex>
+#include <unordered_map>
 
 #define RET(expr) return int(expr)
 
@@ -108,6 +110,66 @@ int tempi_hip_stream_destroy(void *stream) { RET(hipStreamDestroy(static_cast<hi
 int tempi_hip_stream_synchronize(void *stream) {
   RET(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
 }
+
+namespace {
+// one-lane kernel queued behind a synchronous call's work: its system-scope
+// release store of `ticket` to pinned host memory is what the host waits for
+__global__ void signal_ticket(uint32_t *flag, uint32_t ticket) {
+  if (threadIdx.x == 0) __hip_atomic_store(flag, ticket, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+struct Ticket {
+  uint32_t *host = nullptr, *dev = nullptr;
+  uint32_t next = 0;
+};
+// one flag per stream: tickets reach a stream in increasing order (issued
+// under the mutex), so a flag >= mine means the work before my ticket is done
+std::unordered_map<void *, Ticket> tickets;
+std::mutex ticketMutex;
+} // namespace
+
+// Wait for everything queued on `stream` the quick way: a kernel enqueued
+// behind it stores a ticket to a pinned flag, and the host spins on the flag.
+// Same-stream kernels run in order and each one's writes are visible
+// device-wide before the next starts (HIP's stream semantics), so the ticket
+// becomes visible only after the work before it is complete and written back
+// from L2; host memory written by that work is coherent (fine-grained). On
+// MI355X the host sees it 5 µs sooner than hipStreamSynchronize's completion
+// (7.6-8.9 vs 12.9-14.3 µs for a small kernel: tools/flagbench.hip,
+// profiles/r02/completion_flag_bench_s13.jsonl). The stream is queried every
+// ~20 µs of spinning, so a faulted stream (which never runs the signal) or a
+// stream that completed anyway ends the wait; any failure falls back to
+// hipStreamSynchronize.
+int tempi_hip_stream_signal_wait(void *stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  std::unique_lock<std::mutex> lock(ticketMutex);
+  Ticket &t = tickets[stream];
+  if (!t.host) {
+    void *h = nullptr, *d = nullptr;
+    if (hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable) != hipSuccess ||
+        hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+      lock.unlock();
+      RET(hipStreamSynchronize(s));
+    }
+    t.host = static_cast<uint32_t *>(h);
+    t.dev = static_cast<uint32_t *>(d);
+    __atomic_store_n(t.host, 0u, __ATOMIC_RELEASE);
+  }
+  const uint32_t ticket = ++t.next;
+  hipLaunchKernelGGL(signal_ticket, dim3(1), dim3(64), 0, s, t.dev, ticket);
+  const bool launched = hipGetLastError() == hipSuccess;
+  lock.unlock();
+  if (!launched) RET(hipStreamSynchronize(s));
+  for (uint32_t spins = 1;; ++spins) {
+    if (int32_t(__atomic_load_n(t.host, __ATOMIC_ACQUIRE) - ticket) >= 0) return 0;
+    if ((spins & 1023) == 0) { // ~20 µs of pause loops
+      const hipError_t e = hipStreamQuery(s);
+      if (e == hipSuccess) return 0;
+      if (e != hipErrorNotReady) return int(e);
+    }
+    __builtin_ia32_pause();
+  }
+}
+
 int tempi_hip_stream_wait_event(void *stream, void *event) {
   RET(hipStreamWaitEvent(static_cast<hipStream_t>(stream), static_cast<hipEvent_t>(event), 0));
 }
