@@ -136,6 +136,9 @@ int tempi_hip_stream_synchronize(void *stream);
 /* wait for `stream` by a ticket a kernel queued behind its work stores to
    pinned memory (faster than tempi_hip_stream_synchronize for small work) */
 int tempi_hip_stream_signal_wait(void *stream);
+/* queue a ticket behind the work on `stream`: once `*flag` (pinned host
+   memory) reaches `*ticket` (as a wrapping uint32 compare), that work is done */
+int tempi_hip_stream_ticket(void *stream, const uint32_t **flag, uint32_t *ticket);
 int tempi_hip_stream_wait_event(void *stream, void *event);
 /* flags: bit 0 = timing enabled, bit 1 = blocking sync, bit 2 = interprocess */
 int tempi_hip_event_create(void **event, int flags);

@@ -139,28 +139,32 @@ std::mutex ticketMutex;
 // ~20 µs of spinning, so a faulted stream (which never runs the signal) or a
 // stream that completed anyway ends the wait; any failure falls back to
 // hipStreamSynchronize.
-int tempi_hip_stream_signal_wait(void *stream) {
+int tempi_hip_stream_ticket(void *stream, const uint32_t **flag, uint32_t *ticket) {
   hipStream_t s = static_cast<hipStream_t>(stream);
-  std::unique_lock<std::mutex> lock(ticketMutex);
+  std::lock_guard<std::mutex> lock(ticketMutex);
   Ticket &t = tickets[stream];
   if (!t.host) {
     void *h = nullptr, *d = nullptr;
-    if (hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable) != hipSuccess ||
-        hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
-      lock.unlock();
-      RET(hipStreamSynchronize(s));
-    }
+    hipError_t e = hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable);
+    if (e == hipSuccess) e = hipHostGetDevicePointer(&d, h, 0);
+    if (e != hipSuccess) return int(e);
     t.host = static_cast<uint32_t *>(h);
     t.dev = static_cast<uint32_t *>(d);
     __atomic_store_n(t.host, 0u, __ATOMIC_RELEASE);
   }
-  const uint32_t ticket = ++t.next;
-  hipLaunchKernelGGL(signal_ticket, dim3(1), dim3(64), 0, s, t.dev, ticket);
-  const bool launched = hipGetLastError() == hipSuccess;
-  lock.unlock();
-  if (!launched) RET(hipStreamSynchronize(s));
+  *ticket = ++t.next;
+  hipLaunchKernelGGL(signal_ticket, dim3(1), dim3(64), 0, s, t.dev, *ticket);
+  *flag = t.host;
+  RET(hipGetLastError());
+}
+
+int tempi_hip_stream_signal_wait(void *stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const uint32_t *flag = nullptr;
+  uint32_t ticket = 0;
+  if (tempi_hip_stream_ticket(stream, &flag, &ticket) != 0) RET(hipStreamSynchronize(s));
   for (uint32_t spins = 1;; ++spins) {
-    if (int32_t(__atomic_load_n(t.host, __ATOMIC_ACQUIRE) - ticket) >= 0) return 0;
+    if (int32_t(__atomic_load_n(flag, __ATOMIC_ACQUIRE) - ticket) >= 0) return 0;
     if ((spins & 1023) == 0) { // ~20 µs of pause loops
       const hipError_t e = hipStreamQuery(s);
       if (e == hipSuccess) return 0;
