@@ -123,14 +123,14 @@ def make_2d(mpi, rows, pitch, block):
     return mpi.Type_commit(t)
 
 
-def cpu_baseline(mpi, pitch, block, seconds):
+def cpu_baseline(mpi, rows, pitch, block, seconds):
     """Host MPI (MPICH) MPI_Pack + MPI_Unpack on host buffers, one pinned core:
-    the reference's CPU path (/root/reference/src/pack.cpp:51-54)."""
+    the reference's CPU path (/root/reference/src/pack.cpp:51-54), on the
+    headline's own object (the same subarray, the same 1 GiB packed size)."""
     import numpy as np
 
-    rows = max(1, (128 * 1024 * 1024) // block)  # 128 MiB packed sample
     t = make_2d(mpi, rows, pitch, block)
-    src = (np.arange(rows * pitch, dtype=np.int64) & 0xFF).astype(np.uint8)
+    src = np.resize(np.arange(256, dtype=np.uint8), rows * pitch)  # byte i = i & 0xFF
     packed = np.zeros(rows * block, dtype=np.uint8)
     dst = np.zeros(rows * pitch, dtype=np.uint8)
     old = os.sched_getaffinity(0)
@@ -160,10 +160,8 @@ def cpu_baseline(mpi, pitch, block, seconds):
         "unit": "GB/s",
         "cores": 1,
         "kind": "reference",
-        "sample": (f"host MPICH 3.3.2 MPI_Pack+MPI_Unpack (the reference's CPU path for host buffers, "
-                   f"src/pack.cpp:51-54) of subarray({rows}x{pitch} -> {rows}x{block} B), "
-                   f"{rows * block >> 20} MiB packed, {n} pack+unpack pairs in {el:.1f} s, pinned to 1 core "
-                   f"of {model}"),
+        "sample": (f"MPICH 3.3.2 MPI_Pack+MPI_Unpack of the headline object ({rows * block >> 20} MiB packed) on "
+                   f"host buffers, {n} pairs in {el:.1f} s, 1 pinned core of {model}"),
     }
 
 
@@ -489,9 +487,8 @@ def headline(args, mpi, torch, rank, world, pg, dev):
         "dtype": "u8",
         "data": "synthetic (byte i = i & 0xFF)",
         "config": {
-            "workload": (f"config 2 point: MPI_Pack+MPI_Unpack of MPI_Type_create_subarray({{{rows},{pitch}}}, "
-                         f"{{{rows},{block}}}, {{0,0}}, MPI_BYTE), count 1 (bench-mpi-pack's vector(1024,512,1024) "
-                         f"scaled to {payload >> 20} MiB packed), device buffers, per rank"),
+            "workload": (f"config 2 point: MPI_Pack+MPI_Unpack, subarray({{{rows},{pitch}}}->{{{rows},{block}}}) "
+                         f"MPI_BYTE, {payload >> 20} MiB packed, device buffers, per rank"),
             "packed_bytes": payload,
             "extent_bytes": rows * pitch,
             "block_bytes": block,
@@ -568,6 +565,8 @@ def halo(args, mpi, world, grid=None):
     out = {
         "workload": (f"{g}^3 grid, 8 quantities x 8 B, radius 3, 26 neighbours, periodic, 3 substeps/iter, "
                      f"{world} rank(s) {r['dims']} (recursive bisection), MPI_Isend/Irecv/Wait of subarray types"),
+        "grid": g,
+        "dims": r["dims"],
         "us_per_iter": r["us_per_iter"],
         "us_min": r["us_min"],
         "bytes_per_iter_all_ranks": r["total_bytes_per_iter"],
@@ -980,6 +979,182 @@ def sweep_geomean(args, mpi, torch, dev):
                         "MPI_Unpack from HIP events on TEMPI's stream"}
 
 
+SHARED_GPU_NOTE = ("ranks share one GPU: no byte crosses xGMI, so xGMI fractions are null (the algorithmic bytes "
+                   "never left HBM)")
+
+
+def null_shared_gpu_fractions(rec):
+    """With ranks sharing one GPU an 'xGMI' fraction is physically
+    meaningless (it exceeds the link peak): null every one of them"""
+    for name in ("halo", "halo_weak"):
+        r = (rec.get(name) or {}).get("roofline")
+        if r and r.get("bound") == "xgmi":
+            for k in ("frac", "aggregate_frac", "busiest_link_GBps", "aggregate_xgmi_GBps"):
+                if k in r:
+                    r[k] = None
+            r["note"] = SHARED_GPU_NOTE
+    for name in ("pingpong", "pingpong_1d", "alltoallv", "nbr_alltoallv"):
+        p = rec.get(name)
+        if isinstance(p, dict) and "points" in p:
+            for q in p["points"]:
+                q["xgmi_frac"] = None
+            p["note"] = SHARED_GPU_NOTE
+
+
+LINE_LIMIT = 3800  # bytes of the final stdout line; the driver keeps ~8 KB of stdout tail
+
+
+def _sig(x, digits=4):
+    """a float rounded to `digits` significant digits (ints and None pass)"""
+    if isinstance(x, float) and x != 0 and math.isfinite(x):
+        return float(f"{x:.{digits}g}")
+    return x
+
+
+def _err(sec):
+    return {"error": str(sec["error"])[:160]} if isinstance(sec, dict) and "error" in sec else None
+
+
+def _compact_sections(rec, shared_gpu):
+    """{name: compact summary} of every section after the headline; each
+    one's full record stays in the detail file"""
+    out = {}
+    s = rec.get("sweep_geomean")
+    if s:
+        out["sweep"] = _err(s) or {
+            "points": s["points"], "pack_GBps": s["pack_GBps"], "unpack_GBps": s["unpack_GBps"],
+            "pack_frac": s["pack_frac"], "unpack_frac": s["unpack_frac"], "pack_ge_0.7": s["pack_ge_0.7"],
+            "unpack_ge_0.7": s["unpack_ge_0.7"], "pack_frac_touched": s["pack_frac_touched"],
+            "unpack_frac_touched": s["unpack_frac_touched"],
+            "worst_touched": [f"{w['shape'].split()[0]} {w['block']}:{w['stride']} p{w['pack_frac_touched']:.3f} "
+                              f"u{w['unpack_frac_touched']:.3f}" for w in s.get("worst_touched", [])]}
+    for name in ("halo", "halo_weak"):
+        h = rec.get(name)
+        if not h:
+            continue
+        e = _err(h)
+        if e:
+            out[name] = e
+            continue
+        r = h.get("roofline") or {}
+        c = {"grid": h.get("grid"), "dims": h.get("dims"), "us_per_iter": h["us_per_iter"], "us_min": h["us_min"],
+             "bound": r.get("bound"), "frac": r.get("frac")}
+        if r.get("bound") == "hbm":
+            c.update({"alg_bytes_per_iter": r.get("algorithmic_bytes_per_iter"),
+                      "traffic_per_iter": r.get("traffic_per_iter"), "frac_touched": r.get("frac_touched")})
+        else:
+            c.update({"busiest_link_GBps": r.get("busiest_link_GBps"), "aggregate_frac": r.get("aggregate_frac"),
+                      "remote_bytes_per_iter": r.get("remote_bytes_per_iter")})
+            x = h.get("xgmi_counters") or {}
+            c["xgmi_counter_bytes_per_iter"] = x.get("per_unit_bytes") if x.get("available") else None
+        if h.get("rank0_phase_us"):
+            c["rank0_phase_us"] = h["rank0_phase_us"]
+        cb = h.get("cpu_baseline")
+        if cb and "value" in cb:
+            c["cpu_us_per_iter"] = _sig(cb["value"])
+        out[name] = c
+    if rec.get("config1"):
+        c = rec["config1"]
+        out["config1"] = _err(c) or {k: c.get(k) for k in ("cpu_us", "gpu_us", "speedup", "gpu_matches_cpu")}
+    if rec.get("type_commit"):
+        c = rec["type_commit"]
+        out["type_commit"] = _err(c) or {"tempi_us": c["tempi"]["commit_us_median"],
+                                         "library_us": c["library"]["commit_us_median"]}
+    if rec.get("mpi_pack"):
+        c = rec["mpi_pack"]
+        out["mpi_pack"] = _err(c) or {"errors": c["errors"], "points": len(c.get("points", [])),
+                                      "pack_speedup_geomean_by_target": c["pack_speedup_geomean_by_target"]}
+    lb = rec.get("cpu_baselines_configs_3_5")
+    if lb:
+        c = _err(lb) or {}
+        if not c:
+            if "halo" in lb:
+                c["halo_us_per_iter"] = _sig(lb["halo"]["value"])
+            if "pingpong" in lb:
+                c["pingpong_oneway_us"] = [[p["total"], p["block"], _sig(p["oneway_us"])] for p in lb["pingpong"]["points"]]
+            if "alltoallv" in lb:
+                c["alltoallv_us"] = _sig(lb["alltoallv"]["value"])
+            c["cores"] = "halo 1, pingpong 2, alltoallv 8 (MPICH, TEMPI_DISABLE=1, host buffers)"
+        out["cpu_baselines_configs_3_5"] = c
+    for name, cols in (("pingpong", ("total", "block", "oneway_us", "GBps", "xgmi_frac")),
+                       ("pingpong_1d", ("total", "pairs", "oneway_us", "aggregate_GBps", "xgmi_frac")),
+                       ("alltoallv", ("scale", "density", "min_us", "max_pairwise_bytes", "xgmi_frac")),
+                       ("nbr_alltoallv", ("scale", "density", "min_us", "max_pairwise_bytes", "xgmi_frac"))):
+        p = rec.get(name)
+        if not p:
+            continue
+        out[name] = _err(p) or {"cols": list(cols), "points": [[_sig(q.get(k)) for k in cols] for q in p["points"]],
+                                "errors": sum(q.get("errors", 0) for q in p["points"])}
+    if rec.get("perf_model"):
+        pm = rec["perf_model"]
+        out["perf_model"] = _err(pm) or {"measured_here": pm.get("measured_here"),
+                                         "auto_model": os.path.basename(str(pm.get("auto_model", ""))) or None}
+    return out
+
+
+# sections dropped, in this order, if the line is still over LINE_LIMIT
+_DROP_ORDER = ("mpi_pack", "type_commit", "perf_model", "cpu_baselines_configs_3_5", "halo_weak", "nbr_alltoallv",
+               "pingpong_1d", "alltoallv", "pingpong", "config1", "sweep")
+
+
+def compact_line(rec, shared_gpu=False, detail=None, limit=LINE_LIMIT):
+    """The driver's one JSON line: the contract's keys, the headline's
+    roofline and cpu_baseline, and a bounded summary of every other section
+    (the full record goes to the detail file). Guaranteed <= limit bytes."""
+    line = {k: rec[k] for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                                "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config") if k in rec}
+    ro = rec.get("roofline")
+    if ro:
+        line["roofline"] = {k: ro[k] for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "traffic_read",
+                                               "traffic_write", "kernel", "algorithmic_bytes_per_launch",
+                                               "avg_launch_ms", "pack_avg_ms", "unpack_avg_ms", "timed_launches",
+                                               "achievable_peak", "frac_achievable", "d2d_copy_GBps",
+                                               "traffic_error") if k in ro}
+    cb = rec.get("cpu_baseline")
+    if cb:
+        line["cpu_baseline"] = _err(cb) or {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample") if k in cb}
+    if rec.get("incomplete"):
+        line["incomplete"] = rec["incomplete"]
+    line["shared_gpu"] = bool(shared_gpu)
+    secs = _compact_sections(rec, shared_gpu)
+    line.update(secs)
+    if detail:
+        line["detail"] = detail
+    dropped = []
+    for name in _DROP_ORDER:
+        if len(json.dumps(line)) <= limit:
+            break
+        if name in line:
+            del line[name]
+            dropped.append(name)
+    if dropped:
+        line["dropped"] = dropped
+    while len(json.dumps(line)) > limit:  # last resort: never hand the driver an unparseable tail
+        extra = [k for k in line if k not in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                                              "higher_is_better", "scaling", "vs_baseline", "dtype", "data",
+                                              "config", "roofline", "cpu_baseline")]
+        if not extra:
+            line["config"] = {"workload": str(line.get("config", {}).get("workload", ""))[:120]}
+            line.get("cpu_baseline", {}).pop("sample", None)
+            break
+        del line[extra[-1]]
+    return line
+
+
+def write_detail(rec, world):
+    """the full record, next to the line (gpurun_out/ is merged back from
+    the GPU box); returns the path relative to the repo, or None"""
+    d = os.path.join(ROOT, "gpurun_out")
+    path = os.path.join(d, f"bench_detail_n{world}.json")
+    try:
+        os.makedirs(d, exist_ok=True)
+        with open(path, "w") as f:
+            json.dump(rec, f, indent=1)
+        return os.path.relpath(path, ROOT)
+    except OSError:
+        return None
+
+
 class Sections:
     """The sections after the headline (sweep, halo, configs 3 and 5,
     traffic, CPU baselines) are evidence beside the metric, not the metric:
@@ -988,10 +1163,11 @@ class Sections:
     this pool never ran, e.g. the first cross-GPU IPC) ends the run with the
     line so far, its "incomplete" field naming the section."""
 
-    def __init__(self, rec, rank, deadline):
+    def __init__(self, rec, rank, deadline, world=1, shared_gpu=False):
         import threading
 
         self.rec, self.rank, self.current = rec, rank, "start"
+        self.world, self.shared_gpu = world, shared_gpu
         self.timer = threading.Timer(deadline, self._expire, args=(deadline,))
         self.timer.daemon = True
         self.timer.start()
@@ -1001,11 +1177,13 @@ class Sections:
             line = dict(self.rec)
             line["incomplete"] = {"section": self.current, "deadline_s": deadline}
             try:
-                print(json.dumps(line), flush=True)
+                if self.shared_gpu:
+                    null_shared_gpu_fractions(line)
+                print(json.dumps(compact_line(line, self.shared_gpu, write_detail(line, self.world))), flush=True)
             except Exception as e:  # a section was mutating the record
-                print(json.dumps({k: line[k] for k in ("metric", "value", "unit", "n_gpus")} |
+                print(json.dumps({k: line[k] for k in ("metric", "value", "unit", "n_gpus") if k in line} |
                                  {"incomplete": {"section": self.current, "deadline_s": deadline,
-                                                 "print_error": str(e)}}), flush=True)
+                                                 "print_error": str(e)[:200]}}), flush=True)
         sys.stdout.flush()
         os._exit(0)
 
@@ -1043,11 +1221,11 @@ def main():
         if args.inner:
             return
         torch.cuda.empty_cache()
-        sec = Sections(rec, rank, args.extras_deadline)
+        shared_gpu = world > max(torch.cuda.device_count(), 1)
+        sec = Sections(rec, rank, args.extras_deadline, world, shared_gpu)
         if world == 1 and not args.no_sweep_geomean:
             rec["sweep_geomean"] = sec.run("sweep_geomean", sweep_geomean, args, mpi, torch, dev)
             torch.cuda.empty_cache()
-        shared_gpu = world > max(torch.cuda.device_count(), 1)
         if world > 1:
             pm = sec.run("perf_model", node_perf_model, args, mpi, pg, rank, world, shared_gpu)
             if rank == 0:
@@ -1117,7 +1295,7 @@ def main():
                                                 "copy kernels of halo_exchange 3 GRID, per iteration, FETCH_SIZE x2; "
                                                 "bound at the 6.3 TB/s achievable rate")
             if not args.no_cpu_baseline:
-                rec["cpu_baseline"] = sec.run("cpu_baseline", cpu_baseline, mpi, args.pitch, args.block,
+                rec["cpu_baseline"] = sec.run("cpu_baseline", cpu_baseline, mpi, args.rows, args.pitch, args.block,
                                               args.cpu_seconds)
                 rec["config1"] = sec.run("config1", config1, mpi, torch, dev)
                 rec["type_commit"] = sec.run("type_commit", type_commit_cost)
@@ -1129,7 +1307,9 @@ def main():
                         rec["halo"]["cpu_baseline"] = lb["halo"]
         sec.done()
         if rank == 0:
-            print(json.dumps(rec), flush=True)
+            if shared_gpu:
+                null_shared_gpu_fractions(rec)
+            print(json.dumps(compact_line(rec, shared_gpu, write_detail(rec, world))), flush=True)
     finally:
         mpi.Finalize()
         if pg is not None:

@@ -48,6 +48,8 @@ typedef struct tempi_counters_t {
   uint64_t self_matched; /* messages to this same process matched inside TEMPI (no library message) */
   uint64_t staged_packs;   /* MPI_Pack of a GPU object into pageable host memory (through a pinned slab) */
   uint64_t staged_unpacks; /* MPI_Unpack into a GPU object from pageable host memory */
+  uint64_t ticket_waits;   /* synchronous MPI_Pack / MPI_Unpack completed by a ticket the GPU stored */
+  uint64_t sync_waits;     /* ... completed by hipStreamSynchronize (kernel wrote application host memory) */
 } tempi_counters_t;
 void tempi_get_counters(tempi_counters_t *out);
 void tempi_reset_counters(void);

@@ -93,6 +93,18 @@ int tempi_hip_copy_supported(void *dst_first, const void *src_first,
                              const tempi_hip_desc *dst, const tempi_hip_desc *src);
 int tempi_hip_copy_batch(const tempi_hip_copy_item *items, int n, void *stream);
 
+/* synchronous forms (MPI_Pack / MPI_Unpack, /root/reference/src/internal/
+   packer_2d.cu:101-118): the same work plus a completion ticket. Once `*flag`
+   (pinned, coherent host memory) reaches `*ticket` (wrapping uint32 compare,
+   tempi_hip_ticket_wait), the work is complete and its writes to device
+   memory are visible device-wide. A launch of at most TEMPI_FOLD_MAX_BLOCKS
+   workgroups stores the ticket from its own last workgroup; larger work gets
+   the ticket kernel queued behind it. */
+int tempi_hip_pack_ticket(void *packed, const void *first, const tempi_hip_desc *d, void *stream,
+                          const uint32_t **flag, uint32_t *ticket);
+int tempi_hip_unpack_ticket(void *first, const void *packed, const tempi_hip_desc *d, void *stream,
+                            const uint32_t **flag, uint32_t *ticket);
+
 /* number of packed bytes a descriptor describes */
 int64_t tempi_hip_desc_bytes(const tempi_hip_desc *d);
 /* the word width (1,2,4,8,16) the kernels will use for these pointers */
@@ -139,6 +151,11 @@ int tempi_hip_stream_signal_wait(void *stream);
 /* queue a ticket behind the work on `stream`: once `*flag` (pinned host
    memory) reaches `*ticket` (as a wrapping uint32 compare), that work is done */
 int tempi_hip_stream_ticket(void *stream, const uint32_t **flag, uint32_t *ticket);
+/* spin until *flag reaches ticket; the stream is queried every ~20 us, so a
+   faulted stream returns its error */
+int tempi_hip_ticket_wait(void *stream, const uint32_t *flag, uint32_t ticket);
+/* tickets issued so far: stored by the work kernel itself / by a ticket kernel */
+void tempi_hip_ticket_stats(uint64_t *folded, uint64_t *queued);
 int tempi_hip_stream_wait_event(void *stream, void *event);
 /* flags: bit 0 = timing enabled, bit 1 = blocking sync, bit 2 = interprocess */
 int tempi_hip_event_create(void **event, int flags);

@@ -16,6 +16,10 @@ struct Counters {
   uint64_t lib_packs = 0, lib_unpacks = 0; // handed to the library
   // GPU packs into / unpacks from pageable host memory through a pinned slab
   uint64_t staged_packs = 0, staged_unpacks = 0;
+  // synchronous MPI_Pack / MPI_Unpack completed by a ticket (device memory or
+  // TEMPI's coherent slab written) or by hipStreamSynchronize (the
+  // application's pinned host memory written, or TEMPI_STREAM_SYNC)
+  uint64_t ticket_waits = 0, sync_waits = 0;
   uint64_t sends = 0, recvs = 0, isends = 0, irecvs = 0;
   uint64_t send_device = 0, send_oneshot = 0, send_staged = 0, send_ipc = 0;
   uint64_t lib_sends = 0, lib_recvs = 0;

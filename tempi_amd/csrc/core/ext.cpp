@@ -73,6 +73,8 @@ TEMPI_EXPORT void tempi_get_counters(tempi_counters_t *o) {
   o->self_matched = c.self_matched;
   o->staged_packs = c.staged_packs;
   o->staged_unpacks = c.staged_unpacks;
+  o->ticket_waits = c.ticket_waits;
+  o->sync_waits = c.sync_waits;
 }
 
 TEMPI_EXPORT void tempi_reset_counters(void) { counters = Counters(); }

@@ -172,14 +172,19 @@ MPI_Comm private_comm(MPI_Comm comm) {
 }
 
 void coll_init() { private_comm(MPI_COMM_WORLD); }
+void neighbourhood_finalize(); // interpose_neighbor.cpp
 void coll_finalize() {
+  neighbourhood_finalize();
   for (auto &kv : privateComms) next.MPI_Comm_free(&kv.second);
   privateComms.clear();
 }
 
 // the application frees `comm`: drop what TEMPI cached for the handle
+void neighbourhood_forget(MPI_Comm comm); // interpose_neighbor.cpp
+
 void comm_release(MPI_Comm comm) {
   p2p::self_forget(comm);
+  neighbourhood_forget(comm);
   topology::uncache(comm);
   auto it = privateComms.find(comm);
   if (it != privateComms.end()) {

@@ -106,9 +106,14 @@ namespace {
 
 // run fn on the stream of `device`, with that device current, and wait for
 // it (MPI_Pack / MPI_Unpack are synchronous: /root/reference/src/internal/
-// packer_2d.cu:101-118). With kernel profiling on, HIP events bracket the
+// packer_2d.cu:101-118). fn(stream, done) launches; `done` is non-null when
+// the call may complete by ticket (Packer::Completion), i.e. when everything
+// the work writes is device memory or a TEMPI coherent slab: kernel stores
+// to the application's pinned host memory (possibly coarse-grained) are made
+// host-visible by hipStreamSynchronize's system-scope release, not by a
+// ticket. With kernel profiling on, HIP events bracket the
 // launches on that stream and their elapsed time is accumulated.
-template <typename F> int on_device(int device, bool pack, F &&fn) {
+template <typename F> int on_device(int device, bool pack, bool ticketOk, F &&fn) {
   int cur = 0;
   tempi_hip_get_device(&cur);
   if (cur != device) tempi_hip_set_device(device);
@@ -116,12 +121,22 @@ template <typename F> int on_device(int device, bool pack, F &&fn) {
   void *ev0 = nullptr, *ev1 = nullptr;
   if (kernelProfiling) gpu::profiling_events(device, &ev0, &ev1);
   if (ev0) tempi_hip_event_record(ev0, s);
-  int e = fn(s);
+  const bool byTicket = ticketOk && !env.streamSync;
+  Packer::Completion done;
+  int e = fn(s, byTicket ? &done : nullptr);
   if (ev1) tempi_hip_event_record(ev1, s);
-  if (e == 0) e = env.streamSync ? tempi_hip_stream_synchronize(s) : tempi_hip_stream_signal_wait(s);
+  if (e == 0) {
+    if (!byTicket) {
+      counters.sync_waits++;
+      e = tempi_hip_stream_synchronize(s);
+    } else if (done.flag) {
+      counters.ticket_waits++;
+      e = tempi_hip_ticket_wait(s, done.flag, done.ticket);
+    }
+  }
   // (the ticket can be seen before HIP has noted ev1 complete, which it
   // already is on the GPU: wait for it before reading the elapsed time)
-  if (e == 0 && ev1 && !env.streamSync) e = tempi_hip_event_synchronize(ev1);
+  if (e == 0 && ev1 && byTicket) e = tempi_hip_event_synchronize(ev1);
   if (e == 0 && ev0 && ev1) {
     float ms = 0;
     if (tempi_hip_event_elapsed_ms(&ms, ev0, ev1) == 0) {
@@ -289,8 +304,13 @@ int pack(const void *inbuf, int incount, MPI_Datatype datatype, void *outbuf, in
   Slab *stage = dst.device_accessible ? nullptr : pinned_pool().get(size_t(std::max<int64_t>(bytes, 1)), src.device);
   if (!dst.device_accessible && !stage)
     return library_pack(inbuf, incount, datatype, outbuf, outsize, position, comm);
-  const int e = env.faultPack ? 1 : on_device(src.device, true, [&](void *s) {
-    return rec->packer->pack_async(stage ? stage->dev : dst.dptr, origin, incount, s);
+  // the kernel writes device memory or TEMPI's coherent slab: the ticket may
+  // complete the call; into the application's pinned host memory it may not
+  const bool ticketOk = stage != nullptr || !dst.host_accessible;
+  const int e = env.faultPack ? 1 : on_device(src.device, true, ticketOk, [&](void *s, Packer::Completion *done) {
+    void *out = stage ? stage->dev : dst.dptr;
+    return done ? rec->packer->pack_ticket(out, origin, incount, s, done)
+                : rec->packer->pack_async(out, origin, incount, s);
   });
   if (e != 0) { // (a GPU error falls back to the library instead of exiting)
     LOG_WARN("MPI_Pack: the GPU pack failed (" << tempi_hip_error_string(e) << "); the library packs it");
@@ -331,8 +351,12 @@ int unpack(const void *inbuf, int insize, int *position, void *outbuf, int outco
     counters.staged_unpacks++;
     std::memcpy(stage->host, static_cast<const char *>(inbuf) + *position, size_t(bytes));
   }
-  const int e = env.faultPack ? 1 : on_device(dst.device, false, [&](void *s) {
-    return rec->packer->unpack_async(origin, stage ? stage->dev : src.dptr, outcount, s);
+  // the kernel writes the strided object: by ticket only when it is device memory
+  const int e = env.faultPack ? 1 : on_device(dst.device, false, !dst.host_accessible,
+                                              [&](void *s, Packer::Completion *done) {
+    const void *in = stage ? stage->dev : src.dptr;
+    return done ? rec->packer->unpack_ticket(origin, in, outcount, s, done)
+                : rec->packer->unpack_async(origin, in, outcount, s);
   });
   if (stage) pinned_pool().put(stage);
   if (e != 0) {

@@ -44,6 +44,9 @@
 
 #include "tempi_mpi.h"
 
+#include <cstring>
+#include <list>
+#include <unordered_map>
 #include <vector>
 
 #define TEMPI_EXPORT extern "C" __attribute__((visibility("default")))
@@ -57,7 +60,7 @@ namespace {
 
 // incoming / outgoing neighbours in MPI's canonical order; false when the
 // communicator has no topology (the library then raises the error)
-bool neighbours(MPI_Comm comm, std::vector<int> &in, std::vector<int> &out) {
+bool query_neighbours(MPI_Comm comm, std::vector<int> &in, std::vector<int> &out) {
   int topo = MPI_UNDEFINED;
   MPI_Topo_test(comm, &topo);
   in.clear();
@@ -96,41 +99,125 @@ bool neighbours(MPI_Comm comm, std::vector<int> &in, std::vector<int> &out) {
   return false;
 }
 
-// one Isend / Irecv per edge through the interposed entry points (device
-// blocks -> TEMPI transport, host blocks -> library sends and
-// descriptor-aware receives), receives first
-int isir(const void *sendbuf, const int *scounts, const MPI_Aint *sdispls, const MPI_Datatype *stypes,
-         void *recvbuf, const int *rcounts, const MPI_Aint *rdispls, const MPI_Datatype *rtypes, MPI_Comm comm,
-         const std::vector<int> &in, const std::vector<int> &out) {
-  const MPI_Comm c = private_comm(comm);
-  const int tag = 0x4E41; // "NA": alone on the private communicator
-  std::vector<MPI_Request> reqs;
-  reqs.reserve(in.size() + out.size());
+// a topology's neighbour lists never change: kept per communicator until it
+// is freed (neighbourhood_forget)
+struct Neighbours {
+  std::vector<int> in, out;
+};
+std::unordered_map<MPI_Comm, Neighbours> neighbourCache;
+
+const Neighbours *neighbours(MPI_Comm comm) {
+  auto it = neighbourCache.find(comm);
+  if (it != neighbourCache.end()) return &it->second;
+  Neighbours n;
+  if (!query_neighbours(comm, n.in, n.out)) return nullptr;
+  return &neighbourCache.emplace(comm, std::move(n)).first->second;
+}
+
+// The per-call plan of a neighbourhood collective: which edges are self
+// edges carried as strided -> strided copies, and those copies (descriptors
+// resolved, pointers classified). The halo's MPI_Neighbor_alltoallw repeats
+// the same few calls every iteration, and re-planning 26 self edges cost
+// ~5 us of each ~63 us call. A plan is reused
+// while the call is the same -- communicator, buffers, every count,
+// displacement and type handle -- no type record was added or dropped since
+// (type_generation), and both buffers still classify to the same device.
+struct Plan {
+  MPI_Comm comm;
+  const void *sbuf;
+  void *rbuf;
+  std::vector<int> scounts, rcounts;
+  std::vector<MPI_Aint> sdispls, rdispls;
+  std::vector<MPI_Datatype> stypes, rtypes;
+  uint64_t typeGen = 0;
+  int sdev = -2, rdev = -2;
+  MPI_Comm priv = MPI_COMM_NULL;
+  int me = 0;
+  std::vector<char> doneIn, doneOut;
+  p2p::LocalCopies copies;
+};
+constexpr size_t kMaxPlans = 64;
+std::list<Plan> plans; // most recently used first
+
+int base_device(const void *p) {
+  const gpu::Ptr q = gpu::classify(p);
+  return q.device_accessible ? q.device : -1;
+}
+
+template <typename T> bool same(const std::vector<T> &v, const T *a, size_t n) {
+  return v.size() == n && (n == 0 || std::memcmp(v.data(), a, n * sizeof(T)) == 0);
+}
+
+const Plan &plan_for(const void *sendbuf, const int *scounts, const MPI_Aint *sdispls, const MPI_Datatype *stypes,
+                     void *recvbuf, const int *rcounts, const MPI_Aint *rdispls, const MPI_Datatype *rtypes,
+                     MPI_Comm comm, const Neighbours &nb) {
+  const size_t ni = nb.in.size(), no = nb.out.size();
+  const uint64_t gen = type_generation();
+  const int sdev = base_device(sendbuf), rdev = base_device(recvbuf);
+  for (auto it = plans.begin(); it != plans.end(); ++it) {
+    const Plan &p = *it;
+    if (p.comm == comm && p.sbuf == sendbuf && p.rbuf == recvbuf && p.typeGen == gen && p.sdev == sdev &&
+        p.rdev == rdev && same(p.scounts, scounts, no) && same(p.sdispls, sdispls, no) &&
+        same(p.stypes, stypes, no) && same(p.rcounts, rcounts, ni) && same(p.rdispls, rdispls, ni) &&
+        same(p.rtypes, rtypes, ni)) {
+      plans.splice(plans.begin(), plans, it);
+      return plans.front();
+    }
+  }
+  Plan p;
+  p.comm = comm;
+  p.sbuf = sendbuf;
+  p.rbuf = recvbuf;
+  p.scounts.assign(scounts, scounts + no);
+  p.sdispls.assign(sdispls, sdispls + no);
+  p.stypes.assign(stypes, stypes + no);
+  p.rcounts.assign(rcounts, rcounts + ni);
+  p.rdispls.assign(rdispls, rdispls + ni);
+  p.rtypes.assign(rtypes, rtypes + ni);
+  p.typeGen = gen;
+  p.sdev = sdev;
+  p.rdev = rdev;
+  p.priv = private_comm(comm);
+  next.MPI_Comm_rank(p.priv, &p.me);
   // Self edges: the k-th edge to this rank meets the k-th edge from it (edge
   // order, as message matching would pair them). Each such pair whose blocks
-  // are device objects is one strided -> strided copy queued right here, with
-  // no library messages; the rest go as messages, still in edge order.
-  std::vector<char> doneIn(in.size(), 0), doneOut(out.size(), 0);
-  int me = 0;
-  next.MPI_Comm_rank(c, &me);
-  {
-    std::vector<size_t> selfIn, selfOut;
-    for (size_t j = 0; j < in.size(); ++j)
-      if (in[j] == me) selfIn.push_back(j);
-    for (size_t i = 0; i < out.size(); ++i)
-      if (out[i] == me) selfOut.push_back(i);
-    bool any = false;
-    for (size_t k = 0; k < selfIn.size() && k < selfOut.size(); ++k) {
-      const size_t i = selfOut[k], j = selfIn[k];
-      MPI_Request r;
-      if (p2p::local_copy(static_cast<const char *>(sendbuf) + sdispls[i], scounts[i], stypes[i],
-                          static_cast<char *>(recvbuf) + rdispls[j], rcounts[j], rtypes[j], &r)) {
-        reqs.push_back(r);
-        doneOut[i] = doneIn[j] = 1;
-        any = true;
-      }
-    }
-    if (any) p2p::start_queued(); // the copies run while the messages are posted
+  // are device objects is one strided -> strided copy, with no library
+  // messages; the rest go as messages, still in edge order.
+  p.doneIn.assign(ni, 0);
+  p.doneOut.assign(no, 0);
+  std::vector<size_t> selfIn, selfOut;
+  for (size_t j = 0; j < ni; ++j)
+    if (nb.in[j] == p.me) selfIn.push_back(j);
+  for (size_t i = 0; i < no; ++i)
+    if (nb.out[i] == p.me) selfOut.push_back(i);
+  for (size_t k = 0; k < selfIn.size() && k < selfOut.size(); ++k) {
+    const size_t i = selfOut[k], j = selfIn[k];
+    if (p2p::plan_local_copy(static_cast<const char *>(sendbuf) + sdispls[i], scounts[i], stypes[i],
+                             static_cast<char *>(recvbuf) + rdispls[j], rcounts[j], rtypes[j], &p.copies))
+      p.doneOut[i] = p.doneIn[j] = 1;
+  }
+  plans.push_front(std::move(p));
+  if (plans.size() > kMaxPlans) plans.pop_back();
+  return plans.front();
+}
+
+// one Isend / Irecv per edge through the interposed entry points (device
+// blocks -> TEMPI transport, host blocks -> library sends and
+// descriptor-aware receives), receives first; self edges between device
+// objects as one request of queued copies
+int isir(const void *sendbuf, const int *scounts, const MPI_Aint *sdispls, const MPI_Datatype *stypes,
+         void *recvbuf, const int *rcounts, const MPI_Aint *rdispls, const MPI_Datatype *rtypes, MPI_Comm comm,
+         const Neighbours &nb) {
+  const std::vector<int> &in = nb.in, &out = nb.out;
+  const Plan &plan = plan_for(sendbuf, scounts, sdispls, stypes, recvbuf, rcounts, rdispls, rtypes, comm, nb);
+  const MPI_Comm c = plan.priv;
+  const int tag = 0x4E41; // "NA": alone on the private communicator
+  const std::vector<char> &doneIn = plan.doneIn, &doneOut = plan.doneOut;
+  std::vector<MPI_Request> reqs;
+  reqs.reserve(in.size() + out.size() + 1);
+  if (!plan.copies.items.empty()) {
+    reqs.push_back(p2p::start_local_copies(plan.copies));
+    p2p::start_queued(); // the copies run while the messages are posted
   }
   for (size_t i = 0; i < in.size(); ++i) {
     if (in[i] == MPI_PROC_NULL || doneIn[i]) continue;
@@ -154,6 +241,20 @@ int isir(const void *sendbuf, const int *scounts, const MPI_Aint *sdispls, const
 }
 
 } // namespace
+
+// a communicator being freed: its handle may come back for another one
+void neighbourhood_forget(MPI_Comm comm) {
+  neighbourCache.erase(comm);
+  for (auto it = plans.begin(); it != plans.end();)
+    it = it->comm == comm ? plans.erase(it) : std::next(it);
+}
+
+// MPI_Finalize: drop every plan (they hold type records)
+void neighbourhood_finalize() {
+  plans.clear();
+  neighbourCache.clear();
+}
+
 } // namespace tempi
 
 using namespace tempi;
@@ -167,13 +268,13 @@ TEMPI_EXPORT int MPI_Neighbor_alltoallw(const void *sendbuf, const int sendcount
     return next.MPI_Neighbor_alltoallw(sendbuf, sendcounts, sdispls, sendtypes, recvbuf, recvcounts, rdispls,
                                        recvtypes, comm);
   };
-  std::vector<int> in, out;
   // every rank takes the per-edge route, whatever memory its own blocks are
   // in: its neighbours' device blocks travel on the private duplicate, which
   // the library's own algorithm on `comm` would never match
-  if (!state.active || !gpu::available() || !neighbours(comm, in, out)) return lib();
+  const Neighbours *nb = state.active && gpu::available() ? neighbours(comm) : nullptr;
+  if (!nb) return lib();
   counters.neighbor_colls++;
-  return isir(sendbuf, sendcounts, sdispls, sendtypes, recvbuf, recvcounts, rdispls, recvtypes, comm, in, out);
+  return isir(sendbuf, sendcounts, sdispls, sendtypes, recvbuf, recvcounts, rdispls, recvtypes, comm, *nb);
 }
 
 TEMPI_EXPORT int MPI_Neighbor_alltoallv(const void *sendbuf, const int sendcounts[], const int sdispls[],
@@ -185,8 +286,9 @@ TEMPI_EXPORT int MPI_Neighbor_alltoallv(const void *sendbuf, const int sendcount
     return next.MPI_Neighbor_alltoallv(sendbuf, sendcounts, sdispls, sendtype, recvbuf, recvcounts, rdispls,
                                        recvtype, comm);
   };
-  std::vector<int> in, out;
-  if (!state.active || !gpu::available() || !neighbours(comm, in, out)) return lib();
+  const Neighbours *nb = state.active && gpu::available() ? neighbours(comm) : nullptr;
+  if (!nb) return lib();
+  const std::vector<int> &in = nb->in, &out = nb->out;
   // displacements are in extents of the one type: make the alltoallw form
   MPI_Aint lb, sext, rext;
   MPI_Type_get_extent(sendtype, &lb, &sext);
@@ -196,7 +298,7 @@ TEMPI_EXPORT int MPI_Neighbor_alltoallv(const void *sendbuf, const int sendcount
   for (size_t i = 0; i < in.size(); ++i) rd[i] = MPI_Aint(rdispls[i]) * rext;
   std::vector<MPI_Datatype> st(out.size(), sendtype), rt(in.size(), recvtype);
   counters.neighbor_colls++; // (every rank takes this route: see MPI_Neighbor_alltoallw)
-  return isir(sendbuf, sendcounts, sd.data(), st.data(), recvbuf, recvcounts, rd.data(), rt.data(), comm, in, out);
+  return isir(sendbuf, sendcounts, sd.data(), st.data(), recvbuf, recvcounts, rd.data(), rt.data(), comm, *nb);
 }
 
 TEMPI_EXPORT int MPI_Dist_graph_create_adjacent(MPI_Comm comm_old, int indegree, const int sources[],

@@ -1877,14 +1877,14 @@ struct HostIrecvOp : Op {
   }
 };
 
-// a self edge of a collective: the copy alone (see p2p::local_copy)
+// self edges of a collective: the copies alone, one request for all of
+// them (see p2p::local_copy, p2p::start_local_copies)
 struct LocalCopyOp : Op {
-  RecordRef srec, rrec;
+  std::vector<RecordRef> recs;
   int64_t bytes;
-  LocalCopyOp(const TypeRecord *s, const TypeRecord *r, int dev, int64_t b, const tempi_hip_copy_item &c)
-      : srec(s->ref()), rrec(r->ref()), bytes(b) {
-    device = dev;
-    pendingUnpack.add_copy(this, c);
+  explicit LocalCopyOp(const LocalCopies &plan) : recs(plan.recs), bytes(plan.bytes) {
+    device = plan.device;
+    for (const tempi_hip_copy_item &c : plan.items) pendingUnpack.add_copy(this, c);
     pendingUnpack.queue(this);
   }
   void gpu_done() override { done = true; }
@@ -2140,6 +2140,19 @@ int irecv(void *buf, int count, MPI_Datatype dt, int source, int tag, MPI_Comm c
 
 bool local_copy(const void *sbuf, int scount, MPI_Datatype stype, void *rbuf, int rcount, MPI_Datatype rtype,
                 MPI_Request *req) {
+  LocalCopies plan;
+  if (!plan_local_copy(sbuf, scount, stype, rbuf, rcount, rtype, &plan)) return false;
+  *req = start_local_copies(plan);
+  return true;
+}
+
+MPI_Request start_local_copies(const LocalCopies &plan) {
+  counters.send_direct += plan.items.size();
+  return add(std::make_unique<LocalCopyOp>(plan));
+}
+
+bool plan_local_copy(const void *sbuf, int scount, MPI_Datatype stype, void *rbuf, int rcount, MPI_Datatype rtype,
+                     LocalCopies *plan) {
   if (!directEnabled) return false;
   Route sr, rr;
   if (!handles(sbuf, scount, stype, 0, &sr) || !handles(rbuf, rcount, rtype, 0, &rr)) return false;
@@ -2154,8 +2167,12 @@ bool local_copy(const void *sbuf, int scount, MPI_Datatype stype, void *rbuf, in
   c.dst_first = rr.ptr.dptr;
   c.src = sflat;
   c.dst = rflat;
-  counters.send_direct++;
-  *req = add(std::make_unique<LocalCopyOp>(sr.rec, rr.rec, rr.ptr.device, bytes, c));
+  if (plan->device >= 0 && plan->device != rr.ptr.device) return false; // one request, one device
+  plan->device = rr.ptr.device;
+  plan->items.push_back(c);
+  plan->recs.push_back(sr.rec->ref());
+  plan->recs.push_back(rr.rec->ref());
+  plan->bytes += bytes;
   return true;
 }
 

@@ -38,8 +38,11 @@
 #pragma once
 
 #include "gpu.hpp"
+#include "type_cache.hpp"
 
 #include <mpi.h>
+
+#include <vector>
 
 namespace tempi {
 struct TypeRecord;
@@ -92,6 +95,19 @@ int irecv(void *buf, int count, MPI_Datatype dt, int source, int tag, MPI_Comm c
 bool local_copy(const void *sbuf, int scount, MPI_Datatype stype, void *rbuf, int rcount, MPI_Datatype rtype,
                 MPI_Request *req);
 void start_queued();
+// The same copies planned once and started many times (a neighbourhood
+// collective's self edges, cached per call signature): plan_local_copy
+// appends one copy to `plan` (false, nothing appended, when local_copy would
+// refuse it); start_local_copies queues all of them as ONE request.
+struct LocalCopies {
+  std::vector<tempi_hip_copy_item> items;
+  std::vector<RecordRef> recs; // the copies' type records, held while planned
+  int device = -1;
+  int64_t bytes = 0;
+};
+bool plan_local_copy(const void *sbuf, int scount, MPI_Datatype stype, void *rbuf, int rcount, MPI_Datatype rtype,
+                     LocalCopies *plan);
+MPI_Request start_local_copies(const LocalCopies &plan);
 
 // Messages of this process to itself are matched inside TEMPI while every
 // such message of the communicator can be (p2p.cpp, "self channel"). An

@@ -84,7 +84,7 @@ bool Packer::flat(int64_t count, tempi_hip_desc *out) const {
   return true;
 }
 
-int Packer::launch(bool pack, char *packed, char *origin, int64_t count, void *stream) const {
+int Packer::launch(bool pack, char *packed, char *origin, int64_t count, void *stream, Completion *done) const {
   if (count <= 0 || sb_.size == 0) return 0;
   std::vector<Dim> dims;
   dims.reserve(sb_.dims.size() + 1);
@@ -102,17 +102,42 @@ int Packer::launch(bool pack, char *packed, char *origin, int64_t count, void *s
     counters.unpacks++;
     counters.unpack_bytes += uint64_t(bytes);
   }
-  return issue(pack, packed, origin + sb_.start, tmp.block, tmp.dims.data(), int(tmp.dims.size()), stream);
+  char *first = origin + sb_.start;
+  if (done && tmp.dims.size() <= size_t(TEMPI_HIP_MAX_DIMS)) { // one descriptor: the ticket may fold into it
+    tempi_hip_desc d{};
+    d.block = tmp.block;
+    d.ndims = int32_t(tmp.dims.size());
+    for (size_t k = 0; k < tmp.dims.size(); ++k) {
+      d.counts[k] = tmp.dims[k].count;
+      d.strides[k] = tmp.dims[k].stride;
+    }
+    counters.launches++;
+    return pack ? tempi_hip_pack_ticket(packed, first, &d, stream, &done->flag, &done->ticket)
+                : tempi_hip_unpack_ticket(first, packed, &d, stream, &done->flag, &done->ticket);
+  }
+  const int e = issue(pack, packed, first, tmp.block, tmp.dims.data(), int(tmp.dims.size()), stream);
+  if (e || !done) return e;
+  return tempi_hip_stream_ticket(stream, &done->flag, &done->ticket);
 }
 
 int Packer::pack_async(void *packed, const void *origin, int64_t count, void *stream) const {
   return launch(true, static_cast<char *>(packed), const_cast<char *>(static_cast<const char *>(origin)),
-                count, stream);
+                count, stream, nullptr);
 }
 
 int Packer::unpack_async(void *origin, const void *packed, int64_t count, void *stream) const {
   return launch(false, const_cast<char *>(static_cast<const char *>(packed)), static_cast<char *>(origin),
-                count, stream);
+                count, stream, nullptr);
+}
+
+int Packer::pack_ticket(void *packed, const void *origin, int64_t count, void *stream, Completion *done) const {
+  return launch(true, static_cast<char *>(packed), const_cast<char *>(static_cast<const char *>(origin)),
+                count, stream, done);
+}
+
+int Packer::unpack_ticket(void *origin, const void *packed, int64_t count, void *stream, Completion *done) const {
+  return launch(false, const_cast<char *>(static_cast<const char *>(packed)), static_cast<char *>(origin),
+                count, stream, done);
 }
 
 } // namespace tempi

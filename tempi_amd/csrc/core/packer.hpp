@@ -30,6 +30,16 @@ public:
   int pack_async(void *packed, const void *origin, int64_t count, void *stream) const;
   int unpack_async(void *origin, const void *packed, int64_t count, void *stream) const;
 
+  // the same plus a completion ticket for a synchronous caller: done->flag
+  // reaching done->ticket means the work is complete (tempi_hip_ticket_wait);
+  // done->flag stays nullptr when nothing was launched
+  struct Completion {
+    const uint32_t *flag = nullptr;
+    uint32_t ticket = 0;
+  };
+  int pack_ticket(void *packed, const void *origin, int64_t count, void *stream, Completion *done) const;
+  int unpack_ticket(void *origin, const void *packed, int64_t count, void *stream, Completion *done) const;
+
   // the same work as launch items, appended to `out` (nothing is launched):
   // the transport batches many messages into one kernel launch
   void items(void *packed, const void *origin, int64_t count, std::vector<tempi_hip_batch_item> &out) const;
@@ -41,7 +51,7 @@ public:
   const StridedBlock &desc() const { return sb_; }
 
 private:
-  int launch(bool pack, char *packed, char *origin, int64_t count, void *stream) const;
+  int launch(bool pack, char *packed, char *origin, int64_t count, void *stream, Completion *done) const;
   StridedBlock sb_;
 };
 

@@ -11,7 +11,13 @@ namespace tempi {
 namespace {
 std::mutex mtx;
 std::unordered_map<MPI_Datatype, std::shared_ptr<TypeRecord>> cache;
+uint64_t generation = 1;
 } // namespace
+
+uint64_t type_generation() {
+  std::lock_guard<std::mutex> g(mtx);
+  return generation;
+}
 
 const TypeRecord *type_commit(MPI_Datatype t) {
   {
@@ -30,7 +36,10 @@ const TypeRecord *type_commit(MPI_Datatype t) {
   }
   std::lock_guard<std::mutex> g(mtx);
   auto &slot = cache[t];
-  if (!slot) slot = std::move(rec);
+  if (!slot) {
+    slot = std::move(rec);
+    generation++;
+  }
   return slot.get();
 }
 
@@ -42,7 +51,7 @@ const TypeRecord *type_lookup(MPI_Datatype t) {
 
 void type_release(MPI_Datatype t) {
   std::lock_guard<std::mutex> g(mtx);
-  cache.erase(t);
+  if (cache.erase(t)) generation++;
 }
 
 void types_init() {
@@ -57,6 +66,7 @@ void types_init() {
 void types_finalize() {
   std::lock_guard<std::mutex> g(mtx);
   cache.clear();
+  generation++;
 }
 
 } // namespace tempi

@@ -40,6 +40,9 @@ const TypeRecord *type_commit(MPI_Datatype t);
 // nullptr when unknown
 const TypeRecord *type_lookup(MPI_Datatype t);
 void type_release(MPI_Datatype t);
+// bumped whenever a record is added or dropped: plans that captured type
+// records by handle (neighbourhood-collective plans) are stale once it moves
+uint64_t type_generation();
 // records for the predefined dense types
 void types_init();
 void types_finalize();

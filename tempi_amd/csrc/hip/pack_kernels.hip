@@ -34,9 +34,11 @@
 #include <hip/hip_runtime.h>
 
 #include "tempi_hip.h"
+#include "ticket.hpp"
 
 #include <cstdint>
 #include <cstdlib>
+#include <mutex>
 #include <vector>
 
 namespace {
@@ -140,6 +142,23 @@ __device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t n, uint32_t fl
   if (!(flags & kXcdRange)) return b;
   const uint32_t x = b & 7, q = n >> 3, r = n & 7;
   return x * q + (x < r ? x : r) + (b >> 3);
+}
+
+// The end of a workgroup of a launch that stores its own completion ticket
+// (ticket.hpp): every wave waits for its memory operations to be acknowledged,
+// then one lane per workgroup releases them device-wide (agent scope: the XCD
+// L2s are not coherent with each other) as it counts the workgroup, and the
+// workgroup that completes the count stores the ticket for the host with a
+// system-scope release. sg.flag == nullptr (uniform): nothing to do.
+using tempi_ticket::Sig;
+__device__ __forceinline__ void wg_signal(const Sig &sg) {
+  if (!sg.flag) return;
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t old = __hip_atomic_fetch_add(sg.counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (old + 1u == sg.target) __hip_atomic_store(sg.flag, sg.ticket, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 constexpr int kBlock = TEMPI_BLOCK;
@@ -442,13 +461,15 @@ __device__ __forceinline__ void unpack_body(const KArgs<ND> &a, uint32_t blk, ui
 }
 
 template <int W, int ND>
-__global__ __launch_bounds__(kBlock) void pack_kernel(const KArgs<ND> a) {
+__global__ __launch_bounds__(kBlock) void pack_kernel(const KArgs<ND> a, const Sig sg) {
   pack_body<W, ND>(a, xcd_tile(blockIdx.x, gridDim.x, a.flags), gridDim.x);
+  wg_signal(sg);
 }
 
 template <int W, int ND>
-__global__ __launch_bounds__(kBlock) void unpack_kernel(const KArgs<ND> a) {
+__global__ __launch_bounds__(kBlock) void unpack_kernel(const KArgs<ND> a, const Sig sg) {
   unpack_body<W, ND>(a, xcd_tile(blockIdx.x, gridDim.x, a.flags), gridDim.x);
+  wg_signal(sg);
 }
 
 // ------------------------------------------- wave-interleaved scatter (unpack)
@@ -559,11 +580,13 @@ __device__ __forceinline__ void pack_il_tile(const KArgs<ND> &a, uint32_t tileId
   st(reinterpret_cast<uint4 *>(a.chunk0 + size_t(c0 + threadIdx.x) * 16), tile[threadIdx.x], kNtPacked);
 }
 
-template <int W, int ND> __global__ __launch_bounds__(kBlock) void pack_il_kernel(const KArgs<ND> a) {
+template <int W, int ND> __global__ __launch_bounds__(kBlock) void pack_il_kernel(const KArgs<ND> a, const Sig sg) {
   pack_il_tile<W, ND>(a, xcd_tile(blockIdx.x, gridDim.x, a.flags), gridDim.x);
+  wg_signal(sg);
 }
-template <int W, int ND> __global__ __launch_bounds__(kBlock) void unpack_il_kernel(const KArgs<ND> a) {
+template <int W, int ND> __global__ __launch_bounds__(kBlock) void unpack_il_kernel(const KArgs<ND> a, const Sig sg) {
   unpack_il_tile<W, ND>(a, xcd_tile(blockIdx.x, gridDim.x, a.flags), gridDim.x);
+  wg_signal(sg);
 }
 
 // ------------------------------------------------- dense-window gather (pack)
@@ -591,9 +614,8 @@ constexpr int kDenseMaxBlock = 32;
 static_assert(kDenseLds <= 64 * 1024, "dense window too large for LDS");
 
 template <int ND>
-__global__ __launch_bounds__(kBlock) void pack_dense_kernel(const KArgs<ND> a) {
+__device__ __forceinline__ void pack_dense_tile(const KArgs<ND> &a, uint32_t blk) {
   __shared__ uint4 win[kDenseLds / 16];
-  const uint32_t blk = xcd_tile(blockIdx.x, gridDim.x, a.flags);
   const uint32_t c0 = blk * kBlock; // first chunk of this tile
   const uint32_t c1 = min(c0 + uint32_t(kBlock), a.nchunks);
   // packed bytes of the tile (W = 1: words are bytes)
@@ -650,6 +672,12 @@ __global__ __launch_bounds__(kBlock) void pack_dense_kernel(const KArgs<ND> a) {
       a.chunk0[size_t(c) * 16 + size_t(j)] = w8[int64_t(base) + int64_t(row - rl) * stride + w];
     }
   }
+}
+
+template <int ND>
+__global__ __launch_bounds__(kBlock) void pack_dense_kernel(const KArgs<ND> a, const Sig sg) {
+  pack_dense_tile<ND>(a, xcd_tile(blockIdx.x, gridDim.x, a.flags));
+  wg_signal(sg);
 }
 
 // Many objects in ONE launch (e.g. the 26 x nQuants faces of a halo step):
@@ -788,6 +816,26 @@ uint32_t xcd_flag(const char *first, const Norm &n) {
 // item by run_batch; 0 for the single-object entry points)
 thread_local uint32_t gItemFlags = 0;
 
+// the completion-ticket fold offered to this thread's next single-object
+// launch (the *_ticket entry points set it around their launch)
+thread_local tempi_ticket::Fold *gFold = nullptr;
+
+// the kernel's Sig for a launch of `blocks` workgroups: the fold when one is
+// offered and the grid is small enough (counted on the host as the kernel
+// will count on the device), else none
+Sig take_fold(uint32_t blocks) {
+  Sig sg{nullptr, nullptr, 0, 0};
+  tempi_ticket::Fold *f = gFold;
+  if (!f || f->taken || !f->t || !f->t->counter || blocks == 0 || blocks > f->max_blocks) return sg;
+  f->t->counted += blocks;
+  f->taken = true;
+  sg.counter = f->t->counter;
+  sg.flag = f->t->dev;
+  sg.target = f->t->counted;
+  sg.ticket = f->ticket;
+  return sg;
+}
+
 // descriptor + workgroup count of one object
 template <int W, int ND>
 void make_args(char *packed, char *first, const Norm &n, KArgs<ND> *out, uint32_t *blocks) {
@@ -824,10 +872,11 @@ int launch_nd(bool pack, char *packed, char *first, const Norm &n, hipStream_t s
   make_args<W, ND>(packed, first, n, &a, &blocks);
   if (blocks == 0) return 0;
   if (!pack) a.flags |= xcd_flag(first, n);
+  const Sig sg = take_fold(blocks);
   if (pack)
-    hipLaunchKernelGGL((pack_kernel<W, ND>), dim3(blocks), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL((pack_kernel<W, ND>), dim3(blocks), dim3(kBlock), 0, s, a, sg);
   else
-    hipLaunchKernelGGL((unpack_kernel<W, ND>), dim3(blocks), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL((unpack_kernel<W, ND>), dim3(blocks), dim3(kBlock), 0, s, a, sg);
   return int(hipGetLastError());
 }
 
@@ -926,7 +975,8 @@ template <int ND> int launch_dense_nd(char *packed, char *first, const Norm &n, 
   uint32_t blocks;
   make_args<1, ND>(packed, first, n, &a, &blocks);
   if (blocks == 0) return 0;
-  hipLaunchKernelGGL((pack_dense_kernel<ND>), dim3(blocks), dim3(kBlock), 0, s, a);
+  const Sig sg = take_fold(blocks);
+  hipLaunchKernelGGL((pack_dense_kernel<ND>), dim3(blocks), dim3(kBlock), 0, s, a, sg);
   return int(hipGetLastError());
 }
 
@@ -948,10 +998,11 @@ template <int W, int ND> int launch_il_nd(bool pack, char *packed, char *first, 
   blocks = (a.nchunks + kBlock - 1) / kBlock; // one tile per workgroup, no grid-stride
   if (blocks == 0) return 0;
   if (!pack) a.flags |= xcd_flag(first, n);
+  const Sig sg = take_fold(blocks);
   if (pack)
-    hipLaunchKernelGGL((pack_il_kernel<W, ND>), dim3(blocks), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL((pack_il_kernel<W, ND>), dim3(blocks), dim3(kBlock), 0, s, a, sg);
   else
-    hipLaunchKernelGGL((unpack_il_kernel<W, ND>), dim3(blocks), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL((unpack_il_kernel<W, ND>), dim3(blocks), dim3(kBlock), 0, s, a, sg);
   return int(hipGetLastError());
 }
 
@@ -1399,6 +1450,54 @@ int tempi_hip_unpack(void *first, const void *packed, const tempi_hip_desc *d, v
   if (!normalise(d, &n)) return int(hipErrorInvalidValue);
   return launch_split(false, const_cast<char *>(static_cast<const char *>(packed)),
                       static_cast<char *>(first), n, static_cast<hipStream_t>(stream));
+}
+
+} // extern "C"
+
+namespace {
+// pack / unpack + a completion ticket: folded into the work kernel when the
+// work is one launch of at most fold_max_blocks() workgroups, else the ticket
+// kernel queued behind it. The mutex keeps tickets and folded counts in
+// launch order on the stream.
+int with_ticket(bool pack, char *packed, char *first, const tempi_hip_desc *d, hipStream_t s, const uint32_t **flag,
+                uint32_t *ticket) {
+  Norm n;
+  if (!normalise(d, &n)) return int(hipErrorInvalidValue);
+  bool single = norm_bytes(n) < kMaxLaunchBytes; // launch_split makes exactly one launch
+  for (int k = 0; k < n.nd; ++k) single &= n.cnt[k] < (int64_t(1) << 32);
+  std::lock_guard<std::mutex> lock(tempi_ticket::mutex());
+  tempi_ticket::Ticket *t = tempi_ticket::of(s);
+  if (!t) return int(hipErrorOutOfMemory);
+  tempi_ticket::Fold fold;
+  fold.t = t;
+  fold.ticket = ++t->next;
+  fold.max_blocks = single ? tempi_ticket::fold_max_blocks() : 0;
+  gFold = &fold;
+  const int e = launch_split(pack, packed, first, n, s);
+  gFold = nullptr;
+  if (e) {
+    if (fold.taken) t->broken = true; // the host counted a launch that never ran
+    return e;
+  }
+  *flag = t->host;
+  *ticket = fold.ticket;
+  if (fold.taken) tempi_ticket::stats().folded++;
+  return fold.taken ? 0 : int(tempi_ticket::queue_kernel(*t, s, fold.ticket));
+}
+} // namespace
+
+extern "C" {
+
+int tempi_hip_pack_ticket(void *packed, const void *first, const tempi_hip_desc *d, void *stream,
+                          const uint32_t **flag, uint32_t *ticket) {
+  return with_ticket(true, static_cast<char *>(packed), const_cast<char *>(static_cast<const char *>(first)), d,
+                     static_cast<hipStream_t>(stream), flag, ticket);
+}
+
+int tempi_hip_unpack_ticket(void *first, const void *packed, const tempi_hip_desc *d, void *stream,
+                            const uint32_t **flag, uint32_t *ticket) {
+  return with_ticket(false, const_cast<char *>(static_cast<const char *>(packed)), static_cast<char *>(first), d,
+                     static_cast<hipStream_t>(stream), flag, ticket);
 }
 
 int tempi_hip_pack_batch(const tempi_hip_batch_item *items, int n, void *stream) {

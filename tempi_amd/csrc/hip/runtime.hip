@@ -12,8 +12,10 @@
 #include <hip/hip_runtime.h>
 
 #include "tempi_hip.h"
+#include "ticket.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <unordered_map>
@@ -111,58 +113,70 @@ int tempi_hip_stream_synchronize(void *stream) {
   RET(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
 }
 
+} // extern "C"
+
 namespace {
 // one-lane kernel queued behind a synchronous call's work: its system-scope
 // release store of `ticket` to pinned host memory is what the host waits for
 __global__ void signal_ticket(uint32_t *flag, uint32_t ticket) {
   if (threadIdx.x == 0) __hip_atomic_store(flag, ticket, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-struct Ticket {
-  uint32_t *host = nullptr, *dev = nullptr;
-  uint32_t next = 0;
-};
 // one flag per stream: tickets reach a stream in increasing order (issued
 // under the mutex), so a flag >= mine means the work before my ticket is done
-std::unordered_map<void *, Ticket> tickets;
-std::mutex ticketMutex;
+std::unordered_map<void *, tempi_ticket::Ticket> tickets;
 } // namespace
 
-// Wait for everything queued on `stream` the quick way: a kernel enqueued
-// behind it stores a ticket to a pinned flag, and the host spins on the flag.
-// Same-stream kernels run in order and each one's writes are visible
-// device-wide before the next starts (HIP's stream semantics), so the ticket
-// becomes visible only after the work before it is complete and written back
-// from L2; host memory written by that work is coherent (fine-grained). On
-// MI355X the host sees it 5 µs sooner than hipStreamSynchronize's completion
-// (7.6-8.9 vs 12.9-14.3 µs for a small kernel: tools/flagbench.hip,
-// profiles/r02/completion_flag_bench_s13.jsonl). The stream is queried every
-// ~20 µs of spinning, so a faulted stream (which never runs the signal) or a
-// stream that completed anyway ends the wait; any failure falls back to
-// hipStreamSynchronize.
-int tempi_hip_stream_ticket(void *stream, const uint32_t **flag, uint32_t *ticket) {
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  std::lock_guard<std::mutex> lock(ticketMutex);
-  Ticket &t = tickets[stream];
+namespace tempi_ticket {
+
+std::mutex &mutex() {
+  static std::mutex m;
+  return m;
+}
+
+Stats &stats() {
+  static Stats s;
+  return s;
+}
+
+Ticket *of(hipStream_t s) {
+  Ticket &t = tickets[s];
   if (!t.host) {
     void *h = nullptr, *d = nullptr;
     hipError_t e = hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable);
     if (e == hipSuccess) e = hipHostGetDevicePointer(&d, h, 0);
-    if (e != hipSuccess) return int(e);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      return nullptr;
+    }
     t.host = static_cast<uint32_t *>(h);
     t.dev = static_cast<uint32_t *>(d);
     __atomic_store_n(t.host, 0u, __ATOMIC_RELEASE);
   }
-  *ticket = ++t.next;
-  hipLaunchKernelGGL(signal_ticket, dim3(1), dim3(64), 0, s, t.dev, *ticket);
-  *flag = t.host;
-  RET(hipGetLastError());
+  if (!t.counter || t.broken) { // (re)start the workgroup count at 0 once the stream is idle
+    if (!t.counter && hipMalloc(reinterpret_cast<void **>(&t.counter), 64) != hipSuccess) {
+      (void)hipGetLastError();
+      t.counter = nullptr;
+      return &t; // tickets work; folds are refused (no counter)
+    }
+    if (hipStreamSynchronize(s) != hipSuccess || hipMemsetAsync(t.counter, 0, 64, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess) {
+      (void)hipGetLastError();
+      t.broken = true;
+      return &t;
+    }
+    t.counted = 0;
+    t.broken = false;
+  }
+  return &t;
 }
 
-int tempi_hip_stream_signal_wait(void *stream) {
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  const uint32_t *flag = nullptr;
-  uint32_t ticket = 0;
-  if (tempi_hip_stream_ticket(stream, &flag, &ticket) != 0) RET(hipStreamSynchronize(s));
+hipError_t queue_kernel(Ticket &t, hipStream_t s, uint32_t ticket) {
+  stats().queued++;
+  hipLaunchKernelGGL(signal_ticket, dim3(1), dim3(64), 0, s, t.dev, ticket);
+  return hipGetLastError();
+}
+
+int wait(hipStream_t s, const uint32_t *flag, uint32_t ticket) {
   for (uint32_t spins = 1;; ++spins) {
     if (int32_t(__atomic_load_n(flag, __ATOMIC_ACQUIRE) - ticket) >= 0) return 0;
     if ((spins & 1023) == 0) { // ~20 µs of pause loops
@@ -172,6 +186,57 @@ int tempi_hip_stream_signal_wait(void *stream) {
     }
     __builtin_ia32_pause();
   }
+}
+
+uint32_t fold_max_blocks() {
+  static const uint32_t v = [] {
+    const char *e = std::getenv("TEMPI_FOLD_MAX_BLOCKS");
+    return e ? uint32_t(std::strtoul(e, nullptr, 10)) : uint32_t(TEMPI_FOLD_MAX_BLOCKS);
+  }();
+  return v;
+}
+
+} // namespace tempi_ticket
+
+extern "C" {
+
+// Wait for everything queued on `stream` the quick way: a kernel enqueued
+// behind it stores a ticket to a pinned flag, and the host spins on the flag.
+// Same-stream kernels run in order and each one's writes are visible
+// device-wide before the next starts (HIP's stream semantics), so the ticket
+// becomes visible only after the work before it is complete and written back
+// from L2. On MI355X the host sees it 5 µs sooner than hipStreamSynchronize's
+// completion (7.6-8.9 vs 12.9-14.3 µs for a small kernel: tools/flagbench.hip,
+// profiles/r02/completion_flag_bench_s13.jsonl). Callers use it only when the
+// work wrote device memory or TEMPI's own coherent slabs (host memory of the
+// application may be coarse-grained: hipStreamSynchronize's system-scope
+// release is what makes it host-visible).
+int tempi_hip_stream_ticket(void *stream, const uint32_t **flag, uint32_t *ticket) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  std::lock_guard<std::mutex> lock(tempi_ticket::mutex());
+  tempi_ticket::Ticket *t = tempi_ticket::of(s);
+  if (!t) return int(hipErrorOutOfMemory);
+  *ticket = ++t->next;
+  *flag = t->host;
+  RET(tempi_ticket::queue_kernel(*t, s, *ticket));
+}
+
+void tempi_hip_ticket_stats(uint64_t *folded, uint64_t *queued) {
+  std::lock_guard<std::mutex> lock(tempi_ticket::mutex());
+  *folded = tempi_ticket::stats().folded;
+  *queued = tempi_ticket::stats().queued;
+}
+
+int tempi_hip_ticket_wait(void *stream, const uint32_t *flag, uint32_t ticket) {
+  return tempi_ticket::wait(static_cast<hipStream_t>(stream), flag, ticket);
+}
+
+int tempi_hip_stream_signal_wait(void *stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const uint32_t *flag = nullptr;
+  uint32_t ticket = 0;
+  if (tempi_hip_stream_ticket(stream, &flag, &ticket) != 0) RET(hipStreamSynchronize(s));
+  return tempi_ticket::wait(s, flag, ticket);
 }
 
 int tempi_hip_stream_wait_event(void *stream, void *event) {

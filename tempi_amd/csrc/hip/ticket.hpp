@@ -1,0 +1,76 @@
+// tempi_amd/csrc/hip/ticket.hpp -- completion tickets of synchronous calls,
+// shared by runtime.hip (the tickets, the wait) and pack_kernels.hip (work
+// kernels that store the ticket themselves). Internal to libtempi_hip.so.
+//
+// A synchronous MPI_Pack / MPI_Unpack (/root/reference/src/internal/
+// packer_2d.cu:101-118 waits with cudaStreamSynchronize) waits here for a
+// ticket in pinned, coherent host memory instead: HIP's completion path costs
+// ~5 us more than a flag the GPU stores (tools/flagbench.hip,
+// profiles/r02/completion_flag_bench_s13.jsonl). Two ways to store it:
+//  * a one-lane kernel queued behind the work (any work, any size);
+//  * FOLDED into a small work kernel: every workgroup, once its stores are
+//    done, makes them visible device-wide (agent-scope release) and counts
+//    itself on a per-stream device counter; the workgroup that completes the
+//    count stores the ticket with a system-scope release. That saves the
+//    second kernel's dispatch behind the first.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <mutex>
+
+// grids up to this many workgroups store their ticket themselves: each one
+// adds an agent-scope release (an L2 write-back) to its end, so a large grid
+// keeps the separate ticket kernel (tools/gpu_fold_ab.sh measures the cut)
+#ifndef TEMPI_FOLD_MAX_BLOCKS
+#define TEMPI_FOLD_MAX_BLOCKS 2048
+#endif
+
+namespace tempi_ticket {
+
+struct Ticket {
+  uint32_t *host = nullptr, *dev = nullptr; // the flag (pinned, coherent)
+  uint32_t next = 0;                        // last ticket issued
+  uint32_t *counter = nullptr;              // device: workgroups of folded launches counted so far
+  uint32_t counted = 0;                     // the host's running total of the same (mod 2^32)
+  bool broken = false;                      // a folded launch failed: counter and total disagree
+};
+
+// tickets stored by work kernels / by the ticket kernel, all streams
+struct Stats {
+  uint64_t folded = 0, queued = 0;
+};
+Stats &stats(); // (caller holds mutex())
+
+// A fold offered to the next single launch of this thread (set by the
+// *_ticket entry points around their launch): the launch takes it only when
+// its grid is at most max_blocks workgroups.
+struct Fold {
+  Ticket *t = nullptr;
+  uint32_t ticket = 0;
+  uint32_t max_blocks = 0;
+  bool taken = false;
+};
+
+// the kernel-side view, passed as a kernel argument (flag == nullptr: none)
+struct Sig {
+  uint32_t *counter;
+  uint32_t *flag;
+  uint32_t target; // counter value once this launch's last workgroup counts itself
+  uint32_t ticket;
+};
+
+std::mutex &mutex();
+// the stream's ticket state, flag and counter allocated on first use
+// (caller holds mutex()); nullptr when allocation failed
+Ticket *of(hipStream_t s);
+// queue the one-lane ticket kernel storing `ticket` (caller holds mutex())
+hipError_t queue_kernel(Ticket &t, hipStream_t s, uint32_t ticket);
+// spin until the flag reaches `ticket`; the stream is queried every ~20 us,
+// so a faulted stream ends the wait with its error
+int wait(hipStream_t s, const uint32_t *flag, uint32_t ticket);
+// largest grid a work kernel takes a fold for (TEMPI_FOLD_MAX_BLOCKS, 0 = never)
+uint32_t fold_max_blocks();
+
+} // namespace tempi_ticket

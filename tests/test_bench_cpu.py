@@ -140,3 +140,86 @@ def test_type_commit_cost_section():
         assert 0 < r[k]["commit_us_median"] <= r[k]["commit_us_max"]
         assert set(r[k]["per_factory_median_us"]) == {"subarray", "byte_v_hv", "byte_v1_hv_hv", "byte_vn_hv_hv",
                                                       "subarray_v"}
+
+
+# ---- the driver's line: bounded size, parseable, every section summarised ----
+
+def _full_n1_record():
+    """round 2's fully populated N = 1 record (35 KB as printed then), with the
+    1 GiB cpu_baseline sample of this round"""
+    rec = json.load(open(os.path.join(ROOT, "profiles", "r02", "bench_line_s15.json")))
+    rec["halo"]["grid"], rec["halo"]["dims"] = 512, [1, 1, 1]
+    return rec
+
+
+def _n8_record():
+    """a synthetic N = 8 record with every N > 1 section at its largest"""
+    rec = json.load(open(os.path.join(ROOT, "profiles", "r02", "bench_line_torchrun_n2_s13.json")))
+    rec["n_gpus"] = 8
+    for name, g in (("halo", 512), ("halo_weak", 1024)):
+        rec[name]["grid"], rec[name]["dims"] = g, [2, 2, 2]
+        rec[name]["rank0_phase_us"] = {"isend": 1234.5, "irecv": 2345.6, "wait": 34567.8}
+        rec[name]["xgmi_counters"] = {"available": True, "per_unit_bytes": 123456789012, "read_bytes": 1 << 40}
+    for p in rec["pingpong_1d"]["points"]:
+        p["pairs"] = 4
+    for name in ("alltoallv", "nbr_alltoallv"):
+        for p in rec[name]["points"]:
+            p["ranks"] = 8
+    rec["perf_model"]["auto_model"] = "/some/very/long/path/" + "x" * 200 + "/perf.json"
+    return rec
+
+
+@pytest.mark.parametrize("which", ["n1", "n8", "n8_shared"])
+def test_line_is_bounded_and_parses(which):
+    rec = _full_n1_record() if which == "n1" else _n8_record()
+    shared = which == "n8_shared"
+    if shared:
+        bench.null_shared_gpu_fractions(rec)
+    line = bench.compact_line(rec, shared, "gpurun_out/bench_detail_n8.json")
+    s = json.dumps(line)
+    assert len(s) < 4096 and len(s) <= bench.LINE_LIMIT
+    back = json.loads(s)
+    # the contract's keys, the headline's roofline and cpu_baseline survive whole
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config"):
+        assert back[k] == rec[k]
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+        assert back["roofline"][k] == rec["roofline"][k]
+    assert "dropped" not in back  # nothing had to be dropped to fit
+    if which == "n1":
+        assert back["cpu_baseline"]["value"] == rec["cpu_baseline"]["value"]
+        assert back["cpu_baseline"]["cores"] == 1 and back["cpu_baseline"]["kind"] == "reference"
+        assert back["sweep"]["points"] == 64 and len(back["sweep"]["worst_touched"]) == 3
+        assert back["halo"]["us_per_iter"] == rec["halo"]["us_per_iter"] and back["halo"]["bound"] == "hbm"
+        assert back["mpi_pack"]["errors"] == 0 and back["config1"]["speedup"] == rec["config1"]["speedup"]
+    else:
+        for name in ("halo", "halo_weak", "pingpong", "pingpong_1d", "alltoallv", "nbr_alltoallv", "perf_model"):
+            assert name in back, name
+        assert len(back["alltoallv"]["points"]) == 3 and back["halo"]["dims"] == [2, 2, 2]
+    if shared:
+        assert back["shared_gpu"] is True and back["halo"]["frac"] is None and back["halo"]["aggregate_frac"] is None
+        assert all(p[-1] is None for n in ("pingpong", "pingpong_1d", "alltoallv", "nbr_alltoallv")
+                   for p in back[n]["points"])
+
+
+def test_line_overflow_drops_sections_in_order():
+    rec = _full_n1_record()
+    rec["mpi_pack"]["pack_speedup_geomean_by_target"] = {str(i): 1.0 for i in range(400)}
+    line = bench.compact_line(rec, False, None)
+    assert len(json.dumps(line)) <= bench.LINE_LIMIT
+    assert line["dropped"][0] == "mpi_pack" and "roofline" in line and "cpu_baseline" in line
+
+
+def test_line_section_errors_are_short():
+    rec = _full_n1_record()
+    rec["halo"] = {"error": "RuntimeError: " + "x" * 5000}
+    line = bench.compact_line(rec, False, None)
+    assert len(line["halo"]["error"]) <= 160 and len(json.dumps(line)) <= bench.LINE_LIMIT
+
+
+def test_shared_gpu_fractions_are_null():
+    rec = _n8_record()
+    bench.null_shared_gpu_fractions(rec)
+    r = rec["halo"]["roofline"]
+    assert r["frac"] is None and r["aggregate_frac"] is None and "note" in r
+    assert all(q["xgmi_frac"] is None for q in rec["pingpong_1d"]["points"])

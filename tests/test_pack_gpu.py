@@ -621,3 +621,122 @@ def test_unpack_batch_xcd_mapped_large(gpu):
         got = dst.view(rows, st)
         assert torch.equal(got[:, :bl], packed.view(rows, bl)), (rows, bl, st)
         assert int(got[:, bl:].count_nonzero()) == 0
+
+
+def _ticket_stats():
+    import tempi_amd
+
+    H = ctypes.CDLL(tempi_amd.LIBTEMPI_HIP)
+    f, q = ctypes.c_uint64(), ctypes.c_uint64()
+    H.tempi_hip_ticket_stats(ctypes.byref(f), ctypes.byref(q))
+    return f.value, q.value
+
+
+@pytest.mark.parametrize("rows,block,stride", [(1024, 512, 1024),     # config 1: 256 workgroups, folded
+                                               (4096, 24, 4608),      # halo x-face rows (interleaved unpack)
+                                               (20000, 3, 7),         # dense-window gather (1-byte words)
+                                               (16384, 512, 1024)])   # 8 MiB: 4096 workgroups, ticket kernel
+def test_synchronous_ticket_visible_device_wide(mpi, gpu, rows, block, stride):
+    """Synchronous MPI_Pack / MPI_Unpack between device buffers complete by a
+    ticket -- stored by the work kernel's last workgroup for small grids
+    (VERDICT r02 next 5), by the ticket kernel behind larger ones. Right
+    after each call returns, a kernel on ANOTHER stream (torch's) compares
+    the result: the bytes must already be visible device-wide. 60 rounds
+    with fresh contents each, so a stale line would show."""
+    torch = _torch()
+    t = mpi.Type_commit(mpi.Type_vector(rows, block, stride, mpi.BYTE))
+    ext = (rows - 1) * stride + block
+    try:
+        src = torch.empty(ext, dtype=torch.uint8, device=gpu)
+        packed = torch.empty(rows * block, dtype=torch.uint8, device=gpu)
+        back = torch.zeros(ext, dtype=torch.uint8, device=gpu)
+        c0, f0 = mpi.counters(), _ticket_stats()
+        g = torch.Generator(device=gpu).manual_seed(rows)
+        for r in range(60):
+            src.random_(0, 256, generator=g)
+            idx = torch.arange(rows, device=gpu).unsqueeze(1) * stride + torch.arange(block, device=gpu)
+            exp = src[idx.reshape(-1)]
+            torch.cuda.synchronize()
+            mpi.Pack(src.data_ptr(), 1, t, packed.data_ptr(), packed.numel(), 0)
+            assert torch.equal(packed, exp), f"round {r}: packed bytes not visible on torch's stream"
+            back.fill_(r & 0xFF)
+            torch.cuda.synchronize()
+            mpi.Unpack(packed.data_ptr(), packed.numel(), 0, back.data_ptr(), 1, t)
+            assert torch.equal(back[idx.reshape(-1)], exp), f"round {r}: unpacked bytes not visible"
+        c1, f1 = mpi.counters(), _ticket_stats()
+        assert c1["ticket_waits"] - c0["ticket_waits"] == 120 and c1["sync_waits"] == c0["sync_waits"]
+        if rows * block <= 4096 * 512:  # at most 2048 workgroups: every ticket folded into the work kernel
+            assert f1[0] - f0[0] == 120 and f1[1] == f0[1]
+        else:
+            assert f1[1] - f0[1] == 120
+    finally:
+        mpi.Type_free(t)
+
+
+def _hip():
+    hip = ctypes.CDLL("libamdhip64.so")
+    vp = ctypes.c_void_p
+    hip.hipHostMalloc.argtypes = [ctypes.POINTER(vp), ctypes.c_size_t, ctypes.c_uint]
+    hip.hipHostFree.argtypes = [vp]
+    hip.hipHostRegister.argtypes = [vp, ctypes.c_size_t, ctypes.c_uint]
+    hip.hipHostUnregister.argtypes = [vp]
+    return hip
+
+
+@pytest.mark.parametrize("kind", ["noncoherent", "registered", "coherent"])
+def test_application_pinned_memory_waits_with_stream_sync(mpi, gpu, kind):
+    """a kernel writing the APPLICATION's pinned host memory --
+    hipHostMalloc(NonCoherent) (coarse-grained), a hipHostRegister'ed buffer,
+    or coherent -- completes MPI_Pack (packed side there) and MPI_Unpack
+    (strided object there) with hipStreamSynchronize, never a ticket; the
+    host reads the bytes right after the call, 40 rounds with fresh data."""
+    torch = _torch()
+    hip = _hip()
+    rows, block, stride = 4096, 24, 4608
+    n = rows * block
+    ext = (rows - 1) * stride + block
+    t = mpi.Type_commit(mpi.Type_vector(rows, block, stride, mpi.BYTE))
+    ptrs = []
+    keep = []
+
+    def host_buf(nbytes):
+        if kind == "registered":
+            a = np.zeros(nbytes + 4096, dtype=np.uint8)
+            p = (a.ctypes.data + 4095) & ~4095
+            assert hip.hipHostRegister(ctypes.c_void_p(p), nbytes, 0x2 | 0x1) == 0  # mapped, portable
+            keep.append(a)
+            ptrs.append(("unreg", p))
+        else:
+            v = ctypes.c_void_p()
+            flags = 0x2 | 0x1 | (0x80000000 if kind == "noncoherent" else 0x40000000)
+            assert hip.hipHostMalloc(ctypes.byref(v), nbytes, flags) == 0
+            p = v.value
+            ptrs.append(("free", p))
+        return p, np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(p))
+
+    try:
+        hp, hview = host_buf(n)
+        sp, sview = host_buf(ext)
+        src = torch.empty(ext, dtype=torch.uint8, device=gpu)
+        c0 = mpi.counters()
+        rng = np.random.default_rng(5)
+        for r in range(40):
+            h = rng.integers(0, 256, ext, dtype=np.uint8)
+            src.copy_(torch.from_numpy(h))
+            torch.cuda.synchronize()
+            exp = np.lib.stride_tricks.as_strided(h, (rows, block), (stride, 1)).reshape(-1)
+            mpi.Pack(src.data_ptr(), 1, t, hp, n, 0)  # device object -> application pinned packed buffer
+            assert np.array_equal(hview, exp), f"round {r}: pack into {kind} host memory"
+            sview[:] = 0
+            pk = torch.from_numpy(exp.copy()).to(gpu)
+            torch.cuda.synchronize()
+            mpi.Unpack(pk.data_ptr(), n, 0, sp, 1, t)  # device packed -> application pinned object
+            got = np.lib.stride_tricks.as_strided(sview, (rows, block), (stride, 1)).reshape(-1)
+            assert np.array_equal(got, exp), f"round {r}: unpack into {kind} host memory"
+        c1 = mpi.counters()
+        assert c1["packs"] - c0["packs"] == 40 and c1["unpacks"] - c0["unpacks"] == 40  # the GPU path ran
+        assert c1["sync_waits"] - c0["sync_waits"] == 80 and c1["ticket_waits"] == c0["ticket_waits"]
+    finally:
+        mpi.Type_free(t)
+        for how, p in ptrs:
+            (hip.hipHostUnregister if how == "unreg" else hip.hipHostFree)(ctypes.c_void_p(p))
