@@ -71,6 +71,26 @@ void SlabPool::put(Slab *s) {
   free_[size_t(c)].push_back(s);
 }
 
+void SlabPool::discard(Slab *s, bool free) {
+  if (!s) return;
+  {
+    std::lock_guard<std::mutex> g(mtx_);
+    for (size_t i = 0; i < all_.size(); ++i)
+      if (all_[i] == s) {
+        all_.erase(all_.begin() + long(i));
+        break;
+      }
+    held_ -= s->size;
+  }
+  if (free) {
+    if (kind_ == DEVICE)
+      tempi_hip_free(s->dev);
+    else
+      tempi_hip_host_free(s->host);
+  }
+  delete s;
+}
+
 void SlabPool::release_all() {
   std::lock_guard<std::mutex> g(mtx_);
   for (Slab *s : all_) {

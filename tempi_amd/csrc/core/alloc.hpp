@@ -39,6 +39,10 @@ public:
   // a slab of at least n bytes (nullptr on allocation failure)
   Slab *get(size_t n, int device);
   void put(Slab *s);
+  // free a slab now instead of keeping it (an oversized one-off); free =
+  // false leaves the memory allocated (a kernel may still be using it) and
+  // only forgets it
+  void discard(Slab *s, bool free = true);
   void release_all();
   size_t bytes_held() const { return held_; }
 

@@ -153,6 +153,24 @@ template <typename F> int on_device(int device, bool pack, bool ticketOk, F &&fn
   return e;
 }
 
+// A staged MPI_Pack / MPI_Unpack's pinned slab is as large as the payload.
+// Kept in the pool it would hold up to GiB of pinned memory until MPI_Finalize
+// (ADVICE r02): slabs above this go back to the system after the call. After
+// a failed GPU call the slab is only returned once its stream has drained
+// (and leaked if that fails: a kernel may still be using it).
+constexpr size_t kKeepStagedMax = size_t(64) << 20;
+void stage_done(Slab *s, int device, bool failed) {
+  if (!s) return;
+  if (failed && tempi_hip_stream_synchronize(gpu::stream(device)) != 0) {
+    pinned_pool().discard(s, false);
+    return;
+  }
+  if (s->size > kKeepStagedMax)
+    pinned_pool().discard(s);
+  else
+    pinned_pool().put(s);
+}
+
 // byte span [lo, hi) relative to the origin touched by `n` elements
 void touched_span(MPI_Datatype t, int n, int64_t *lo, int64_t *hi) {
   MPI_Aint tlb, text, lb, ext;
@@ -314,13 +332,13 @@ int pack(const void *inbuf, int incount, MPI_Datatype datatype, void *outbuf, in
   });
   if (e != 0) { // (a GPU error falls back to the library instead of exiting)
     LOG_WARN("MPI_Pack: the GPU pack failed (" << tempi_hip_error_string(e) << "); the library packs it");
-    if (stage) pinned_pool().put(stage);
+    stage_done(stage, src.device, true);
     return library_pack(inbuf, incount, datatype, outbuf, outsize, position, comm);
   }
   if (stage) {
     counters.staged_packs++;
     std::memcpy(static_cast<char *>(outbuf) + *position, stage->host, size_t(bytes));
-    pinned_pool().put(stage);
+    stage_done(stage, src.device, false);
   }
   *position += int(bytes);
   return MPI_SUCCESS;
@@ -358,7 +376,7 @@ int unpack(const void *inbuf, int insize, int *position, void *outbuf, int outco
     return done ? rec->packer->unpack_ticket(origin, in, outcount, s, done)
                 : rec->packer->unpack_async(origin, in, outcount, s);
   });
-  if (stage) pinned_pool().put(stage);
+  stage_done(stage, dst.device, e != 0);
   if (e != 0) {
     LOG_WARN("MPI_Unpack: the GPU unpack failed (" << tempi_hip_error_string(e) << "); the library unpacks it");
     return library_unpack(inbuf, insize, position, outbuf, outcount, datatype, comm);

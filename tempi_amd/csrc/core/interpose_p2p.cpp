@@ -7,6 +7,7 @@
 // (SURVEY F8), and library waits keep TEMPI operations progressing.
 #include "trace.hpp"
 #include "counters.hpp"
+#include "log.hpp"
 #include "next_mpi.hpp"
 #include "p2p.hpp"
 #include "state.hpp"
@@ -410,11 +411,33 @@ TEMPI_EXPORT int MPI_Rsend_init(const void *buf, int count, MPI_Datatype datatyp
 }
 TEMPI_EXPORT int MPI_Recv_init(void *buf, int count, MPI_Datatype datatype, int source, int tag, MPI_Comm comm,
                                MPI_Request *request) {
+  resolve_next();
+  // (a persistent receive is the library's: a message a probe holds, or a
+  // descriptor from a co-located device send, never reaches it -- DESIGN §6)
+  if (state.active && p2p::holds(source, tag, comm))
+    LOG_WARN("MPI_Recv_init: a message it matches is held by an earlier MPI_Probe; the persistent receive "
+             "will not see it");
   TEMPI_SPILL_THEN(source, next.MPI_Recv_init(buf, count, datatype, source, tag, comm, request))
 }
+// MPI_Sendrecv_replace: when the receive is TEMPI's (a device object, or a
+// host buffer a descriptor or a held message may reach: p2p::host_recv_aware)
+// the outgoing element is packed into a host buffer first and the exchange
+// is MPI_Sendrecv through the interposed entry point (MPI_PACKED matches any
+// receive type); otherwise the library's.
 TEMPI_EXPORT int MPI_Sendrecv_replace(void *buf, int count, MPI_Datatype datatype, int dest, int sendtag, int source,
                                       int recvtag, MPI_Comm comm, MPI_Status *status) {
   resolve_next();
+  p2p::Route rr;
+  if (state.active && count > 0 &&
+      (p2p::handles(buf, count, datatype, source, &rr) || p2p::host_recv_aware(source, recvtag, comm))) {
+    int size = 0, pos = 0;
+    MPI_Pack_size(count, datatype, comm, &size);
+    std::vector<char> tmp(size_t(size > 0 ? size : 1));
+    int rc = tempi::pack(buf, count, datatype, tmp.data(), size, &pos, comm); // (device objects too)
+    if (rc != MPI_SUCCESS) return rc;
+    return MPI_Sendrecv(tmp.data(), pos, MPI_PACKED, dest, sendtag, buf, count, datatype, source, recvtag, comm,
+                        status);
+  }
   if (state.active) p2p::self_spill(comm, source);
   TEMPI_SPILL_THEN(dest, next.MPI_Sendrecv_replace(buf, count, datatype, dest, sendtag, source, recvtag, comm, status))
 }

@@ -1231,6 +1231,10 @@ struct Probed {
 };
 std::deque<std::unique_ptr<Probed>> probed;
 std::unordered_map<uint32_t, std::unique_ptr<Probed>> probedMsgs; // MPI_Mprobe handles
+// the communicator of each library message an MPI_Mprobe / MPI_Improbe here
+// returned: a matched receive of it raises errors on that communicator's
+// error handler
+std::unordered_map<MPI_Message, MPI_Comm> libMsgComm;
 uint32_t nextMsgHandle = 1;
 
 bool probed_matches(const Probed &p, int source, int tag, MPI_Comm comm) {
@@ -2501,10 +2505,15 @@ int recv_host_ipc_aware(void *buf, int count, MPI_Datatype dt, int source, int t
   return land(raw, n, st);
 }
 
+bool holds(int source, int tag, MPI_Comm comm) {
+  for (const auto &p : probed)
+    if (probed_matches(*p, source, tag, comm)) return true;
+  return false;
+}
+
 bool host_recv_aware(int source, int tag, MPI_Comm comm) {
   if (!state.active || !gpu::available() || source == MPI_PROC_NULL) return false;
-  for (const auto &p : probed) // a probe holds a message it may match
-    if (probed_matches(*p, source, tag, comm)) return true;
+  if (holds(source, tag, comm)) return true; // a probe holds a message it may match
   if (!hostRecvAware) return false; // TEMPI_NO_HOST_RECV (A/B only): host receives straight to the library
   return source == MPI_ANY_SOURCE || topology::colocated(comm, source);
 }
@@ -2530,6 +2539,26 @@ std::unique_ptr<Probed> receive_probed(MPI_Message *m, int n, MPI_Comm comm) {
   p->st.MPI_ERROR = MPI_SUCCESS;
   p->payload = descriptor_payload(p->bytes.data(), n);
   return p;
+}
+
+// A probe found a message of a descriptor's size from `src` with tag `tag`
+// and must receive it to look at it. Messages of `src` earlier than it (other
+// tags) would then be overtaken by a later receive that matches both (MPI's
+// non-overtaking rule), so they are received first, in order, and
+// kept too: the kept messages of a source are always its earliest, in send
+// order, and every TEMPI receive takes from them before the library.
+void hold_through(int src, int tag, MPI_Comm comm) {
+  for (;;) {
+    MPI_Message m = MPI_MESSAGE_NULL;
+    MPI_Status st;
+    int g = 0;
+    next.MPI_Improbe(src, MPI_ANY_TAG, comm, &g, &m, &st); // the earliest message of src
+    if (!g) LOG_FATAL("a probed message could not be matched");
+    int n = 0;
+    MPI_Get_count(&st, MPI_BYTE, &n);
+    probed.push_back(receive_probed(&m, n, comm));
+    if (st.MPI_TAG == tag) return; // the probed message: the first of src with its tag
+  }
 }
 
 void report(const Probed &p, MPI_Status *status) {
@@ -2564,7 +2593,9 @@ int probe(int source, int tag, MPI_Comm comm, int *flag, MPI_Status *status) {
     if (f) {
       int n = 0;
       MPI_Get_count(&st, MPI_BYTE, &n);
-      if (!descriptor_sized(n)) {
+      // only a co-located sender (this process included) can send a
+      // descriptor: anything else is reported as the library sees it
+      if (!descriptor_sized(n) || !topology::colocated(comm, st.MPI_SOURCE)) {
         if (status != MPI_STATUS_IGNORE) *status = st;
         if (flag) *flag = 1;
         return MPI_SUCCESS;
@@ -2572,13 +2603,9 @@ int probe(int source, int tag, MPI_Comm comm, int *flag, MPI_Status *status) {
       // The earliest message from that source with that tag is the one just
       // probed (the library keeps one sender's messages in order, and any
       // earlier one would have matched the probe first): take it out to look
-      // at it, and keep it for the receive that will match it.
-      MPI_Message m = MPI_MESSAGE_NULL;
-      int g = 0;
-      MPI_Status st2;
-      next.MPI_Improbe(st.MPI_SOURCE, st.MPI_TAG, comm, &g, &m, &st2);
-      if (!g) LOG_FATAL("a probed message could not be matched");
-      probed.push_back(receive_probed(&m, n, comm));
+      // at it -- with the source's earlier messages, in order -- and keep it
+      // for the receive that will match it.
+      hold_through(st.MPI_SOURCE, st.MPI_TAG, comm);
       continue;
     }
     if (flag) {
@@ -2620,8 +2647,11 @@ int mprobe(int source, int tag, MPI_Comm comm, int *flag, MPI_Message *msg, MPI_
     if (f) {
       int n = 0;
       MPI_Get_count(&st, MPI_BYTE, &n);
-      if (!descriptor_sized(n)) { // the library's message, as it is
+      // (a matched message leaves the matching order, so nothing before it
+      // needs keeping; only a co-located sender can send a descriptor)
+      if (!descriptor_sized(n) || !topology::colocated(comm, st.MPI_SOURCE)) { // the library's message, as it is
         *msg = m;
+        libMsgComm[m] = comm;
         if (status != MPI_STATUS_IGNORE) *status = st;
         if (flag) *flag = 1;
         return MPI_SUCCESS;
@@ -2640,16 +2670,22 @@ int imrecv(void *buf, int count, MPI_Datatype dt, MPI_Message *msg, MPI_Request 
   Route route;
   auto it = probedMsgs.find(uint32_t(*msg));
   if (it == probedMsgs.end()) { // the library's message
+    MPI_Comm mc = MPI_COMM_WORLD; // (a message probed before TEMPI was active)
+    auto lc = libMsgComm.find(*msg);
+    if (lc != libMsgComm.end()) {
+      mc = lc->second;
+      libMsgComm.erase(lc);
+    }
     if (*msg == MPI_MESSAGE_NULL || *msg == MPI_MESSAGE_NO_PROC || !handles(buf, count, dt, 0, &route))
       return next.MPI_Imrecv(buf, count, dt, msg, req);
     counters.irecvs++;
     if (!route.rec->packer) {
-      *req = add(std::make_unique<LibIrecvOp>(buf, count, dt, MPI_ANY_SOURCE, MPI_ANY_TAG, MPI_COMM_WORLD, msg));
+      *req = add(std::make_unique<LibIrecvOp>(buf, count, dt, MPI_ANY_SOURCE, MPI_ANY_TAG, mc, msg));
     } else {
-      const int64_t bytes = packed_bytes(route.rec, count, dt, MPI_COMM_WORLD);
+      const int64_t bytes = packed_bytes(route.rec, count, dt, mc);
       char *origin = static_cast<char *>(route.ptr.dptr) - route.rec->desc.start;
-      *req = add(std::make_unique<IrecvOp>(route.rec, origin, count, dt, MPI_ANY_SOURCE, MPI_ANY_TAG,
-                                           MPI_COMM_WORLD, route.ptr.device, bytes, msg));
+      *req = add(std::make_unique<IrecvOp>(route.rec, origin, count, dt, MPI_ANY_SOURCE, MPI_ANY_TAG, mc,
+                                           route.ptr.device, bytes, msg));
     }
     *msg = MPI_MESSAGE_NULL;
     return MPI_SUCCESS;
@@ -2676,8 +2712,10 @@ int imrecv(void *buf, int count, MPI_Datatype dt, MPI_Message *msg, MPI_Request 
 
 int mrecv(void *buf, int count, MPI_Datatype dt, MPI_Message *msg, MPI_Status *status) {
   Route route;
-  if (!probedMsgs.count(uint32_t(*msg)) && !handles(buf, count, dt, 0, &route))
+  if (!probedMsgs.count(uint32_t(*msg)) && !handles(buf, count, dt, 0, &route)) {
+    libMsgComm.erase(*msg);
     return next.MPI_Mrecv(buf, count, dt, msg, status); // the library's message into host memory
+  }
   MPI_Request r = MPI_REQUEST_NULL;
   const int rc = imrecv(buf, count, dt, msg, &r);
   if (rc != MPI_SUCCESS) return rc;

@@ -160,6 +160,8 @@ int recv_host_ipc_aware(void *buf, int count, MPI_Datatype dt, int source, int t
 // (TEMPI active with a GPU, and the source is this node or MPI_ANY_SOURCE),
 // or a message a probe is holding
 bool host_recv_aware(int source, int tag, MPI_Comm comm);
+// a probe holds a message a receive (source, tag, comm) would match
+bool holds(int source, int tag, MPI_Comm comm);
 // MPI_Irecv into host memory that recognises a descriptor and lands its bytes
 int irecv_host(void *buf, int count, MPI_Datatype dt, int source, int tag, MPI_Comm comm, MPI_Request *req);
 // MPI_Probe (flag == nullptr) / MPI_Iprobe: a descriptor is reported with its

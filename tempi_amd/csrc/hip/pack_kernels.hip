@@ -115,6 +115,14 @@ constexpr bool il_width(bool pack, int w) {
   return w <= 8 && ((pack ? TEMPI_PACK_IL_WIDTHS : TEMPI_UNPACK_IL_WIDTHS) & w) != 0;
 }
 template <int W> struct NtStrided { static constexpr bool value = TEMPI_NT == 2 || (TEMPI_NT == 3 && W == 16); };
+// the strided-side stores of the chunk-per-lane scatter (unpack_body):
+// -1 as NtStrided, 0 plain, 1 nontemporal (A/B knob, tools/gpu_gap_ab.sh)
+#ifndef TEMPI_NT_SCATTER
+#define TEMPI_NT_SCATTER -1
+#endif
+template <int W> struct NtScatter {
+  static constexpr bool value = TEMPI_NT_SCATTER < 0 ? NtStrided<W>::value : TEMPI_NT_SCATTER == 1;
+};
 
 // chunks each lane keeps in flight per grid-stride step
 template <int W> struct Unroll {
@@ -146,17 +154,21 @@ __device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t n, uint32_t fl
 
 // The end of a workgroup of a launch that stores its own completion ticket
 // (ticket.hpp): every wave waits for its memory operations to be acknowledged,
-// then one lane per workgroup releases them device-wide (agent scope: the XCD
-// L2s are not coherent with each other) as it counts the workgroup, and the
-// workgroup that completes the count stores the ticket for the host with a
-// system-scope release. sg.flag == nullptr (uniform): nothing to do.
+// then one lane per workgroup releases them as it counts the workgroup, and
+// the workgroup that completes the count stores the ticket for the host. The
+// release is system scope (an L2 write-back of this XCD; the XCD L2s are not
+// coherent with each other): the interposer takes a ticket only when the
+// kernel writes device memory or TEMPI's coherent slabs, but a process with
+// two HIP runtimes sees the other runtime's pinned host memory as device
+// memory, and host-visible must hold for that too.
+// sg.flag == nullptr (uniform): nothing to do.
 using tempi_ticket::Sig;
 __device__ __forceinline__ void wg_signal(const Sig &sg) {
   if (!sg.flag) return;
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
   if (threadIdx.x == 0) {
-    const uint32_t old = __hip_atomic_fetch_add(sg.counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t old = __hip_atomic_fetch_add(sg.counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
     if (old + 1u == sg.target) __hip_atomic_store(sg.flag, sg.ticket, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
@@ -437,7 +449,7 @@ __device__ __forceinline__ void unpack_body(const KArgs<ND> &a, uint32_t blk, ui
         if (CW == 1 || (CW <= 8 && one_run<ND>(row, mdiv(q + (CW - 1), a.mwpr), dig, a))) {
 #pragma unroll
           for (int j = 0; j < CW; ++j) {
-            st(reinterpret_cast<WT *>(a.strided + off + int64_t(w) * W), buf[u].w[j], NtStrided<W>::value);
+            st(reinterpret_cast<WT *>(a.strided + off + int64_t(w) * W), buf[u].w[j], NtScatter<W>::value);
             if (j + 1 < CW && ++w == a.wpr) {
               w = 0;
               if constexpr (ND >= 1) off += a.stride[0];
@@ -446,7 +458,7 @@ __device__ __forceinline__ void unpack_body(const KArgs<ND> &a, uint32_t blk, ui
         } else {
 #pragma unroll
           for (int j = 0; j < CW; ++j) {
-            st(reinterpret_cast<WT *>(a.strided + off + int64_t(w) * W), buf[u].w[j], NtStrided<W>::value);
+            st(reinterpret_cast<WT *>(a.strided + off + int64_t(w) * W), buf[u].w[j], NtScatter<W>::value);
             if (j + 1 < CW && ++w == a.wpr) {
               w = 0;
               next_row<ND>(off, dig, a);
@@ -802,8 +814,16 @@ int word_width(uintptr_t packed, uintptr_t first, const Norm &n) {
 #ifndef TEMPI_XCD_MAX_BLOCK
 #define TEMPI_XCD_MAX_BLOCK 1024
 #endif
+// TEMPI_XCD_GAPPED (A/B knob): also rows of whole 64-byte sectors with gaps
+// of >= 128 B between them
+#ifndef TEMPI_XCD_GAPPED
+#define TEMPI_XCD_GAPPED 0
+#endif
 uint32_t xcd_flag(const char *first, const Norm &n) {
   static const bool off = std::getenv("TEMPI_NO_XCD_MAP") != nullptr;
+  if (TEMPI_XCD_GAPPED && TEMPI_XCD_MAP && !off && n.nd > 0 && n.str[n.nd - 1] - n.block >= 128 &&
+      n.block % 64 == 0)
+    return kXcdRange;
   if (!TEMPI_XCD_MAP || off || n.nd == 0 || n.block >= TEMPI_XCD_MAX_BLOCK) return 0;
   const int64_t inner = n.str[n.nd - 1];
   if (inner < n.block || inner - n.block >= 128) return 0;

@@ -295,6 +295,13 @@ class MPI:
                    rcount, self.h(rt), source, rtag, self.h(self.COMM_WORLD if comm is None else comm), status)
         return self._decode(status, rt)
 
+    def Sendrecv_replace(self, buf, count, t, dest, stag, source, rtag, comm=None):
+        """MPI_Sendrecv_replace; returns (source, tag, count of t) of the receive"""
+        status = self._status()
+        self._call("MPI_Sendrecv_replace", ctypes.c_void_p(buf), count, self.h(t), dest, stag, source, rtag,
+                   self.h(self.COMM_WORLD if comm is None else comm), status)
+        return self._decode(status, t)
+
     def Cancel(self, req):
         r = self.Request(req)
         self._call("MPI_Cancel", ctypes.byref(r))

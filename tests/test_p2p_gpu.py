@@ -154,6 +154,16 @@ def test_every_receive_sees_payload(gpu, n, method):
         assert int(c["ipc"]) > 0 and int(c["ipc_copy"]) > 0 and int(c["oneshot"]) > 0, line
 
 
+@pytest.mark.parametrize("n,device", [(1, False), (2, False), (1, True), (2, True)])
+def test_probe_keeps_non_overtaking(gpu, n, device):
+    """a probe that must receive a descriptor-sized message to look at it
+    keeps the sender's earlier messages too, so a later MPI_ANY_TAG receive
+    still gets them in send order; MPI_Improbe / MPI_Mrecv and
+    MPI_Sendrecv_replace after a probe likewise"""
+    rc, out = mpi_launch.run(n, mpi_launch.py("probe_order.py", *(["--device"] if device else [])), timeout=180)
+    assert rc == 0 and "RESULT errors=0" in out, out[-3000:]
+
+
 @pytest.mark.parametrize("fault", [False, True])
 @pytest.mark.parametrize("method", ["AUTO", "XCOPY"])
 def test_cross_gpu_first_contact_canary(gpu, method, fault):

@@ -674,7 +674,17 @@ def test_synchronous_ticket_visible_device_wide(mpi, gpu, rows, block, stride):
 
 
 def _hip():
-    hip = ctypes.CDLL("libamdhip64.so")
+    """the HIP runtime libtempi_hip.so uses in this process. (When TEMPI is
+    loaded before torch, a PyTorch process holds two: ROCm's and torch's
+    bundled one, and each sees the other's pinned allocations as device
+    memory -- tools/diag_ptrattr.py)"""
+    import tempi_amd
+
+    ctypes.CDLL(tempi_amd.LIBTEMPI_HIP)
+    with open("/proc/self/maps") as f:
+        libs = sorted({line.split()[-1] for line in f if "libamdhip64" in line})
+    mine = [p for p in libs if "torch" not in p] or libs
+    hip = ctypes.CDLL(mine[0])
     vp = ctypes.c_void_p
     hip.hipHostMalloc.argtypes = [ctypes.POINTER(vp), ctypes.c_size_t, ctypes.c_uint]
     hip.hipHostFree.argtypes = [vp]
