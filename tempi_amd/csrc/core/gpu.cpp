@@ -19,6 +19,11 @@ std::vector<void *> streams; // [device * kMaxLanes + lane]
 std::vector<void *> evStart, evStop;
 int nLanes = 3;
 bool highPriority = true; // TEMPI_NO_STREAM_PRIORITY
+// TEMPI_TEST_HOST_ONLY (CPU tests): with no GPU visible, TEMPI still takes the
+// host-side paths it takes beside a GPU (descriptor-aware host receives, the
+// probe family, send gates), so they can be exercised on a machine without
+// one. Device pointers never occur there, so nothing reaches HIP.
+bool hostOnlyTest = false;
 } // namespace
 
 int lanes() { return nLanes; }
@@ -29,12 +34,13 @@ void choose_lanes(int ranksOnNode) {
   LOG_DEBUG("stream lanes: " << nLanes);
 }
 
-bool available() { return nDevices > 0; }
+bool available() { return nDevices > 0 || hostOnlyTest; }
 
 void init() {
   int n = 0;
   if (tempi_hip_device_count(&n) != 0) n = 0;
   nDevices = n;
+  hostOnlyTest = n == 0 && std::getenv("TEMPI_TEST_HOST_ONLY") != nullptr;
   std::lock_guard<std::mutex> g(mtx);
   streams.assign(size_t(n) * kMaxLanes, nullptr);
   nLanes = 1; // until choose_lanes()

@@ -1,0 +1,520 @@
+// tempi_amd/csrc/core/p2p_routes.cpp -- method choice, descriptors, peer
+// mappings, the first-contact canary (p2p_internal.hpp)
+#include "p2p_internal.hpp"
+
+#include "alloc.hpp"
+#include "counters.hpp"
+#include "env.hpp"
+#include "gpu.hpp"
+#include "log.hpp"
+#include "next_mpi.hpp"
+#include "packer.hpp"
+#include "perf_model.hpp"
+#include "state.hpp"
+#include "topology.hpp"
+#include "trace.hpp"
+#include "type_cache.hpp"
+
+#include <algorithm>
+#include <chrono>
+#include <cstdlib>
+#include <cstring>
+#include <unistd.h>
+
+namespace tempi {
+namespace p2p {
+namespace detail {
+
+std::unordered_map<uint64_t, std::shared_ptr<DirectShared>> directShared;
+uint64_t nextDirectToken = 1;
+bool directEnabled = true;
+bool ipcSystemLoads = true;
+bool hostRecvAware = true;
+MPI_Comm ctrlComm = MPI_COMM_NULL;
+int tagUb = 32767;
+bool gpuAwareLibrary = false;
+int64_t ipcMinBytes = 4 * 1024;
+
+namespace {
+// peer slabs mapped into this process: (world rank, slab id) -> base
+std::map<std::pair<int, uint64_t>, void *> ipcOpen;
+// peer allocations mapped for IPC COPY: (world rank, buffer id) -> mapping
+struct AllocMap {
+  void *base;                // the mapping in this process
+  uint64_t senderBase;       // the allocation's base in the sender's address space
+  unsigned char handle[TEMPI_HIP_IPC_HANDLE_BYTES];
+};
+std::map<std::pair<int, uint64_t>, AllocMap> ipcAllocOpen;
+// this process's allocations exported for IPC COPY: base -> (buffer id, handle)
+struct Export {
+  uint64_t id;
+  unsigned char handle[TEMPI_HIP_IPC_HANDLE_BYTES];
+};
+std::unordered_map<uintptr_t, Export> ipcExports;
+} // namespace
+bool ipcCopyEnabled = true;             // TEMPI_NO_IPC_COPY
+// Inside MPI_Alltoallv every receive is posted before any send is waited on,
+// so a rendezvous send cannot deadlock there: IPC COPY takes messages of any
+// size (TEMPI_NO_COLL_COPY keeps the point-to-point threshold)
+bool collCopyEnabled = true;
+// above MPICH's own eager limit (MPIR_CVAR_CH3_EAGER_MAX_MSG_SIZE, 128 KiB):
+// a program that works with the library's rendezvous works with this one
+int64_t ipcCopyMinBytes = 128 * 1024 + 1; // TEMPI_IPC_COPY_MIN_BYTES
+int64_t ipcCopyMinBlock = 256;          // TEMPI_IPC_COPY_MIN_BLOCK
+uint32_t nextCopyTag = 0;
+
+// A datatype handle that stays valid while an operation still needs it:
+// the application may MPI_Type_free its type right after MPI_Isend /
+// MPI_Irecv returns. Derived types are duplicated (the duplicate of a
+// committed type is committed); named types are returned as they are.
+bool named_type(MPI_Datatype t) {
+  int ni = 0, na = 0, nd = 0, comb = 0;
+  MPI_Type_get_envelope(t, &ni, &na, &nd, &comb);
+  return comb == MPI_COMBINER_NAMED;
+}
+MPI_Datatype hold_type(MPI_Datatype t) {
+  if (named_type(t)) return t;
+  MPI_Datatype d = MPI_DATATYPE_NULL;
+  MPI_Type_dup(t, &d);
+  return d;
+}
+void drop_type(MPI_Datatype t) {
+  if (t != MPI_DATATYPE_NULL && !named_type(t)) next.MPI_Type_free(&t);
+}
+
+// the status of a completed receive: `bytes` received (MPI_Get_count with
+// the receive's datatype then gives whole elements), without touching the
+// application's datatype handle, which may have been freed meanwhile
+void set_received(MPI_Status *s, int64_t bytes) { MPI_Status_set_elements_x(s, MPI_BYTE, MPI_Count(bytes)); }
+
+int64_t packed_bytes(const TypeRecord *rec, int count, MPI_Datatype dt, MPI_Comm comm) {
+  if (rec->desc.valid) return rec->desc.size * int64_t(count);
+  return pack_size(count, dt, comm);
+}
+
+int64_t pack_size(int count, MPI_Datatype dt, MPI_Comm comm) {
+  int s = 0;
+  MPI_Pack_size(count, dt, comm, &s);
+  return s;
+}
+
+namespace {
+// AUTO with a measured perf.json: the cheapest modelled method, cached per
+// (colocated, bytes, block) as in the reference (/root/reference/src/internal/
+// sender.cpp:251-290, async_operation.cpp:334-389). The DEVICE curve is
+// carried out by IPC between co-located ranks when the library is not
+// GPU-aware (the intra-node GPU-GPU curve is measured through that path).
+std::map<std::tuple<bool, int64_t, int64_t>, Method> modelCache;
+
+bool model_choice(int64_t bytes, bool colocated, int64_t block, Method *out) {
+  if (!systemPerformanceLoaded) return false;
+  const auto key = std::make_tuple(colocated, bytes, block);
+  auto it = modelCache.find(key);
+  if (it != modelCache.end()) {
+    *out = it->second;
+    return true;
+  }
+  const SystemPerformance &sp = systemPerformance;
+  const Opt o = model_oneshot(sp, colocated, bytes, block);
+  const Opt d = model_device(sp, colocated, bytes, block, !gpuAwareLibrary);
+  const Opt s = model_staged(sp, colocated, bytes, block);
+  Method best = Method::ONESHOT;
+  double t = o.ok ? o.v : 1e300;
+  const Method dev = gpuAwareLibrary ? Method::DEVICE : (colocated ? Method::IPC : Method::STAGED);
+  if (d.ok && d.v < t) {
+    best = dev;
+    t = d.v;
+  }
+  if (s.ok && s.v < t) best = Method::STAGED;
+  if (!o.ok && !d.ok && !s.ok) return false;
+  modelCache[key] = best;
+  *out = best;
+  return true;
+}
+} // namespace
+
+int64_t modelBlock = 512; // block length of the type being sent (set per call)
+
+Method choose(int64_t bytes, bool colocated) {
+  switch (env.datatype) {
+  case DatatypeMethod::ONESHOT:
+    return Method::ONESHOT;
+  case DatatypeMethod::STAGED:
+    return Method::STAGED;
+  case DatatypeMethod::DEVICE:
+    if (gpuAwareLibrary) return Method::DEVICE;
+    return colocated ? Method::IPC : Method::STAGED;
+  case DatatypeMethod::IPC:
+    return colocated ? Method::IPC : Method::ONESHOT;
+  case DatatypeMethod::AUTO:
+  default: {
+    Method m;
+    if (model_choice(bytes, colocated, modelBlock, &m)) return m;
+    if (colocated && bytes >= ipcMinBytes) return Method::IPC;
+    return Method::ONESHOT;
+  }
+  }
+}
+
+void clear_model_cache() { modelCache.clear(); }
+
+namespace {
+// peers whose memory could not be mapped: no more IPC to or from them
+std::vector<char> ipcBroken;
+} // namespace
+
+bool ipc_broken(int world) { return world >= 0 && size_t(world) < ipcBroken.size() && ipcBroken[size_t(world)]; }
+
+void mark_ipc_broken(int world) {
+  if (world < 0) return;
+  if (ipcBroken.size() <= size_t(world)) ipcBroken.resize(size_t(world) + 1, 0);
+  if (!ipcBroken[size_t(world)]) LOG_WARN("IPC with rank " << world << " unavailable; using host-staged transfers");
+  ipcBroken[size_t(world)] = 1;
+}
+
+// the sender's slab mapped into this process, or nullptr when it cannot be
+void *peer_pointer(const IpcDesc &d) {
+  if (d.senderPid == int32_t(getpid())) return reinterpret_cast<void *>(d.rawPtr);
+  auto key = std::make_pair(int(d.senderWorld), d.slabId);
+  auto it = ipcOpen.find(key);
+  if (it != ipcOpen.end()) return it->second;
+  void *p = nullptr;
+  // fault injection (tests): TEMPI_FAULT_IPC_OPEN makes every mapping fail
+  static const bool injectFault = std::getenv("TEMPI_FAULT_IPC_OPEN") != nullptr;
+  const int e = injectFault ? 1 : tempi_hip_ipc_open_handle(&p, d.handle);
+  if (e != 0) {
+    LOG_WARN("cannot map rank " << d.senderWorld << "'s slab: " << tempi_hip_error_string(e));
+    mark_ipc_broken(d.senderWorld);
+    return nullptr;
+  }
+  ipcOpen[key] = p;
+  return p;
+}
+
+// First contact with a peer on ANOTHER GPU. This pool's boxes have one GPU,
+// so the cross-GPU IPC path is first met on the driver's 8-GPU node: before
+// the transport trusts a mapping of that peer's memory, the first bytes a
+// descriptor names are read twice -- by a DMA copy (hipMemcpy) and by the
+// remote-load copy kernel the receiver uses (TEMPI_HIP_ITEM_REMOTE,
+// system-scope loads) -- and compared on the host. The kernel runs only after
+// the DMA read succeeded and when HIP reports that this GPU can load from the
+// mapping's GPU, so a mapping the fabric cannot serve fails as a HIP error,
+// never as a faulting kernel. A failed read or a mismatch turns IPC with that
+// peer off: this message and every later one go through the host (the NACK
+// path). Once per peer; at most 64 KiB.
+namespace {
+std::vector<signed char> canaryVerdict; // per world rank: 0 untested, 1 passed, -1 failed
+} // namespace
+bool faultCanary = false;               // TEMPI_FAULT_CANARY: the comparison fails (tests)
+
+bool canary(int world, const void *peerBytes, int64_t n, int device) {
+  if (world < 0) return true;
+  if (canaryVerdict.size() <= size_t(world)) canaryVerdict.resize(size_t(world) + 1, 0);
+  signed char &v = canaryVerdict[size_t(world)];
+  if (v) return v > 0;
+  n = std::min<int64_t>(n, 64 * 1024);
+  if (n <= 0) return true; // nothing to read yet: decide on a later message
+  int cur = 0;
+  tempi_hip_get_device(&cur);
+  if (cur != device) tempi_hip_set_device(device);
+  std::vector<unsigned char> viaKernel(size_t(n), 0), viaDma(size_t(n), 1);
+  bool ok = tempi_hip_memcpy(viaDma.data(), peerBytes, size_t(n)) == 0;
+  if (ok) {
+    tempi_hip_ptrinfo info;
+    if (tempi_hip_pointer_info(peerBytes, &info) == 0 && info.device >= 0 &&
+        !tempi_hip_can_access_peer(device, info.device)) {
+      LOG_WARN("canary: GPU " << device << " cannot load from GPU " << info.device << " (rank " << world << ")");
+      ok = false;
+    }
+  }
+  void *scratch = nullptr;
+  ok = ok && tempi_hip_malloc(&scratch, size_t(n)) == 0;
+  if (ok) {
+    tempi_hip_copy_item c{};
+    c.dst_first = scratch;
+    c.src_first = peerBytes;
+    c.dst.block = n;
+    c.dst.ndims = 0;
+    c.src = c.dst;
+    c.flags = TEMPI_HIP_ITEM_REMOTE;
+    void *s = gpu::stream(device);
+    ok = tempi_hip_copy_batch(&c, 1, s) == 0 && tempi_hip_stream_synchronize(s) == 0 &&
+         tempi_hip_memcpy(viaKernel.data(), scratch, size_t(n)) == 0;
+  }
+  if (scratch) tempi_hip_free(scratch);
+  if (cur != device) tempi_hip_set_device(cur);
+  if (ok && faultCanary) viaDma[0] ^= 0xFF;
+  ok = ok && viaKernel == viaDma;
+  v = ok ? 1 : -1;
+  if (ok) {
+    counters.canary_ok++;
+    LOG_DEBUG("canary: rank " << world << "'s GPU memory reads back right (" << n << " B)");
+  } else {
+    counters.canary_fail++;
+    LOG_WARN("canary: rank " << world << "'s GPU memory does not read back right through IPC");
+    mark_ipc_broken(world);
+  }
+  return ok;
+}
+
+void clear_canary() { canaryVerdict.clear(); }
+
+namespace {
+// A new allocation of a sender at the base of one we hold mapped, or with the
+// same handle bytes, means that sender freed the old one (its sends from it
+// have completed, so no copy of ours still reads it). Close those mappings
+// first: the runtime may hand back its cached import for identical handle
+// bytes -- the freed allocation's pages, not the new one's.
+void forget_freed_allocs(const IpcCopyDesc &d) {
+  const uint64_t senderBase = d.rawFirst - d.offset;
+  bool synced = false;
+  for (auto it = ipcAllocOpen.begin(); it != ipcAllocOpen.end();) {
+    const AllocMap &m = it->second;
+    if (it->first.first == int(d.senderWorld) &&
+        (m.senderBase == senderBase || std::memcmp(m.handle, d.handle, sizeof m.handle) == 0)) {
+      if (!synced) {
+        gpu::check(tempi_hip_device_synchronize(), "ipc mapping replace");
+        synced = true;
+      }
+      LOG_DEBUG("ipc copy unmap: rank " << d.senderWorld << " id " << it->first.second << " (replaced by id "
+                                        << d.bufferId << ")");
+      tempi_hip_ipc_close_handle(m.base);
+      counters.ipc_maps_replaced++;
+      it = ipcAllocOpen.erase(it);
+    } else {
+      ++it;
+    }
+  }
+}
+} // namespace
+
+// the sender's allocation mapped into this process (its first byte), or
+// nullptr when it cannot be
+const char *peer_object(const IpcCopyDesc &d) {
+  if (d.senderPid == int32_t(getpid())) return reinterpret_cast<const char *>(d.rawFirst);
+  auto key = std::make_pair(int(d.senderWorld), d.bufferId);
+  auto it = ipcAllocOpen.find(key);
+  if (it == ipcAllocOpen.end()) {
+    forget_freed_allocs(d);
+    void *p = nullptr;
+    static const bool injectFault = std::getenv("TEMPI_FAULT_IPC_OPEN") != nullptr;
+    const int e = injectFault ? 1 : tempi_hip_ipc_open_handle(&p, d.handle);
+    if (e != 0) {
+      LOG_WARN("cannot map rank " << d.senderWorld << "'s buffer: " << tempi_hip_error_string(e));
+      mark_ipc_broken(d.senderWorld);
+      return nullptr;
+    }
+    AllocMap m;
+    m.base = p;
+    m.senderBase = d.rawFirst - d.offset;
+    std::memcpy(m.handle, d.handle, sizeof m.handle);
+    it = ipcAllocOpen.emplace(key, m).first;
+    LOG_DEBUG("ipc copy map: rank " << d.senderWorld << " id " << d.bufferId << " -> " << p);
+  }
+  return static_cast<const char *>(it->second.base) + d.offset;
+}
+
+// this process's allocation holding `first` exported for IPC COPY: fills the
+// descriptor's handle / buffer id / offset; false when it cannot be exported
+// (not hipMalloc memory, or the export fails)
+bool export_object(const void *first, IpcCopyDesc *d) {
+  void *base = nullptr;
+  size_t size = 0;
+  uint64_t id = 0;
+  if (tempi_hip_mem_info(first, &base, &size, &id) != 0 || !base) return false;
+  const uintptr_t b = reinterpret_cast<uintptr_t>(base);
+  auto it = ipcExports.find(b);
+  if (it == ipcExports.end() || it->second.id != id) { // new, or freed and replaced at the same address
+    Export x;
+    x.id = id;
+    if (tempi_hip_ipc_get_handle(x.handle, base) != 0) return false;
+    it = ipcExports.insert_or_assign(b, x).first;
+    LOG_DEBUG("ipc copy export: base " << base << " size " << size << " id " << id);
+  } else {
+    LOG_DEBUG("ipc copy export reused: base " << base << " size " << size << " id " << id);
+  }
+  d->bufferId = id;
+  d->offset = uint64_t(reinterpret_cast<uintptr_t>(first) - b);
+  std::memcpy(d->handle, it->second.handle, sizeof d->handle);
+  return true;
+}
+
+// Peer allocations stay mapped for reuse (keyed by buffer id). A peer that
+// keeps allocating new buffers would make that grow without bound and hold
+// its freed memory alive, so past kMaxAllocMaps every mapping is closed --
+// after the copies that may still read them have been launched and run.
+constexpr size_t kMaxAllocMaps = 256;
+void recycle_alloc_maps() {
+  if (ipcAllocOpen.size() < kMaxAllocMaps) return;
+  flush_list(pendingUnpack, false);
+  gpu::check(tempi_hip_device_synchronize(), "ipc mapping recycle");
+  for (auto &kv : ipcAllocOpen) tempi_hip_ipc_close_handle(kv.second.base);
+  ipcAllocOpen.clear();
+}
+
+void close_mappings() {
+  for (auto &kv : ipcOpen) tempi_hip_ipc_close_handle(kv.second);
+  ipcOpen.clear();
+  for (auto &kv : ipcAllocOpen) tempi_hip_ipc_close_handle(kv.second.base);
+  ipcAllocOpen.clear();
+  ipcExports.clear();
+}
+
+// the receiver side is done with a direct send's bytes
+void direct_finish(std::shared_ptr<DirectShared> &sh) {
+  if (!sh) return;
+  if (sh->slab) {
+    device_pool().put(sh->slab);
+    sh->slab = nullptr;
+  }
+  sh->state = DirectShared::DONE;
+  if (sh->sender) sh->sender->peer_done();
+  sh.reset();
+}
+
+// the matched descriptor's shared state (unmatched until now)
+std::shared_ptr<DirectShared> claim_direct(const DirectDesc &d) {
+  auto it = directShared.find(d.token);
+  if (d.senderPid != int32_t(getpid()) || it == directShared.end())
+    LOG_FATAL("direct-send descriptor from another process (rank " << d.senderWorld << ")");
+  std::shared_ptr<DirectShared> sh = it->second;
+  directShared.erase(it);
+  return sh;
+}
+
+// a direct send's packed bytes into pinned host memory `dst`, synchronously
+// (receivers that are not a same-device TEMPI receive), then finish it
+void materialise_direct(std::shared_ptr<DirectShared> &sh, const DirectDesc &d, Slab *dst) {
+  void *s = gpu::stream(sh->device);
+  int cur = 0;
+  tempi_hip_get_device(&cur);
+  if (cur != sh->device) tempi_hip_set_device(sh->device);
+  if (sh->state == DirectShared::PACKED) {
+    gpu::check(tempi_hip_stream_synchronize(s), "direct fallback sync");
+    gpu::check(tempi_hip_memcpy(dst->host, sh->slab->dev, size_t(d.bytes)), "direct fallback copy");
+  } else {
+    gpu::check(tempi_hip_pack(dst->dev, reinterpret_cast<const void *>(d.first), &d.desc, s), "direct gather");
+    gpu::check(tempi_hip_stream_synchronize(s), "direct gather sync");
+  }
+  if (cur != sh->device) tempi_hip_set_device(cur);
+  direct_finish(sh);
+}
+
+bool is_direct(const void *msg, int n) {
+  if (size_t(n) != sizeof(DirectDesc)) return false;
+  uint64_t m[2];
+  std::memcpy(m, msg, sizeof m);
+  return m[0] == kMagicDirect && m[1] == kMagic1;
+}
+bool is_ipc_copy(const void *msg, int n) {
+  if (size_t(n) != sizeof(IpcCopyDesc)) return false;
+  uint64_t m[2];
+  std::memcpy(m, msg, sizeof m);
+  return m[0] == kMagicCopy && m[1] == kMagic1;
+}
+bool is_ipc(const void *msg, int n) {
+  if (size_t(n) != sizeof(IpcDesc)) return false;
+  uint64_t m[2];
+  std::memcpy(m, msg, sizeof m);
+  return m[0] == kMagic0 && m[1] == kMagic1;
+}
+
+// A descriptor landed in a host buffer of a receive that cannot use it
+// in place (library receives): fetch the bytes it names into `out` (the IPC
+// pull or the direct gather, blocking) and release the sender.
+void land_descriptor(const void *msg, int n, std::vector<char> &out) {
+  if (is_direct(msg, n)) {
+    DirectDesc d;
+    std::memcpy(&d, msg, sizeof d);
+    std::shared_ptr<DirectShared> sh = claim_direct(d);
+    Slab *h = pinned_pool().get(size_t(std::max<int64_t>(d.bytes, 1)), sh->device);
+    materialise_direct(sh, d, h);
+    out.assign(static_cast<char *>(h->host), static_cast<char *>(h->host) + d.bytes);
+    pinned_pool().put(h);
+    return;
+  }
+  auto resend = [&](int world, int tag, int64_t bytes, int code) { // the sender gathers and sends the bytes
+    MPI_Request r;
+    next.MPI_Irecv(out.data(), int(bytes), MPI_PACKED, world, tag, ctrlComm, &r);
+    send_ack(world, tag, code);
+    for (;;) {
+      int flag = 0;
+      next.MPI_Test(&r, &flag, MPI_STATUS_IGNORE);
+      if (flag) break;
+      progress();
+    }
+  };
+  if (is_ipc_copy(msg, n)) { // a host receive: the sender gathers for it
+    IpcCopyDesc d;
+    std::memcpy(&d, msg, sizeof d);
+    out.resize(size_t(std::max<int64_t>(d.bytes, 1)));
+    resend(d.senderWorld, d.ackTag, d.bytes, kCopyResend);
+    out.resize(size_t(d.bytes));
+    return;
+  }
+  IpcDesc d;
+  std::memcpy(&d, msg, sizeof d);
+  out.resize(size_t(std::max<int64_t>(d.bytes, 1)));
+  if (void *base = peer_pointer(d)) {
+    gpu::check(tempi_hip_memcpy(out.data(), static_cast<const char *>(base) + d.offset, size_t(d.bytes)), "ipc pull");
+    send_ack(d);
+  } else { // the sender re-sends through the host
+    resend(d.senderWorld, d.ackTag, d.bytes, 1);
+  }
+  out.resize(size_t(d.bytes));
+}
+
+int64_t desc_bytes(const tempi_hip_desc &d) {
+  int64_t b = d.block;
+  for (int k = 0; k < d.ndims; ++k) b *= d.counts[k];
+  return b;
+}
+
+// what tempi_hip_copy_supported() decides, from descriptors that are already
+// simplified (Packer::flat): the kernel's own normalisation can only merge
+// further, so <= 3 dimensions here is <= 3 there
+bool copy_ok(const tempi_hip_desc &dst, const tempi_hip_desc &src) {
+  const int64_t b = desc_bytes(src);
+  return dst.ndims <= 3 && src.ndims <= 3 && b == desc_bytes(dst) && b < (int64_t(1) << 31);
+}
+
+bool is_descriptor(const void *msg, int n) { return is_direct(msg, n) || is_ipc(msg, n) || is_ipc_copy(msg, n); }
+
+int64_t descriptor_payload(const void *msg, int n) {
+  int64_t b = n;
+  if (is_direct(msg, n)) std::memcpy(&b, static_cast<const char *>(msg) + offsetof(DirectDesc, bytes), sizeof b);
+  if (is_ipc(msg, n)) std::memcpy(&b, static_cast<const char *>(msg) + offsetof(IpcDesc, bytes), sizeof b);
+  if (is_ipc_copy(msg, n)) std::memcpy(&b, static_cast<const char *>(msg) + offsetof(IpcCopyDesc, bytes), sizeof b);
+  return b;
+}
+
+// A message that reached host memory (`msg`, n bytes: a descriptor or the
+// packed bytes themselves) delivered into the application's host receive
+// (buf, count, dt): the descriptor's bytes are fetched first, then unpacked.
+// Returns MPI_SUCCESS or MPI_ERR_TRUNCATE (nothing written); *received =
+// bytes delivered.
+int land_host(const char *msg, int n, void *buf, int count, MPI_Datatype dt, MPI_Comm comm, int64_t *received) {
+  std::vector<char> fetched;
+  if (is_descriptor(msg, n)) {
+    land_descriptor(msg, n, fetched); // releases the sender whatever happens next
+    msg = fetched.data();
+    n = int(fetched.size());
+  }
+  int size = 0;
+  MPI_Type_size(dt, &size);
+  *received = 0;
+  if (int64_t(n) > int64_t(size) * count) return MPI_ERR_TRUNCATE;
+  const int elems = size ? n / size : 0;
+  int pos = 0;
+  if (elems) next.MPI_Unpack(msg, n, &pos, buf, elems, dt, comm);
+  *received = int64_t(elems) * size;
+  return MPI_SUCCESS;
+}
+
+bool descriptor_sized(int n) {
+  return size_t(n) == sizeof(IpcDesc) || size_t(n) == sizeof(DirectDesc) || size_t(n) == sizeof(IpcCopyDesc);
+}
+
+} // namespace detail
+} // namespace p2p
+} // namespace tempi

@@ -7,7 +7,10 @@ C (160 B, tag 1), then:
   2. the same sends; MPI_Improbe(src, tag 2) claims B; MPI_Recv(src,
      MPI_ANY_TAG) returns A then C, and MPI_Mrecv returns B;
   3. the same sends; MPI_Probe(src, tag 2); MPI_Sendrecv_replace(src,
-     MPI_ANY_TAG) must return A, MPI_Recv(ANY_TAG) B, then C.
+     MPI_ANY_TAG) must return A, MPI_Recv(ANY_TAG) B, then C. (The exchange's
+     outgoing message has its receive posted beforehand: at one rank it goes
+     to this same process, and MPICH completes a send to itself only once a
+     receive matches it, so the program would hang with the library alone.)
 With --device, B is a strided device object (a real descriptor on IPC /
 DIRECT routes) received into host memory."""
 import os
@@ -97,15 +100,17 @@ for round_ in range(3):
         check_recv(round_, "B", s, t, n, buf)
     else:
         mpi.Probe(src, 2, mpi.BYTE)
-        # the replace buffer sends 1000 bytes to peer (which receives them below)
+        # the replace buffer sends 1000 bytes to peer, whose receive is posted first
+        b7 = np.zeros(1000, dtype=np.uint8)
+        r7 = mpi.Irecv(b7.ctypes.data, 1000, mpi.BYTE, src, 7)
         rep = payload(rank, 99, 1000)
         s, t, n = mpi.Sendrecv_replace(rep.ctypes.data, 1000, mpi.BYTE, peer, 7, src, mpi.ANY_TAG)
         check_recv(round_, "A", s, t, n, rep)
         for which in "BC":
             s, t, n = mpi.Recv_status(buf.ctypes.data, 4096, mpi.BYTE, src, mpi.ANY_TAG)
             check_recv(round_, which, s, t, n, buf)
-        s, t, n = mpi.Recv_status(buf.ctypes.data, 4096, mpi.BYTE, src, 7)
-        if (s, t, n) != (src, 7, 1000) or not np.array_equal(buf[:1000], payload(src, 99, 1000)):
+        _, (s, t, n) = mpi.Wait_status(r7, mpi.BYTE)
+        if (s, t, n) != (src, 7, 1000) or not np.array_equal(b7, payload(src, 99, 1000)):
             fail("Sendrecv_replace's outgoing message")
     mpi.Waitall(reqs)
     mpi.Barrier()

@@ -48,6 +48,21 @@ def test_completion_family_host():
     assert rc == 0 and "RESULT errors=0" in out, out[-3000:]
 
 
+@pytest.mark.parametrize("n,prog", [(2, ("p2p_world.py",)), (2, ("alltoallv.py", "--nnz", "2", "--scale", "100")),
+                                    (1, ("neighbor.py",)), (3, ("neighbor.py",)), (1, ("status.py",)),
+                                    (2, ("status.py",)), (1, ("order.py",)), (2, ("order.py",)),
+                                    (2, ("completion.py",)), (1, ("probe_order.py",)), (2, ("probe_order.py",))])
+def test_tempi_host_paths_without_gpu(n, prog):
+    """TEMPI's own host-side paths -- descriptor-aware host receives, the probe
+    family and its held messages, send gates, host collectives -- which run
+    only beside a GPU, forced on with TEMPI_TEST_HOST_ONLY (gpu.cpp) so that
+    they are checked here too (probe_order at one rank is the program that
+    hung on the GPU box in round 3: it relied on MPICH buffering a send to
+    itself)"""
+    rc, out = mpi_launch.run(n, mpi_launch.py(*prog), env={"TEMPI_TEST_HOST_ONLY": "1"}, timeout=180)
+    assert rc == 0 and out.count("RESULT errors=0") >= 1 and "errors=" not in out.replace("errors=0", ""), out[-3000:]
+
+
 def _torchrun(script, n):
     import os
     import socket
