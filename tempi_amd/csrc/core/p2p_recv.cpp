@@ -447,6 +447,54 @@ struct LibIrecvOp : Op {
   }
 };
 
+// Staging buffers of host receives, reused: a fresh buffer per receive costs
+// its zeroing (std::vector) or its first-touch page faults (new[]) on every
+// message, which on the host-buffer halo was most of TEMPI's overhead over
+// the library (tools/gpu_host_ab.sh). Power-of-two classes from 4 KiB; at
+// most kStageCache bytes kept.
+class StagePool {
+public:
+  struct Buf {
+    char *p = nullptr;
+    size_t cap = 0;
+  };
+  Buf get(size_t n) {
+    int c = 12;
+    while ((size_t(1) << c) < n) ++c;
+    auto &l = free_[size_t(c)];
+    Buf b;
+    if (!l.empty()) {
+      b = l.back();
+      l.pop_back();
+      held_ -= b.cap;
+      return b;
+    }
+    b.cap = size_t(1) << c;
+    b.p = new char[b.cap];
+    return b;
+  }
+  void put(Buf b) {
+    if (!b.p) return;
+    if (held_ + b.cap > kStageCache) {
+      delete[] b.p;
+      return;
+    }
+    int c = 12;
+    while ((size_t(1) << c) < b.cap) ++c;
+    free_[size_t(c)].push_back(b);
+    held_ += b.cap;
+  }
+
+private:
+  static constexpr size_t kStageCache = size_t(256) << 20;
+  std::vector<Buf> free_[64];
+  size_t held_ = 0;
+};
+StagePool &stage_pool() {
+  static auto *p = new StagePool(); // (never destroyed: ops may outlive statics)
+  return *p;
+}
+
 // A receive into host memory (p2p::irecv_host) that a co-located TEMPI send
 // may reach with a descriptor. Contiguous receives of at least kDescCap bytes
 // are posted in place with the buffer's first kDescCap bytes saved: a
@@ -460,7 +508,7 @@ struct HostIrecvOp : Op {
   MPI_Comm comm;
   int64_t cap = 0; // bytes the receive allows
   bool inPlace = false;
-  std::vector<char> stage;
+  StagePool::Buf stage;
   alignas(16) char saved[kDescCap];
   MPI_Status libStatus{};
   int64_t received = 0;
@@ -488,17 +536,25 @@ struct HostIrecvOp : Op {
       deliver(pre->bytes.data(), int(pre->bytes.size()));
       return;
     }
-    stage.resize(std::max({size_t(std::max<int64_t>(cap, 1)), size_t(pack_size(c, d, cm)), kDescCap}));
-    next.MPI_Irecv(stage.data(), int(stage.size()), MPI_PACKED, source, tag, cm, &lib);
+    const size_t n = std::max({size_t(std::max<int64_t>(cap, 1)), size_t(pack_size(c, d, cm)), kDescCap});
+    stage = stage_pool().get(n);
+    next.MPI_Irecv(stage.p, int(n), MPI_PACKED, source, tag, cm, &lib);
     watch(this);
   }
-  ~HostIrecvOp() override { drop_type(dt); }
+  ~HostIrecvOp() override {
+    drop_type(dt);
+    if (lib == MPI_REQUEST_NULL) stage_pool().put(stage); // (else the library may still write it: kept)
+  }
   void cancel() override {
     if (lib != MPI_REQUEST_NULL) next.MPI_Cancel(&lib);
   }
   void deliver(const char *msg, int n) {
     err = land_host(msg, n, user, count, dt, comm, &received);
     done = true;
+    if (msg == stage.p) {
+      stage_pool().put(stage);
+      stage = StagePool::Buf();
+    }
   }
   void lib_done(const MPI_Status &st) override {
     libStatus = st;
@@ -512,7 +568,7 @@ struct HostIrecvOp : Op {
     }
     int n = 0;
     MPI_Get_count(&st, MPI_BYTE, &n);
-    if (!inPlace) return deliver(stage.data(), n);
+    if (!inPlace) return deliver(stage.p, n);
     received = n;
     if (is_descriptor(user, n)) {
       alignas(16) char raw[kDescCap];
