@@ -12,11 +12,14 @@
 // type map.
 //
 // usage: mpiexec -n 1 mpi_pack ITERS [--host] [--factory NAME] [--min-target BYTES] [--max-target BYTES]
-//        one JSON object per point
+//                                   [--shape N:BL:STRIDE] [--pin]
+//        one JSON object per point. --shape times that one vector(N, BL, STRIDE) of MPI_BYTE at count 1
+//        (BASELINE config 1 is 1024:512:1024); --pin runs on one core (the first of the affinity mask).
 #include <hip/hip_runtime.h>
 #include <mpi.h>
 
 #include <algorithm>
+#include <sched.h>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -73,23 +76,49 @@ int main(int argc, char **argv) {
   const int iters = argc > 1 ? std::max(1, std::atoi(argv[1])) : 100;
   bool host = false;
   const char *only = nullptr;
+  bool shape = false;
+  int shapeN = 0, shapeBl = 0, shapeStride = 0;
   long minTarget = 0, maxTarget = 1L << 30;
   for (int i = 2; i < argc; ++i) {
     if (!std::strcmp(argv[i], "--host")) host = true;
     if (!std::strcmp(argv[i], "--max-target") && i + 1 < argc) maxTarget = std::atol(argv[++i]);
     if (!std::strcmp(argv[i], "--min-target") && i + 1 < argc) minTarget = std::atol(argv[++i]);
     if (!std::strcmp(argv[i], "--factory") && i + 1 < argc) only = argv[++i];
+    if (!std::strcmp(argv[i], "--shape") && i + 1 < argc) {
+      shape = true;
+      std::sscanf(argv[++i], "%d:%d:%d", &shapeN, &shapeBl, &shapeStride);
+    }
+    if (!std::strcmp(argv[i], "--pin")) {
+      cpu_set_t m;
+      if (sched_getaffinity(0, sizeof m, &m) == 0)
+        for (int c = 0; c < CPU_SETSIZE; ++c)
+          if (CPU_ISSET(c, &m)) {
+            cpu_set_t one;
+            CPU_ZERO(&one);
+            CPU_SET(c, &one);
+            sched_setaffinity(0, sizeof one, &one);
+            break;
+          }
+    }
   }
   struct Factory {
     const char *name;
     MPI_Datatype (*make)(int, int, int);
   };
   const Factory factories[] = {{"vector", make_vector}, {"hvector", make_hvector}, {"subarray", make_subarray}};
-  const int stride = 512;
   long errorsTotal = 0;
-  for (int target : {1024, 1024 * 1024, 4 * 1024 * 1024})
-    for (int count : {1, 2})
-      for (int bl : {1, 2, 4, 8, 32, 64, 128, 256, 512})
+  std::vector<int> targets = {1024, 1024 * 1024, 4 * 1024 * 1024}, counts = {1, 2},
+                   blocks = {1, 2, 4, 8, 32, 64, 128, 256, 512};
+  if (shape) {
+    targets = {shapeN * shapeBl};
+    counts = {1};
+    blocks = {shapeBl};
+    only = "vector";
+  }
+  const int stride = shape ? shapeStride : 512;
+  for (int target : targets)
+    for (int count : counts)
+      for (int bl : blocks)
         for (const Factory &f : factories) {
           if ((only && std::strcmp(only, f.name)) || target > maxTarget || target < minTarget) continue;
           const int n = target / bl;

@@ -72,11 +72,25 @@ def main():
     rc = L.tempi_bench_halo(a.iters, a.grid, a.grid, a.grid, 8, 3, 0, 0, 0 if torch else 1, buf, 4096)
     el = time.perf_counter() - t0
     c = mpi.counters()
+    # the library's own intra-node channel: a host-buffer ping-pong (shared
+    # memory runs 4 MiB at several GB/s, a socket channel far less)
+    L.tempi_bench_pingpong_1d.argtypes = [ctypes.c_int, ctypes.c_long, ctypes.c_int, ctypes.c_int, ctypes.c_char_p,
+                                          ctypes.c_int]
+    hostpp = {}
+    if mpi.Comm_size() >= 2:
+        os.environ["TEMPI_BENCH_HOST"] = "1"
+        for total in (8, 4 << 20):
+            pb = ctypes.create_string_buffer(1024)
+            L.tempi_bench_pingpong_1d(20, total, 0, 0, pb, 1024)
+            if rank == 0 and pb.value:
+                hostpp[str(total)] = json.loads(pb.value.decode()).get("oneway_us")
+        del os.environ["TEMPI_BENCH_HOST"]
     if rank == 0:
         r = json.loads(buf.value.decode()) if buf.value else {}
         print(json.dumps({"mode": a.mode, "launcher": "torchrun" if torchrun else "mpiexec", "rc": rc,
                           "us_per_iter": r.get("us_per_iter"), "us_min": r.get("us_min"),
                           "rank0_phase_us": r.get("rank0_us_per_iter"), "wall_s": round(el, 2),
+                          "host_pingpong_oneway_us": hostpp,
                           "counters": {k: v for k, v in c.items() if v}}), flush=True)
     mpi.Finalize()
     if torchrun:
