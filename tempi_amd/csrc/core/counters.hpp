@@ -43,6 +43,11 @@ struct Counters {
 
 extern Counters counters;
 extern bool kernelProfiling;
+// settle the kernel-profiling events still pending (interpose_core.cpp)
+void settle_kernel_times();
+void *timing_event(int device);
+void timed(int device, bool pack, void *ev0, void *ev1, bool ok);
+void destroy_timing_events();
 // the ns_* host timers run only when asked for (TEMPI_PRINT_COUNTERS or
 // TEMPI_HOST_TIMING): a clock read is ~20 ns, several per message
 extern bool hostTiming;

@@ -77,11 +77,15 @@ TEMPI_EXPORT void tempi_get_counters(tempi_counters_t *o) {
   o->sync_waits = c.sync_waits;
 }
 
-TEMPI_EXPORT void tempi_reset_counters(void) { counters = Counters(); }
+TEMPI_EXPORT void tempi_reset_counters(void) {
+  settle_kernel_times(); // (pending pairs belong to the counters being reset)
+  counters = Counters();
+}
 
 TEMPI_EXPORT void tempi_set_kernel_profiling(int on) { kernelProfiling = on != 0; }
 
 TEMPI_EXPORT void tempi_get_kernel_times(tempi_kernel_times *o) {
+  settle_kernel_times();
   o->pack_ms = counters.pack_kernel_ms;
   o->unpack_ms = counters.unpack_kernel_ms;
   o->packs = counters.pack_timed;

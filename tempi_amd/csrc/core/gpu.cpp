@@ -16,7 +16,6 @@ namespace {
 int nDevices = 0;
 std::mutex mtx;
 std::vector<void *> streams; // [device * kMaxLanes + lane]
-std::vector<void *> evStart, evStop;
 int nLanes = 3;
 bool highPriority = true; // TEMPI_NO_STREAM_PRIORITY
 // TEMPI_TEST_HOST_ONLY (CPU tests): with no GPU visible, TEMPI still takes the
@@ -53,11 +52,6 @@ void finalize() {
   for (void *s : streams)
     if (s) tempi_hip_stream_destroy(s);
   streams.clear();
-  for (auto *v : {&evStart, &evStop}) {
-    for (void *e : *v)
-      if (e) tempi_hip_event_destroy(e);
-    v->clear();
-  }
 }
 
 uint32_t identity(int device) {
@@ -109,22 +103,6 @@ void *stream(int device, int lane) {
     streams[i] = s;
   }
   return streams[i];
-}
-
-void profiling_events(int device, void **start, void **stop) {
-  *start = *stop = nullptr;
-  if (device < 0 || device >= nDevices) return;
-  std::lock_guard<std::mutex> g(mtx);
-  if (evStart.size() < size_t(nDevices)) {
-    evStart.resize(size_t(nDevices), nullptr);
-    evStop.resize(size_t(nDevices), nullptr);
-  }
-  if (!evStart[size_t(device)]) {
-    check(tempi_hip_event_create(&evStart[size_t(device)], 1), "event create");
-    check(tempi_hip_event_create(&evStop[size_t(device)], 1), "event create");
-  }
-  *start = evStart[size_t(device)];
-  *stop = evStop[size_t(device)];
 }
 
 void check(int status, const char *what) {

@@ -41,8 +41,6 @@ void *stream(int device, int lane = 0);
 int lanes();
 void choose_lanes(int ranksOnNode); // at MPI_Init, after topology::init
 
-// a timing event pair owned by TEMPI for `device` (created on first use)
-void profiling_events(int device, void **start, void **stop);
 
 // 32-bit identity of a device's physical GPU, equal in every process that
 // sees it (FNV-1a of its UUID); used to tell a peer on the same GPU from a
