@@ -69,7 +69,9 @@ def parse():
                    help="skip the 1 GiB points of the config-2 sweep in the default line (sweep_geomean)")
     p.add_argument("--no-measure-system", action="store_true",
                    help="N > 1: do not measure this node's perf.json when it is missing")
-    p.add_argument("--extras-deadline", type=float, default=900.0,
+    # 400 s: with a fresh box's first `import torch` (1-2 min) and the headline
+    # before it, the line is out well inside the driver's 600 s per run
+    p.add_argument("--extras-deadline", type=float, default=400.0,
                    help="seconds after the headline within which the line's other sections must finish; past it "
                         "rank 0 prints the line so far, marked incomplete, and every rank exits")
     p.add_argument("--inner", action="store_true", help=argparse.SUPPRESS)  # child for --traffic
