@@ -51,7 +51,7 @@ int main(int argc, char **argv) {
   CK(tempi_hip_malloc(&dst, 1 << 20));
   CK(tempi_hip_memset_async(src, 1, 2 << 20, s));
   CK(tempi_hip_stream_synchronize(s));
-  for (int n : {1024, 2}) {
+  for (int n : {2, 8, 32, 64, 128, 256, 512, 1024}) { // 1, 2, 8, 16, 32, 64, 128, 256 workgroups of the packer
     tempi_hip_desc d{};
     d.block = 512;
     d.ndims = 1;
@@ -92,9 +92,10 @@ int main(int argc, char **argv) {
     }
     std::printf("{\"shape\": \"vector(%d, 512, 1024)\", \"packed\": %d, \"reps\": %d, \"ptrinfo_us\": %.2f, "
                 "\"launch_us\": %.2f, \"sync_us\": %.2f, \"ticket_fold_us\": %.2f, \"ticket_kern_us\": %.2f, "
-                "\"fold_max_blocks\": \"%s\"}\n",
+                "\"fold_max_blocks\": \"%s\", \"dev_kernarg\": \"%s\"}\n",
                 n, n * 512, reps, median(pi), median(la), median(sy), median(tf), median(tk),
-                std::getenv("TEMPI_FOLD_MAX_BLOCKS") ? std::getenv("TEMPI_FOLD_MAX_BLOCKS") : "default");
+                std::getenv("TEMPI_FOLD_MAX_BLOCKS") ? std::getenv("TEMPI_FOLD_MAX_BLOCKS") : "default",
+                std::getenv("HIP_FORCE_DEV_KERNARG") ? std::getenv("HIP_FORCE_DEV_KERNARG") : "unset");
     std::fflush(stdout);
   }
   return 0;
