@@ -63,6 +63,7 @@ int collectiveDepth = 0;
 void init() {
   gpu::choose_lanes(topology::ranks_on_node());
   gpuAwareLibrary = std::getenv("TEMPI_MPI_GPU_AWARE") != nullptr;
+  modelForIsend = std::getenv("TEMPI_AUTO_MODEL_ISEND") != nullptr;
   directEnabled = std::getenv("TEMPI_NO_DIRECT") == nullptr;
   ipcSystemLoads = std::getenv("TEMPI_IPC_PLAIN_LOADS") == nullptr;
   hostRecvAware = std::getenv("TEMPI_NO_HOST_RECV") == nullptr;
@@ -180,7 +181,7 @@ int isend(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Co
   if (destWorld == state.worldRank) spill_channel(comm); // a message to this rank the self channel cannot carry
   const bool colocated = topology::colocated_world(destWorld);
   modelBlock = std::min<int64_t>(std::max<int64_t>(1, rec->desc.block), 512);
-  Method m = choose(bytes, colocated);
+  Method m = choose(bytes, colocated, blocking);
   if (force >= 0) m = Method(force);
   if (m == Method::IPC && (!colocated || ipc_broken(destWorld))) m = Method::ONESHOT;
   if (m == Method::DEVICE && !gpuAwareLibrary) m = colocated ? Method::IPC : Method::STAGED;

@@ -220,8 +220,10 @@ int64_t pack_size(int count, MPI_Datatype dt, MPI_Comm comm);
 // (homogeneous MPI_Pack_size adds no header), else the library's answer
 int64_t packed_bytes(const TypeRecord *rec, int count, MPI_Datatype dt, MPI_Comm comm);
 
-// the method for a message (TEMPI_DATATYPE_* or AUTO)
-Method choose(int64_t bytes, bool colocated);
+// the method for a message (TEMPI_DATATYPE_* or AUTO; AUTO prices only
+// blocking sends by the measured model, see p2p_routes.cpp)
+Method choose(int64_t bytes, bool colocated, bool blocking);
+extern bool modelForIsend; // TEMPI_AUTO_MODEL_ISEND
 void clear_model_cache();
 
 bool ipc_broken(int world);

@@ -135,7 +135,22 @@ bool model_choice(int64_t bytes, bool colocated, int64_t block, Method *out) {
 
 int64_t modelBlock = 512; // block length of the type being sent (set per call)
 
-Method choose(int64_t bytes, bool colocated) {
+// The measured model prices one message on its own: every term is a
+// synchronous call (a pack kernel launched and waited for, one ping-pong, an
+// unpack), as measure_system times them. Blocking sends are like that.
+// Non-blocking sends are not: their gathers and scatters share one launch per
+// burst and overlap, so what separates the methods is where the bytes travel
+// (HBM and xGMI for IPC, pinned host memory over the host link for ONESHOT),
+// not a kernel's latency. Priced per message, ONESHOT wins below ~1 MiB on
+// MI355X (a 28 us IPC ping-pong against 1 us on the CPU) and turned the 2-rank
+// 512^3 halo from 1.56-1.67 ms into 2.0-2.4 ms per iteration, on whichever
+// boxes the quick measurement put the crossover there (round 3,
+// profiles/r03/n2_variants_s4.jsonl). So non-blocking
+// sends keep the built-in policy; TEMPI_AUTO_MODEL_ISEND=1 prices them by the
+// model too (the reference's rule, async_operation.cpp:334-389).
+bool modelForIsend = false;
+
+Method choose(int64_t bytes, bool colocated, bool blocking) {
   switch (env.datatype) {
   case DatatypeMethod::ONESHOT:
     return Method::ONESHOT;
@@ -149,7 +164,7 @@ Method choose(int64_t bytes, bool colocated) {
   case DatatypeMethod::AUTO:
   default: {
     Method m;
-    if (model_choice(bytes, colocated, modelBlock, &m)) return m;
+    if ((blocking || modelForIsend) && model_choice(bytes, colocated, modelBlock, &m)) return m;
     if (colocated && bytes >= ipcMinBytes) return Method::IPC;
     return Method::ONESHOT;
   }

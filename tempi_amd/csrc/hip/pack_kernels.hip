@@ -814,17 +814,39 @@ int word_width(uintptr_t packed, uintptr_t first, const Norm &n) {
 #ifndef TEMPI_XCD_MAX_BLOCK
 #define TEMPI_XCD_MAX_BLOCK 1024
 #endif
-// TEMPI_XCD_GAPPED (A/B knob): also rows of whole 64-byte sectors with gaps
-// of >= 128 B between them
-#ifndef TEMPI_XCD_GAPPED
-#define TEMPI_XCD_GAPPED 0
+// Rows of whole 64-byte sectors that leave part of every 4 KiB page of the
+// strided side untouched (inner stride >= 4 KiB, rows < 4 KiB), and 64-byte
+// rows with gaps >= 128 B: in the dealt order the eight XCDs write one narrow
+// window at a time, whose addresses keep the same bits below 4 KiB, so only
+// part of the HBM channels take the writes; one contiguous range per XCD puts
+// eight far-apart windows in flight instead. Measured on MI355X (round 3,
+// profiles/r03/gap3_ab_s4.jsonl, 1 GiB, kernel time): unpack 512:4096 +33 %,
+// 1024:8192 +20 %, 1024:4096 +15 %, 3D 2048:4096 +14 %, 256:4096 +13 %,
+// 2048:8192 +12 %, 64:4096 +7 %, 64:512 +6 %; the same shapes' bare access
+// pattern (tools/calib.hip sect_copy, sect3_s4.jsonl) +5 to +41 %. Rows of
+// 4 KiB or more (whole pages: 4096:8192 -5 %), and strides below 4 KiB
+// (512:1024 -5 %, 128:256 -4 %), keep the dealt order.
+// TEMPI_XCD_PAGES=0 turns the rule off; TEMPI_XCD_PAGES_PACK=1 applies it to
+// gathers too (A/B).
+#ifndef TEMPI_XCD_PAGES
+#define TEMPI_XCD_PAGES 1
 #endif
-uint32_t xcd_flag(const char *first, const Norm &n) {
+#ifndef TEMPI_XCD_PAGES_PACK
+#define TEMPI_XCD_PAGES_PACK 0
+#endif
+bool partial_pages(const Norm &n) {
+  if (n.nd == 0 || n.block % 64) return false;
+  const int64_t inner = n.str[n.nd - 1];
+  if (inner < n.block) return false;
+  if (n.block == 64 && inner - n.block >= 128) return true;
+  return inner >= 4096 && n.block < 4096 && inner - n.block >= 128;
+}
+
+uint32_t xcd_flag(const char *first, const Norm &n, bool pack) {
   static const bool off = std::getenv("TEMPI_NO_XCD_MAP") != nullptr;
-  if (TEMPI_XCD_GAPPED && TEMPI_XCD_MAP && !off && n.nd > 0 && n.str[n.nd - 1] - n.block >= 128 &&
-      n.block % 64 == 0)
-    return kXcdRange;
-  if (!TEMPI_XCD_MAP || off || n.nd == 0 || n.block >= TEMPI_XCD_MAX_BLOCK) return 0;
+  if (!TEMPI_XCD_MAP || off) return 0;
+  if (TEMPI_XCD_PAGES && (!pack || TEMPI_XCD_PAGES_PACK) && partial_pages(n)) return kXcdRange;
+  if (pack || n.nd == 0 || n.block >= TEMPI_XCD_MAX_BLOCK) return 0;
   const int64_t inner = n.str[n.nd - 1];
   if (inner < n.block || inner - n.block >= 128) return 0;
   uint64_t g = reinterpret_cast<uintptr_t>(first) | uint64_t(n.block);
@@ -891,7 +913,7 @@ int launch_nd(bool pack, char *packed, char *first, const Norm &n, hipStream_t s
   uint32_t blocks;
   make_args<W, ND>(packed, first, n, &a, &blocks);
   if (blocks == 0) return 0;
-  if (!pack) a.flags |= xcd_flag(first, n);
+  a.flags |= xcd_flag(first, n, pack);
   const Sig sg = take_fold(blocks);
   if (pack)
     hipLaunchKernelGGL((pack_kernel<W, ND>), dim3(blocks), dim3(kBlock), 0, s, a, sg);
@@ -935,7 +957,7 @@ template <int W, int ND> int launch_batch_nd(bool pack, const std::vector<Job> &
     gItemFlags = j.flags;
     make_args<W, ND>(j.packed, j.first, j.n, &a, &blocks);
     gItemFlags = 0;
-    if (!pack) a.flags |= xcd_flag(j.first, j.n);
+    a.flags |= xcd_flag(j.first, j.n, pack);
     if (il) blocks = (a.nchunks + kBlock - 1) / kBlock;
     if (!blocks) continue;
     if (uint64_t(total) + blocks >= (uint64_t(1) << 31))
@@ -1017,7 +1039,7 @@ template <int W, int ND> int launch_il_nd(bool pack, char *packed, char *first, 
   make_args<W, ND>(packed, first, n, &a, &blocks);
   blocks = (a.nchunks + kBlock - 1) / kBlock; // one tile per workgroup, no grid-stride
   if (blocks == 0) return 0;
-  if (!pack) a.flags |= xcd_flag(first, n);
+  a.flags |= xcd_flag(first, n, pack);
   const Sig sg = take_fold(blocks);
   if (pack)
     hipLaunchKernelGGL((pack_il_kernel<W, ND>), dim3(blocks), dim3(kBlock), 0, s, a, sg);
@@ -1343,7 +1365,7 @@ bool plan_copy(void *dst, const void *src, const tempi_hip_desc *dd, const tempi
   if (!make_side(const_cast<char *>(static_cast<const char *>(src)), ns, w, &job->a.s)) return false;
   if (!make_side(static_cast<char *>(dst), nd, w, &job->a.d)) return false;
   job->a.nwords = uint32_t(bytes / w);
-  job->a.flags = xcd_flag(static_cast<char *>(dst), nd);
+  job->a.flags = xcd_flag(static_cast<char *>(dst), nd, false);
   job->a.s2 = job->a.d2 = nullptr;
   job->w = w;
   return true;

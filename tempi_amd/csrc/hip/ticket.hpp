@@ -21,10 +21,13 @@
 #include <mutex>
 
 // grids up to this many workgroups store their ticket themselves: each one
-// adds an agent-scope release (an L2 write-back) to its end, so a large grid
-// keeps the separate ticket kernel (tools/gpu_fold_ab.sh measures the cut)
+// adds a system-scope release (an L2 write-back) and an atomic to its end.
+// Measured on MI355X (tools/syncbench.cpp, profiles/r03/sync3_s4.jsonl,
+// per synchronous pack): folded 6.5 / 8.0 / 8.6 / 9.5 / 11.5 us at 1 / 8 /
+// 64 / 128 / 256 workgroups against 8.4 / 9.8 / 9.8 / 9.9 / 9.9 us with
+// the ticket kernel queued behind: the fold wins up to 128
 #ifndef TEMPI_FOLD_MAX_BLOCKS
-#define TEMPI_FOLD_MAX_BLOCKS 2048
+#define TEMPI_FOLD_MAX_BLOCKS 128
 #endif
 
 namespace tempi_ticket {

@@ -13,29 +13,29 @@ O=gpurun_out; mkdir -p $O
 OUT=$O/n2_variants.jsonl; : > $OUT; : > $O/n2_counters.txt
 PERF=$HOME/.tempi/perf.json
 P=29700
-tr() { P=$((P + 1)); timeout -k 10 240 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+trun() { P=$((P + 1)); timeout -k 10 240 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
          --master-addr 127.0.0.1 --master-port $P "$@"; }
 run() { # label cmd...
   local label=$1; shift
   echo "== $label"
   "$@" > $O/n2_run.out 2> $O/n2_run.err || { tail -5 $O/n2_run.err; exit 3; }
   grep '^{' $O/n2_run.out | tail -1 | sed "s/^{/{\"label\": \"$label\", /" >> $OUT
-  echo "$label: $(grep -h '\[tempi r' $O/n2_run.err | tr '\n' ' ')" >> $O/n2_counters.txt
+  echo "$label: $(grep -h '\[tempi r' $O/n2_run.err | paste -sd ' ')" >> $O/n2_counters.txt
   tail -n 1 $OUT | cut -c1-300
 }
 rm -f $PERF
-for rep in 1 2; do
+for rep in $(seq ${REPS:-2}); do
   run "mpiexec-app-nomodel" timeout -k 10 120 /opt/conda/bin/mpiexec -n 2 tempi_amd/lib/halo_exchange 10 512
-  run "torchrun-plain-nomodel" tr tools/halo_variant.py --mode plain
-  run "torchrun-headline-nomodel" tr tools/halo_variant.py --mode headline
+  run "torchrun-plain-nomodel" trun tools/halo_variant.py --mode plain
+  [ -n "$SHORT" ] || run "torchrun-headline-nomodel" trun tools/halo_variant.py --mode headline
 done
 mkdir -p $(dirname $PERF)
 echo "== measure_system --quick (as bench.py does at N > 1)"
 timeout -k 10 120 /opt/conda/bin/mpiexec -n 2 tempi_amd/lib/measure_system --quick --out $PERF > $O/n2_measure.log 2>&1 || exit 5
 cp $PERF $O/n2_perf.json
-for rep in 1 2; do
+for rep in $(seq ${REPS:-2}); do
   run "mpiexec-app-model" timeout -k 10 120 /opt/conda/bin/mpiexec -n 2 tempi_amd/lib/halo_exchange 10 512
-  run "torchrun-plain-model" tr tools/halo_variant.py --mode plain
+  run "torchrun-plain-model" trun tools/halo_variant.py --mode plain
 done
 echo "== bench torchrun N=2 (halo sections only, with the model)"
 P=$((P + 1))
