@@ -827,6 +827,26 @@ def _line_classes(bl, st, n, first):
 # one whole sector per line 7.5-7.6 TB/s of lines, lines with a partly
 # written sector 2.3-2.7 TB/s of lines: a DRAM read-modify-write)
 LINE_WRITE_WHOLE, LINE_WRITE_HALF, LINE_WRITE_PARTIAL = 128.0, 96.0, 292.0
+# A line with one whole 64-B sector written and the other untouched costs more
+# as such lines get sparser (fewer written sectors per DRAM page): the bare
+# pattern (tools/calib.hip sect_copy, 64-B rows at stride S, the kernel's tile
+# order) runs 5.25 / 4.63 / 4.27 / 4.00 / 3.96 TB/s (read + write) at S = 128
+# / 256 / 512 / 1024 / 4096 (round 3, profiles/r03/sect3_s4.jsonl), i.e.
+# 90 / 110 / 125 / 138 / 140 bytes-equivalent per line at 6.3 TB/s
+HALF_LINE_COST = ((128, 90.0), (256, 110.0), (512, 125.0), (1024, 138.0), (4096, 140.0))
+
+
+def half_line_cost(stride):
+    """bytes-equivalent of a line written in one whole sector, rows `stride`
+    bytes apart (log-linear between the calibrated strides, clamped)"""
+    pts = HALF_LINE_COST
+    if stride <= pts[0][0]:
+        return pts[0][1]
+    for (s0, c0), (s1, c1) in zip(pts, pts[1:]):
+        if stride <= s1:
+            f = (math.log(stride) - math.log(s0)) / (math.log(s1) - math.log(s0))
+            return c0 + f * (c1 - c0)
+    return pts[-1][1]
 
 
 def touched_model(bl, st, nplanes, rows, plane_stride, first):
@@ -841,7 +861,7 @@ def touched_model(bl, st, nplanes, rows, plane_stride, first):
     payload = nplanes * rows * bl
     touched, partial, whole, half = _line_classes(bl, st, rows, first)
     return {"pack_bytes": nplanes * touched * 128.0 + payload,
-            "unpack_bytes": payload + nplanes * (whole * LINE_WRITE_WHOLE + half * LINE_WRITE_HALF +
+            "unpack_bytes": payload + nplanes * (whole * LINE_WRITE_WHOLE + half * half_line_cost(st) +
                                                  partial * LINE_WRITE_PARTIAL)}
 
 
@@ -973,9 +993,9 @@ def sweep_geomean(args, mpi, torch, dev):
                                "pack_frac_touched": round(r["pack_frac_touched"], 3),
                                "unpack_frac_touched": round(r["unpack_frac_touched"], 3)} for r in worst_t],
             "touched_model": ("pack: 128-B lines touched on the strided side + packed bytes; unpack: packed bytes + "
-                              "each strided-side line at its calibrated write cost (whole 128, one whole sector 96, "
-                              "a partly written sector 292 bytes-equivalent: DRAM read-modify-write), all at 6.3 TB/s; "
-                              "profiles/r02/counter_calibration.txt"),
+                              "each strided-side line at its calibrated write cost (whole 128, one whole sector 90-140 "
+                              "by row stride, a partly written sector 292 bytes-equivalent: DRAM read-modify-write), "
+                              "all at 6.3 TB/s; profiles/r02/counter_calibration.txt, profiles/r03/sect3_s4.jsonl"),
             "workload": "config 2 at 1 GiB packed: MPI_Type_create_subarray 2D {rows, S} and 3D {z+2, y+3, S}, "
                         "block 1 B - 4 KiB, S in {2*bl, bl+16, 512 (bl <= 256)}; kernel time per MPI_Pack / "
                         "MPI_Unpack from HIP events on TEMPI's stream"}

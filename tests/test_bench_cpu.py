@@ -127,9 +127,12 @@ def test_touched_model_headline_and_narrow_rows():
     lines = (1 << 31) // 128
     assert m["pack_bytes"] == pytest.approx(lines * 128 + (1 << 30))
     assert m["unpack_bytes"] == pytest.approx((1 << 30) + lines * bench.LINE_WRITE_PARTIAL)
-    # 64 : 512: one whole sector per touched line
+    # 64 : 512: one whole sector per touched line, at the calibrated cost of that sparsity
     m = bench.touched_model(64, 512, 1, 1 << 24, 0, 0)
-    assert m["unpack_bytes"] == pytest.approx((1 << 30) + (1 << 24) * bench.LINE_WRITE_HALF)
+    assert m["unpack_bytes"] == pytest.approx((1 << 30) + (1 << 24) * 125.0)
+    # the half-line cost rises with the stride and stays within the calibration
+    costs = [bench.half_line_cost(s) for s in (64, 128, 192, 256, 512, 1024, 4096, 65536)]
+    assert costs == sorted(costs) and costs[0] == 90.0 and costs[-1] == 140.0
 
 
 def test_type_commit_cost_section():
