@@ -153,23 +153,32 @@ __device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t n, uint32_t fl
 }
 
 // The end of a workgroup of a launch that stores its own completion ticket
-// (ticket.hpp): every wave waits for its memory operations to be acknowledged,
-// then one lane per workgroup releases them as it counts the workgroup, and
-// the workgroup that completes the count stores the ticket for the host. The
-// release is system scope (an L2 write-back of this XCD; the XCD L2s are not
-// coherent with each other): the interposer takes a ticket only when the
-// kernel writes device memory or TEMPI's coherent slabs, but a process with
-// two HIP runtimes sees the other runtime's pinned host memory as device
-// memory, and host-visible must hold for that too.
+// (ticket.hpp): every wave waits until its stores are acknowledged, then one
+// lane per workgroup counts the workgroup, and the workgroup that completes
+// the count stores the ticket for the host. A workgroup whose stores went
+// through the L2 write-back (`fence`) first releases them at system scope (an
+// L2 write-back of this XCD; the XCD L2s are not coherent with each other):
+// the interposer takes a ticket only when the kernel writes device memory or
+// TEMPI's coherent slabs, but a process with two HIP runtimes sees the other
+// runtime's pinned host memory as device memory, and host-visible
+// must hold for that too. A workgroup whose stores were all write-through
+// (kWriteThrough: sc0 sc1, acknowledged once out of L2) needs no release.
+// The waits are inline asm: ROCm 7.2 may drop its own wait after the release's
+// write-back when it can prove the wave's counters empty, and the count would
+// then overtake the write-back (MI355X_MICROARCH.md, "Compiler hazard").
 // sg.flag == nullptr (uniform): nothing to do.
 using tempi_ticket::Sig;
-__device__ __forceinline__ void wg_signal(const Sig &sg) {
+__device__ __forceinline__ void wg_signal(const Sig &sg, bool fence) {
   if (!sg.flag) return;
-  __builtin_amdgcn_s_waitcnt(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    const uint32_t old = __hip_atomic_fetch_add(sg.counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
-    if (old + 1u == sg.target) __hip_atomic_store(sg.flag, sg.ticket, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (fence) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    const uint32_t old = __hip_atomic_fetch_add(sg.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (old + 1u == sg.target) __hip_atomic_store(sg.flag, sg.ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -264,6 +273,26 @@ template <typename T> __device__ __forceinline__ T ld_remote(const T *p) {
 template <typename T, int ND> __device__ __forceinline__ T ld_packed(const KArgs<ND> &a, const T *p, bool nt) {
   if (a.flags & TEMPI_HIP_ITEM_REMOTE) return ld_remote(p);
   return ld(p, nt);
+}
+
+// A gather whose completion ticket is folded into it (wg_signal) stores its
+// 16-byte packed chunks write-through (sc0 sc1: the line leaves L2 as it is
+// written, at the plain store's rate), so that only the workgroups holding the
+// object's partial first / last chunk, stored word by word, release L2 at the
+// end. The store's buffer base is the wave's first active lane, whose chunk is
+// the lowest (chunks ascend with the lane). Internal flag bit, never a
+// TEMPI_HIP_ITEM_*.
+constexpr uint32_t kWriteThrough = 1u << 30;
+__device__ __forceinline__ void st_packed(uint32_t flags, uint4 *p, const uint4 &v) {
+  if (flags & kWriteThrough) {
+    uint32_t off;
+    const __amdgpu_buffer_rsrc_t r = remote_rsrc(p, &off);
+    u32x4 x;
+    __builtin_memcpy(&x, &v, 16);
+    __builtin_amdgcn_raw_buffer_store_b128(x, r, int(off), 0, kSysScope);
+  } else {
+    st(p, v, kNtPacked);
+  }
 }
 
 // row index -> byte offset of the row, plus the odometer digits
@@ -409,7 +438,7 @@ __device__ __forceinline__ void pack_body(const KArgs<ND> &a, uint32_t blk, uint
     for (int u = 0; u < U; ++u) {
       const uint32_t c = base + u * kBlock + threadIdx.x;
       if (full[u]) {
-        st(reinterpret_cast<uint4 *>(a.chunk0 + size_t(c) * 16), buf[u].v, kNtPacked);
+        st_packed(a.flags, reinterpret_cast<uint4 *>(a.chunk0 + size_t(c) * 16), buf[u].v);
       } else if (c < a.nchunks) {
         partial_chunk<W, ND, true>(c, a);
       }
@@ -472,16 +501,24 @@ __device__ __forceinline__ void unpack_body(const KArgs<ND> &a, uint32_t blk, ui
   }
 }
 
+// a workgroup of a write-through gather that still needs the release: the
+// first and last tiles hold the object's partial chunks (folded launches never
+// grid-stride: at most TEMPI_FOLD_MAX_BLOCKS_WT workgroups, one tile each)
+__device__ __forceinline__ bool needs_release(uint32_t flags, uint32_t tile) {
+  return !(flags & kWriteThrough) || tile == 0 || tile + 1 == gridDim.x;
+}
+
 template <int W, int ND>
 __global__ __launch_bounds__(kBlock) void pack_kernel(const KArgs<ND> a, const Sig sg) {
-  pack_body<W, ND>(a, xcd_tile(blockIdx.x, gridDim.x, a.flags), gridDim.x);
-  wg_signal(sg);
+  const uint32_t tile = xcd_tile(blockIdx.x, gridDim.x, a.flags);
+  pack_body<W, ND>(a, tile, gridDim.x);
+  wg_signal(sg, needs_release(a.flags, tile));
 }
 
 template <int W, int ND>
 __global__ __launch_bounds__(kBlock) void unpack_kernel(const KArgs<ND> a, const Sig sg) {
   unpack_body<W, ND>(a, xcd_tile(blockIdx.x, gridDim.x, a.flags), gridDim.x);
-  wg_signal(sg);
+  wg_signal(sg, true);
 }
 
 // ------------------------------------------- wave-interleaved scatter (unpack)
@@ -589,16 +626,17 @@ __device__ __forceinline__ void pack_il_tile(const KArgs<ND> &a, uint32_t tileId
 #pragma unroll
   for (int j = 0; j < CW; ++j) dst[uint32_t(j) * 64 + lane] = v[j];
   __syncthreads();
-  st(reinterpret_cast<uint4 *>(a.chunk0 + size_t(c0 + threadIdx.x) * 16), tile[threadIdx.x], kNtPacked);
+  st_packed(a.flags, reinterpret_cast<uint4 *>(a.chunk0 + size_t(c0 + threadIdx.x) * 16), tile[threadIdx.x]);
 }
 
 template <int W, int ND> __global__ __launch_bounds__(kBlock) void pack_il_kernel(const KArgs<ND> a, const Sig sg) {
-  pack_il_tile<W, ND>(a, xcd_tile(blockIdx.x, gridDim.x, a.flags), gridDim.x);
-  wg_signal(sg);
+  const uint32_t tile = xcd_tile(blockIdx.x, gridDim.x, a.flags);
+  pack_il_tile<W, ND>(a, tile, gridDim.x);
+  wg_signal(sg, needs_release(a.flags, tile));
 }
 template <int W, int ND> __global__ __launch_bounds__(kBlock) void unpack_il_kernel(const KArgs<ND> a, const Sig sg) {
   unpack_il_tile<W, ND>(a, xcd_tile(blockIdx.x, gridDim.x, a.flags), gridDim.x);
-  wg_signal(sg);
+  wg_signal(sg, true);
 }
 
 // ------------------------------------------------- dense-window gather (pack)
@@ -674,7 +712,7 @@ __device__ __forceinline__ void pack_dense_tile(const KArgs<ND> &a, uint32_t blk
         ++idx;
       }
     }
-    st(reinterpret_cast<uint4 *>(a.chunk0 + size_t(c) * 16), out.v, kNtPacked);
+    st_packed(a.flags, reinterpret_cast<uint4 *>(a.chunk0 + size_t(c) * 16), out.v);
   } else { // first / last chunk of the object: only its bytes
     for (int j = 0; j < 16; ++j) {
       const int64_t q = q0 + j;
@@ -688,8 +726,9 @@ __device__ __forceinline__ void pack_dense_tile(const KArgs<ND> &a, uint32_t blk
 
 template <int ND>
 __global__ __launch_bounds__(kBlock) void pack_dense_kernel(const KArgs<ND> a, const Sig sg) {
-  pack_dense_tile<ND>(a, xcd_tile(blockIdx.x, gridDim.x, a.flags));
-  wg_signal(sg);
+  const uint32_t tile = xcd_tile(blockIdx.x, gridDim.x, a.flags);
+  pack_dense_tile<ND>(a, tile);
+  wg_signal(sg, needs_release(a.flags, tile));
 }
 
 // Many objects in ONE launch (e.g. the 26 x nQuants faces of a halo step):
@@ -865,10 +904,12 @@ thread_local tempi_ticket::Fold *gFold = nullptr;
 // the kernel's Sig for a launch of `blocks` workgroups: the fold when one is
 // offered and the grid is small enough (counted on the host as the kernel
 // will count on the device), else none
-Sig take_fold(uint32_t blocks) {
+Sig take_fold(uint32_t blocks, bool writeThrough) {
   Sig sg{nullptr, nullptr, 0, 0};
   tempi_ticket::Fold *f = gFold;
-  if (!f || f->taken || !f->t || !f->t->counter || blocks == 0 || blocks > f->max_blocks) return sg;
+  if (!f || f->taken || !f->t || !f->t->counter || blocks == 0 ||
+      blocks > (writeThrough ? f->max_blocks_wt : f->max_blocks))
+    return sg;
   f->t->counted += blocks;
   f->taken = true;
   sg.counter = f->t->counter;
@@ -914,7 +955,8 @@ int launch_nd(bool pack, char *packed, char *first, const Norm &n, hipStream_t s
   make_args<W, ND>(packed, first, n, &a, &blocks);
   if (blocks == 0) return 0;
   a.flags |= xcd_flag(first, n, pack);
-  const Sig sg = take_fold(blocks);
+  const Sig sg = take_fold(blocks, pack);
+  if (sg.flag && pack) a.flags |= kWriteThrough;
   if (pack)
     hipLaunchKernelGGL((pack_kernel<W, ND>), dim3(blocks), dim3(kBlock), 0, s, a, sg);
   else
@@ -1017,7 +1059,8 @@ template <int ND> int launch_dense_nd(char *packed, char *first, const Norm &n, 
   uint32_t blocks;
   make_args<1, ND>(packed, first, n, &a, &blocks);
   if (blocks == 0) return 0;
-  const Sig sg = take_fold(blocks);
+  const Sig sg = take_fold(blocks, true);
+  if (sg.flag) a.flags |= kWriteThrough;
   hipLaunchKernelGGL((pack_dense_kernel<ND>), dim3(blocks), dim3(kBlock), 0, s, a, sg);
   return int(hipGetLastError());
 }
@@ -1040,7 +1083,8 @@ template <int W, int ND> int launch_il_nd(bool pack, char *packed, char *first, 
   blocks = (a.nchunks + kBlock - 1) / kBlock; // one tile per workgroup, no grid-stride
   if (blocks == 0) return 0;
   a.flags |= xcd_flag(first, n, pack);
-  const Sig sg = take_fold(blocks);
+  const Sig sg = take_fold(blocks, pack);
+  if (sg.flag && pack) a.flags |= kWriteThrough;
   if (pack)
     hipLaunchKernelGGL((pack_il_kernel<W, ND>), dim3(blocks), dim3(kBlock), 0, s, a, sg);
   else
@@ -1514,6 +1558,7 @@ int with_ticket(bool pack, char *packed, char *first, const tempi_hip_desc *d, h
   fold.t = t;
   fold.ticket = ++t->next;
   fold.max_blocks = single ? tempi_ticket::fold_max_blocks() : 0;
+  fold.max_blocks_wt = single ? tempi_ticket::fold_max_blocks_wt() : 0;
   gFold = &fold;
   const int e = launch_split(pack, packed, first, n, s);
   gFold = nullptr;

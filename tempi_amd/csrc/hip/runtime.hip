@@ -196,6 +196,14 @@ uint32_t fold_max_blocks() {
   return v;
 }
 
+uint32_t fold_max_blocks_wt() {
+  static const uint32_t v = [] {
+    const char *e = std::getenv("TEMPI_FOLD_MAX_BLOCKS_WT");
+    return e ? uint32_t(std::strtoul(e, nullptr, 10)) : uint32_t(TEMPI_FOLD_MAX_BLOCKS_WT);
+  }();
+  return v;
+}
+
 } // namespace tempi_ticket
 
 extern "C" {

@@ -29,6 +29,14 @@
 #ifndef TEMPI_FOLD_MAX_BLOCKS
 #define TEMPI_FOLD_MAX_BLOCKS 128
 #endif
+// gathers write their packed chunks write-through (sc0 sc1 stores leave L2 as
+// they are written), so only the workgroups holding the object's partial
+// first / last chunk write back L2 before counting themselves; the fold then
+// costs each workgroup one atomic (MI355X_MICROARCH.md "publish-large":
+// write-through + a drained flag beats a release per workgroup)
+#ifndef TEMPI_FOLD_MAX_BLOCKS_WT
+#define TEMPI_FOLD_MAX_BLOCKS_WT 2048
+#endif
 
 namespace tempi_ticket {
 
@@ -52,7 +60,8 @@ Stats &stats(); // (caller holds mutex())
 struct Fold {
   Ticket *t = nullptr;
   uint32_t ticket = 0;
-  uint32_t max_blocks = 0;
+  uint32_t max_blocks = 0;    // launches whose stores go through L2 write-back
+  uint32_t max_blocks_wt = 0; // launches that store write-through (gathers)
   bool taken = false;
 };
 
@@ -75,5 +84,7 @@ hipError_t queue_kernel(Ticket &t, hipStream_t s, uint32_t ticket);
 int wait(hipStream_t s, const uint32_t *flag, uint32_t ticket);
 // largest grid a work kernel takes a fold for (TEMPI_FOLD_MAX_BLOCKS, 0 = never)
 uint32_t fold_max_blocks();
+// the same for launches whose work is stored write-through (TEMPI_FOLD_MAX_BLOCKS_WT)
+uint32_t fold_max_blocks_wt();
 
 } // namespace tempi_ticket
