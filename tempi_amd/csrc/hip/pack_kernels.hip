@@ -177,8 +177,15 @@ __device__ __forceinline__ void wg_signal(const Sig &sg, bool fence) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    const uint32_t old = __hip_atomic_fetch_add(sg.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    if (old + 1u == sg.target) __hip_atomic_store(sg.flag, sg.ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    using namespace tempi_ticket;
+    const uint32_t k = blockIdx.x % kShards;
+    const uint32_t old = __hip_atomic_fetch_add(sg.counter + k * kCounterStride, 1u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_SYSTEM);
+    if (old + 1u == sg.target[k]) { // the last workgroup of its shard
+      const uint32_t top = __hip_atomic_fetch_add(sg.counter + kShards * kCounterStride, 1u, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_SYSTEM);
+      if (top + 1u == sg.top) __hip_atomic_store(sg.flag, sg.ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
   }
 }
 
@@ -905,16 +912,22 @@ thread_local tempi_ticket::Fold *gFold = nullptr;
 // offered and the grid is small enough (counted on the host as the kernel
 // will count on the device), else none
 Sig take_fold(uint32_t blocks, bool writeThrough) {
-  Sig sg{nullptr, nullptr, 0, 0};
+  using tempi_ticket::kShards;
+  Sig sg{};
   tempi_ticket::Fold *f = gFold;
   if (!f || f->taken || !f->t || !f->t->counter || blocks == 0 ||
       blocks > (writeThrough ? f->max_blocks_wt : f->max_blocks))
     return sg;
-  f->t->counted += blocks;
+  uint32_t *counted = f->t->counted;
+  for (uint32_t k = 0; k < uint32_t(kShards); ++k) { // workgroups b with b % kShards == k
+    if (blocks > k) counted[k] += (blocks - k + kShards - 1) / kShards;
+    sg.target[k] = counted[k];
+  }
+  counted[kShards] += blocks < uint32_t(kShards) ? blocks : uint32_t(kShards); // shards that get a workgroup
+  sg.top = counted[kShards];
   f->taken = true;
   sg.counter = f->t->counter;
   sg.flag = f->t->dev;
-  sg.target = f->t->counted;
   sg.ticket = f->ticket;
   return sg;
 }

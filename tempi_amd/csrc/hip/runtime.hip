@@ -153,18 +153,19 @@ Ticket *of(hipStream_t s) {
     __atomic_store_n(t.host, 0u, __ATOMIC_RELEASE);
   }
   if (!t.counter || t.broken) { // (re)start the workgroup count at 0 once the stream is idle
-    if (!t.counter && hipMalloc(reinterpret_cast<void **>(&t.counter), 64) != hipSuccess) {
+    if (!t.counter && hipMalloc(reinterpret_cast<void **>(&t.counter), kCounterWords * sizeof(uint32_t)) != hipSuccess) {
       (void)hipGetLastError();
       t.counter = nullptr;
       return &t; // tickets work; folds are refused (no counter)
     }
-    if (hipStreamSynchronize(s) != hipSuccess || hipMemsetAsync(t.counter, 0, 64, s) != hipSuccess ||
+    if (hipStreamSynchronize(s) != hipSuccess ||
+        hipMemsetAsync(t.counter, 0, kCounterWords * sizeof(uint32_t), s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess) {
       (void)hipGetLastError();
       t.broken = true;
       return &t;
     }
-    t.counted = 0;
+    for (uint32_t &c : t.counted) c = 0;
     t.broken = false;
   }
   return &t;

@@ -40,12 +40,22 @@
 
 namespace tempi_ticket {
 
+// The workgroup count is sharded: workgroup b counts itself on shard b % 8,
+// the workgroup completing a shard counts the shard on the top counter, and
+// the one completing the top stores the ticket. One counter took every
+// workgroup's system-scope atomic in turn (256 of them added ~2.2 us to a
+// 256-workgroup call, profiles/r03/sync3_s6.jsonl); eight take them at once.
+// Each counter has a 128-byte line of its own.
+constexpr int kShards = 8;
+constexpr int kCounterStride = 32; // uint32 words between counters (128 B)
+constexpr int kCounterWords = (kShards + 1) * kCounterStride;
+
 struct Ticket {
   uint32_t *host = nullptr, *dev = nullptr; // the flag (pinned, coherent)
   uint32_t next = 0;                        // last ticket issued
-  uint32_t *counter = nullptr;              // device: workgroups of folded launches counted so far
-  uint32_t counted = 0;                     // the host's running total of the same (mod 2^32)
-  bool broken = false;                      // a folded launch failed: counter and total disagree
+  uint32_t *counter = nullptr;              // device: kShards shard counters + the top counter
+  uint32_t counted[kShards + 1] = {};       // the host's running totals of the same (mod 2^32)
+  bool broken = false;                      // a folded launch failed: counters and totals disagree
 };
 
 // tickets stored by work kernels / by the ticket kernel, all streams
@@ -69,7 +79,8 @@ struct Fold {
 struct Sig {
   uint32_t *counter;
   uint32_t *flag;
-  uint32_t target; // counter value once this launch's last workgroup counts itself
+  uint32_t target[kShards]; // each shard's count once this launch's workgroups of that shard have counted
+  uint32_t top;             // the top counter's value once this launch's last shard completes
   uint32_t ticket;
 };
 

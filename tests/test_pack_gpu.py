@@ -632,11 +632,18 @@ def _ticket_stats():
     return f.value, q.value
 
 
-@pytest.mark.parametrize("rows,block,stride", [(1024, 512, 1024),     # config 1: 256 workgroups, folded
-                                               (4096, 24, 4608),      # halo x-face rows (interleaved unpack)
-                                               (20000, 3, 7),         # dense-window gather (1-byte words)
-                                               (16384, 512, 1024)])   # 8 MiB: 4096 workgroups, ticket kernel
-def test_synchronous_ticket_visible_device_wide(mpi, gpu, rows, block, stride):
+# (pack, unpack) calls whose ticket the work kernel stores itself: gathers
+# (write-through) fold up to TEMPI_FOLD_MAX_BLOCKS_WT = 2048 workgroups,
+# scatters up to TEMPI_FOLD_MAX_BLOCKS = 128 (hip/ticket.hpp)
+@pytest.mark.parametrize("rows,block,stride,folds", [
+    (1024, 512, 1024, (60, 0)),   # config 1: 256 workgroups, gather folded, scatter ticket kernel
+    (4096, 24, 4608, (60, 60)),   # halo x-face rows (interleaved unpack), 24 / 48 workgroups
+    (20000, 3, 7, (60, 60)),      # dense-window gather (1-byte words), 30 workgroups
+    (64, 512, 1024, (60, 60)),    # 32 KiB: 16 workgroups
+    (2, 512, 1024, (60, 60)),     # one workgroup: one shard, the top counted once
+    (100, 500, 1000, (60, 60)),   # 4-byte words, 13 / 25 workgroups: shards of unequal counts
+    (16384, 512, 1024, (0, 0))])  # 8 MiB: 4096 workgroups, ticket kernel both ways
+def test_synchronous_ticket_visible_device_wide(mpi, gpu, rows, block, stride, folds):
     """Synchronous MPI_Pack / MPI_Unpack between device buffers complete by a
     ticket -- stored by the work kernel's last workgroup for small grids
     (VERDICT r02 next 5), by the ticket kernel behind larger ones. Right
@@ -665,10 +672,7 @@ def test_synchronous_ticket_visible_device_wide(mpi, gpu, rows, block, stride):
             assert torch.equal(back[idx.reshape(-1)], exp), f"round {r}: unpacked bytes not visible"
         c1, f1 = mpi.counters(), _ticket_stats()
         assert c1["ticket_waits"] - c0["ticket_waits"] == 120 and c1["sync_waits"] == c0["sync_waits"]
-        if rows * block <= 4096 * 512:  # at most 2048 workgroups: every ticket folded into the work kernel
-            assert f1[0] - f0[0] == 120 and f1[1] == f0[1]
-        else:
-            assert f1[1] - f0[1] == 120
+        assert f1[0] - f0[0] == sum(folds) and f1[1] - f0[1] == 120 - sum(folds)
     finally:
         mpi.Type_free(t)
 
