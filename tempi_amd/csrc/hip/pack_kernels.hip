@@ -302,6 +302,21 @@ __device__ __forceinline__ void st_packed(uint32_t flags, uint4 *p, const uint4 
   }
 }
 
+// the scatter's store of one strided-side word: write-through for 16-byte
+// words of a folded launch (the host sets kWriteThrough only when every
+// stride is >= 0 and the object spans < 2 GiB, so a wave's addresses ascend
+// with the lane from its first active lane and fit the buffer offset)
+template <int W> __device__ __forceinline__ void st_scatter(uint32_t flags, typename Word<W>::T *p,
+                                                            const typename Word<W>::T &v) {
+  if constexpr (W == 16) {
+    if (flags & kWriteThrough) {
+      st_packed(flags, p, v);
+      return;
+    }
+  }
+  st(p, v, NtScatter<W>::value);
+}
+
 // row index -> byte offset of the row, plus the odometer digits
 template <int ND>
 __device__ __forceinline__ int64_t row_offset(uint32_t row, const KArgs<ND> &a,
@@ -485,7 +500,7 @@ __device__ __forceinline__ void unpack_body(const KArgs<ND> &a, uint32_t blk, ui
         if (CW == 1 || (CW <= 8 && one_run<ND>(row, mdiv(q + (CW - 1), a.mwpr), dig, a))) {
 #pragma unroll
           for (int j = 0; j < CW; ++j) {
-            st(reinterpret_cast<WT *>(a.strided + off + int64_t(w) * W), buf[u].w[j], NtScatter<W>::value);
+            st_scatter<W>(a.flags, reinterpret_cast<WT *>(a.strided + off + int64_t(w) * W), buf[u].w[j]);
             if (j + 1 < CW && ++w == a.wpr) {
               w = 0;
               if constexpr (ND >= 1) off += a.stride[0];
@@ -494,7 +509,7 @@ __device__ __forceinline__ void unpack_body(const KArgs<ND> &a, uint32_t blk, ui
         } else {
 #pragma unroll
           for (int j = 0; j < CW; ++j) {
-            st(reinterpret_cast<WT *>(a.strided + off + int64_t(w) * W), buf[u].w[j], NtScatter<W>::value);
+            st_scatter<W>(a.flags, reinterpret_cast<WT *>(a.strided + off + int64_t(w) * W), buf[u].w[j]);
             if (j + 1 < CW && ++w == a.wpr) {
               w = 0;
               next_row<ND>(off, dig, a);
@@ -524,8 +539,9 @@ __global__ __launch_bounds__(kBlock) void pack_kernel(const KArgs<ND> a, const S
 
 template <int W, int ND>
 __global__ __launch_bounds__(kBlock) void unpack_kernel(const KArgs<ND> a, const Sig sg) {
-  unpack_body<W, ND>(a, xcd_tile(blockIdx.x, gridDim.x, a.flags), gridDim.x);
-  wg_signal(sg, true);
+  const uint32_t tile = xcd_tile(blockIdx.x, gridDim.x, a.flags);
+  unpack_body<W, ND>(a, tile, gridDim.x);
+  wg_signal(sg, needs_release(a.flags, tile));
 }
 
 // ------------------------------------------- wave-interleaved scatter (unpack)
@@ -908,6 +924,17 @@ thread_local uint32_t gItemFlags = 0;
 // launch (the *_ticket entry points set it around their launch)
 thread_local tempi_ticket::Fold *gFold = nullptr;
 
+// a 16-byte-word scatter may store write-through (st_scatter): every stride
+// >= 0 and the object's span below 2 GiB
+bool scatter_write_through(const Norm &n) {
+  int64_t span = n.block;
+  for (int k = 0; k < n.nd; ++k) {
+    if (n.str[k] < 0) return false;
+    span += (n.cnt[k] - 1) * n.str[k];
+  }
+  return span < (int64_t(1) << 31);
+}
+
 // the kernel's Sig for a launch of `blocks` workgroups: the fold when one is
 // offered and the grid is small enough (counted on the host as the kernel
 // will count on the device), else none
@@ -968,8 +995,9 @@ int launch_nd(bool pack, char *packed, char *first, const Norm &n, hipStream_t s
   make_args<W, ND>(packed, first, n, &a, &blocks);
   if (blocks == 0) return 0;
   a.flags |= xcd_flag(first, n, pack);
-  const Sig sg = take_fold(blocks, pack);
-  if (sg.flag && pack) a.flags |= kWriteThrough;
+  const bool wt = pack || (W == 16 && scatter_write_through(n));
+  const Sig sg = take_fold(blocks, wt);
+  if (sg.flag && wt) a.flags |= kWriteThrough;
   if (pack)
     hipLaunchKernelGGL((pack_kernel<W, ND>), dim3(blocks), dim3(kBlock), 0, s, a, sg);
   else

@@ -633,10 +633,12 @@ def _ticket_stats():
 
 
 # (pack, unpack) calls whose ticket the work kernel stores itself: gathers
-# (write-through) fold up to TEMPI_FOLD_MAX_BLOCKS_WT = 2048 workgroups,
-# scatters up to TEMPI_FOLD_MAX_BLOCKS = 128 (hip/ticket.hpp)
+# and 16-byte-word scatters (write-through) fold up to
+# TEMPI_FOLD_MAX_BLOCKS_WT = 2048 workgroups, other scatters up to
+# TEMPI_FOLD_MAX_BLOCKS = 128 (hip/ticket.hpp)
 @pytest.mark.parametrize("rows,block,stride,folds", [
-    (1024, 512, 1024, (60, 0)),   # config 1: 256 workgroups, gather folded, scatter ticket kernel
+    (1024, 512, 1024, (60, 60)),  # config 1: 256 workgroups, both folded (16-byte words)
+    (300, 512, 1024, (60, 60)),   # 75 workgroups, 16-byte words, not a multiple of the 8 shards
     (4096, 24, 4608, (60, 60)),   # halo x-face rows (interleaved unpack), 24 / 48 workgroups
     (20000, 3, 7, (60, 60)),      # dense-window gather (1-byte words), 30 workgroups
     (64, 512, 1024, (60, 60)),    # 32 KiB: 16 workgroups
