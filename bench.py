@@ -1211,10 +1211,14 @@ class Sections:
 
     def run(self, name, fn, *a, **kw):
         self.current = name
+        t0 = time.perf_counter()
         try:
             return fn(*a, **kw)
         except Exception as e:
             return {"error": f"{type(e).__name__}: {e}"}
+        finally:  # progress on stderr (a long multi-rank run is never silent for minutes)
+            if self.rank == 0:
+                print(f"[bench] {name}: {time.perf_counter() - t0:.1f} s", file=sys.stderr, flush=True)
 
     def done(self):
         self.timer.cancel()
