@@ -104,6 +104,18 @@ int tempi_hip_pack_ticket(void *packed, const void *first, const tempi_hip_desc 
                           const uint32_t **flag, uint32_t *ticket);
 int tempi_hip_unpack_ticket(void *first, const void *packed, const tempi_hip_desc *d, void *stream,
                             const uint32_t **flag, uint32_t *ticket);
+/* the batched forms with a ticket folded into the batch's last launch: when
+   that launch is small enough to fold (as above), *flag and *ticket are set
+   as there; otherwise *flag is NULL and the caller waits for the work as it
+   would without a ticket (an event). No ticket kernel is ever queued. Used by
+   the transport: a batch whose ticket is seen is complete without HIP's own
+   completion path. */
+int tempi_hip_pack_batch_ticket(const tempi_hip_batch_item *items, int n, void *stream, const uint32_t **flag,
+                                uint32_t *ticket);
+int tempi_hip_unpack_batch_ticket(const tempi_hip_batch_item *items, int n, void *stream, const uint32_t **flag,
+                                  uint32_t *ticket);
+int tempi_hip_copy_batch_ticket(const tempi_hip_copy_item *items, int n, void *stream, const uint32_t **flag,
+                                uint32_t *ticket);
 
 /* number of packed bytes a descriptor describes */
 int64_t tempi_hip_desc_bytes(const tempi_hip_desc *d);
@@ -145,6 +157,9 @@ int tempi_hip_stream_create(void **stream); /* non-blocking stream */
 int tempi_hip_stream_create_priority(void **stream, int high);
 int tempi_hip_stream_destroy(void *stream);
 int tempi_hip_stream_synchronize(void *stream);
+/* 0 when everything queued on `stream` has completed, 1 when not yet,
+   otherwise the stream's error */
+int tempi_hip_stream_query(void *stream);
 /* wait for `stream` by a ticket a kernel queued behind its work stores to
    pinned memory (faster than tempi_hip_stream_synchronize for small work) */
 int tempi_hip_stream_signal_wait(void *stream);

@@ -75,6 +75,7 @@ TEMPI_EXPORT void tempi_get_counters(tempi_counters_t *o) {
   o->staged_unpacks = c.staged_unpacks;
   o->ticket_waits = c.ticket_waits;
   o->sync_waits = c.sync_waits;
+  o->ticket_batches = c.ticket_batches;
 }
 
 TEMPI_EXPORT void tempi_reset_counters(void) {

@@ -80,6 +80,7 @@ void init() {
   if (const char *s = std::getenv("TEMPI_FIRST_FLUSH")) firstFlush = size_t(std::max(1, std::atoi(s)));
   scattersInFlight = 0;
   eagerFlush = std::getenv("TEMPI_EAGER_FLUSH") != nullptr;
+  batchTickets = std::getenv("TEMPI_NO_BATCH_TICKET") == nullptr;
   directShared.clear();
   directShared.reserve(512);
   active.reserve(2048);
@@ -390,14 +391,31 @@ bool progress(bool full) {
   for (auto &b : batches) {
     const uint64_t bit = uint64_t(1) << ((b->device * gpu::kMaxLanes + b->lane) & 63);
     if (b->complete || (blocked & bit)) continue;
-    const int q = tempi_hip_event_query(b->event);
-    if (q == 1) {
-      blocked |= bit;
-      continue;
+    if (b->flag) { // the batch's last launch stores its ticket (tickets of a stream ascend)
+      if (int32_t(__atomic_load_n(b->flag, __ATOMIC_ACQUIRE) - b->ticket) < 0) {
+        // not yet: now and then ask the stream, so that a faulted launch (which
+        // would never store the ticket) ends in its error instead of a hang
+        if ((++b->polls & 255) == 0) {
+          const int q = tempi_hip_stream_query(b->stream);
+          if (q == 0 && int32_t(__atomic_load_n(b->flag, __ATOMIC_ACQUIRE) - b->ticket) < 0)
+            LOG_FATAL("a batch's stream is idle but its completion ticket was never stored");
+          if (q != 1) gpu::check(q, "stream query");
+        }
+        if (int32_t(__atomic_load_n(b->flag, __ATOMIC_ACQUIRE) - b->ticket) < 0) {
+          blocked |= bit;
+          continue;
+        }
+      }
+    } else {
+      const int q = tempi_hip_event_query(b->event);
+      if (q == 1) {
+        blocked |= bit;
+        continue;
+      }
+      gpu::check(q, "event query");
+      put_event(b->event);
+      b->event = nullptr;
     }
-    gpu::check(q, "event query");
-    put_event(b->event);
-    b->event = nullptr;
     b->complete = true;
     if (b->scatter) --scattersInFlight;
     std::vector<Op *> ops;

@@ -250,8 +250,13 @@ bool copy_ok(const tempi_hip_desc &dst, const tempi_hip_desc &src);
 
 // ---------------------------------------------------- operations (p2p_ops)
 
-// one batched launch (+ its trailing copies) and the event that follows it
+// one batched launch (+ its trailing copies) and how its completion is seen:
+// the ticket its last launch stores (flag != nullptr), or an event behind it
 struct GpuBatch {
+  const uint32_t *flag = nullptr; // ticket flag (pinned host memory)
+  uint32_t ticket = 0;
+  uint32_t polls = 0;             // ticket polls so far (the stream is queried now and then)
+  void *stream = nullptr;
   void *event = nullptr;
   int device = 0;
   int lane = 0;
@@ -351,6 +356,7 @@ extern size_t earlyFlush;      // TEMPI_EARLY_FLUSH
 extern size_t firstFlush;      // TEMPI_FIRST_FLUSH: the same while no scatter batch is in flight
 extern int scattersInFlight;   // scatter / copy batches launched and not yet seen complete
 extern bool eagerFlush;        // TEMPI_EAGER_FLUSH (A/B)
+extern bool batchTickets;      // !TEMPI_NO_BATCH_TICKET: batches complete by a folded ticket when they can
 void flush_list(PendingList &list, bool pack);
 void flush();
 

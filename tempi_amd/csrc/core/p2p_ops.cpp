@@ -162,6 +162,7 @@ size_t earlyFlush = 32;
 size_t firstFlush = 16;
 int scattersInFlight = 0;
 bool eagerFlush = false;
+bool batchTickets = true;
 
 namespace {
 template <typename T> const T *select(const std::vector<T> &v, const std::vector<int> &dev, int d, bool all,
@@ -211,19 +212,41 @@ void flush_list(PendingList &list, bool pack) {
     if (cur != dev) tempi_hip_set_device(dev);
     counters.batches++;
     counters.batched_items += nitems + ncopies;
-    if (nitems)
-      gpu::check(pack ? tempi_hip_pack_batch(items, int(nitems), s) : tempi_hip_unpack_batch(items, int(nitems), s),
-                 pack ? "batched pack" : "batched unpack");
-    if (ncopies) gpu::check(tempi_hip_copy_batch(copies, int(ncopies), s), "batched direct copy");
+    // the last launch of the batch may store a completion ticket itself
+    // (never after a staged copy, which is not a kernel)
+    bool staged = false;
+    for (const PendingList::Stage &st : list.stages) staged |= st.dev == dev;
+    const bool ticketed = batchTickets && !staged;
+    const uint32_t *flag = nullptr;
+    uint32_t ticket = 0;
+    if (nitems) {
+      const bool last = ticketed && !ncopies;
+      const int e = pack ? (last ? tempi_hip_pack_batch_ticket(items, int(nitems), s, &flag, &ticket)
+                                 : tempi_hip_pack_batch(items, int(nitems), s))
+                         : (last ? tempi_hip_unpack_batch_ticket(items, int(nitems), s, &flag, &ticket)
+                                 : tempi_hip_unpack_batch(items, int(nitems), s));
+      gpu::check(e, pack ? "batched pack" : "batched unpack");
+    }
+    if (ncopies)
+      gpu::check(ticketed ? tempi_hip_copy_batch_ticket(copies, int(ncopies), s, &flag, &ticket)
+                          : tempi_hip_copy_batch(copies, int(ncopies), s),
+                 "batched direct copy");
     for (const PendingList::Stage &st : list.stages)
       if (st.dev == dev) gpu::check(tempi_hip_memcpy_async(st.dst, st.src, st.n, s), "staged D2H");
     auto b = std::make_shared<GpuBatch>();
     b->device = dev;
     b->lane = lane;
     b->scatter = !pack;
+    b->stream = s;
     if (!pack) ++scattersInFlight;
-    b->event = get_event();
-    gpu::check(tempi_hip_event_record(b->event, s), "event record");
+    if (flag) {
+      counters.ticket_batches++;
+      b->flag = flag;
+      b->ticket = ticket;
+    } else {
+      b->event = get_event();
+      gpu::check(tempi_hip_event_record(b->event, s), "event record");
+    }
     if (cur != dev) tempi_hip_set_device(cur);
     for (Op *op : list.ops)
       if (op->device == dev) {

@@ -526,22 +526,22 @@ __device__ __forceinline__ void unpack_body(const KArgs<ND> &a, uint32_t blk, ui
 // a workgroup of a write-through gather that still needs the release: the
 // first and last tiles hold the object's partial chunks (folded launches never
 // grid-stride: at most TEMPI_FOLD_MAX_BLOCKS_WT workgroups, one tile each)
-__device__ __forceinline__ bool needs_release(uint32_t flags, uint32_t tile) {
-  return !(flags & kWriteThrough) || tile == 0 || tile + 1 == gridDim.x;
+__device__ __forceinline__ bool needs_release(uint32_t flags, uint32_t tile, uint32_t ntiles) {
+  return !(flags & kWriteThrough) || tile == 0 || tile + 1 == ntiles;
 }
 
 template <int W, int ND>
 __global__ __launch_bounds__(kBlock) void pack_kernel(const KArgs<ND> a, const Sig sg) {
   const uint32_t tile = xcd_tile(blockIdx.x, gridDim.x, a.flags);
   pack_body<W, ND>(a, tile, gridDim.x);
-  wg_signal(sg, needs_release(a.flags, tile));
+  wg_signal(sg, needs_release(a.flags, tile, gridDim.x));
 }
 
 template <int W, int ND>
 __global__ __launch_bounds__(kBlock) void unpack_kernel(const KArgs<ND> a, const Sig sg) {
   const uint32_t tile = xcd_tile(blockIdx.x, gridDim.x, a.flags);
   unpack_body<W, ND>(a, tile, gridDim.x);
-  wg_signal(sg, needs_release(a.flags, tile));
+  wg_signal(sg, needs_release(a.flags, tile, gridDim.x));
 }
 
 // ------------------------------------------- wave-interleaved scatter (unpack)
@@ -655,7 +655,7 @@ __device__ __forceinline__ void pack_il_tile(const KArgs<ND> &a, uint32_t tileId
 template <int W, int ND> __global__ __launch_bounds__(kBlock) void pack_il_kernel(const KArgs<ND> a, const Sig sg) {
   const uint32_t tile = xcd_tile(blockIdx.x, gridDim.x, a.flags);
   pack_il_tile<W, ND>(a, tile, gridDim.x);
-  wg_signal(sg, needs_release(a.flags, tile));
+  wg_signal(sg, needs_release(a.flags, tile, gridDim.x));
 }
 template <int W, int ND> __global__ __launch_bounds__(kBlock) void unpack_il_kernel(const KArgs<ND> a, const Sig sg) {
   unpack_il_tile<W, ND>(a, xcd_tile(blockIdx.x, gridDim.x, a.flags), gridDim.x);
@@ -751,7 +751,7 @@ template <int ND>
 __global__ __launch_bounds__(kBlock) void pack_dense_kernel(const KArgs<ND> a, const Sig sg) {
   const uint32_t tile = xcd_tile(blockIdx.x, gridDim.x, a.flags);
   pack_dense_tile<ND>(a, tile);
-  wg_signal(sg, needs_release(a.flags, tile));
+  wg_signal(sg, needs_release(a.flags, tile, gridDim.x));
 }
 
 // Many objects in ONE launch (e.g. the 26 x nQuants faces of a halo step):
@@ -779,29 +779,37 @@ template <int ND> __device__ __forceinline__ uint32_t find_item(const BatchArgs<
   return lo;
 }
 
+// (sg: a completion ticket folded into the launch, as in the single-object
+// kernels; a workgroup's partial chunks are its item's first / last tile)
 template <int W, int ND>
-__global__ __launch_bounds__(kBlock) void pack_batch_kernel(const BatchArgs<ND> b) {
+__global__ __launch_bounds__(kBlock) void pack_batch_kernel(const BatchArgs<ND> b, const Sig sg) {
   const uint32_t i = find_item<ND>(b, blockIdx.x), n = b.first[i + 1] - b.first[i];
   const uint32_t blk = xcd_tile(blockIdx.x - b.first[i], n, b.item[i].flags); // (within the item: balanced)
   pack_body<W, ND>(b.item[i], blk, n);
-}
-
-template <int W, int ND> __global__ __launch_bounds__(kBlock) void pack_il_batch_kernel(const BatchArgs<ND> b) {
-  const uint32_t i = find_item<ND>(b, blockIdx.x), n = b.first[i + 1] - b.first[i];
-  const uint32_t blk = xcd_tile(blockIdx.x - b.first[i], n, b.item[i].flags); // (within the item: balanced)
-  pack_il_tile<W, ND>(b.item[i], blk, n);
-}
-template <int W, int ND> __global__ __launch_bounds__(kBlock) void unpack_il_batch_kernel(const BatchArgs<ND> b) {
-  const uint32_t i = find_item<ND>(b, blockIdx.x), n = b.first[i + 1] - b.first[i];
-  const uint32_t blk = xcd_tile(blockIdx.x - b.first[i], n, b.item[i].flags); // (within the item: balanced)
-  unpack_il_tile<W, ND>(b.item[i], blk, n);
+  wg_signal(sg, needs_release(b.item[i].flags, blk, n));
 }
 
 template <int W, int ND>
-__global__ __launch_bounds__(kBlock) void unpack_batch_kernel(const BatchArgs<ND> b) {
+__global__ __launch_bounds__(kBlock) void pack_il_batch_kernel(const BatchArgs<ND> b, const Sig sg) {
+  const uint32_t i = find_item<ND>(b, blockIdx.x), n = b.first[i + 1] - b.first[i];
+  const uint32_t blk = xcd_tile(blockIdx.x - b.first[i], n, b.item[i].flags); // (within the item: balanced)
+  pack_il_tile<W, ND>(b.item[i], blk, n);
+  wg_signal(sg, needs_release(b.item[i].flags, blk, n));
+}
+template <int W, int ND>
+__global__ __launch_bounds__(kBlock) void unpack_il_batch_kernel(const BatchArgs<ND> b, const Sig sg) {
+  const uint32_t i = find_item<ND>(b, blockIdx.x), n = b.first[i + 1] - b.first[i];
+  const uint32_t blk = xcd_tile(blockIdx.x - b.first[i], n, b.item[i].flags); // (within the item: balanced)
+  unpack_il_tile<W, ND>(b.item[i], blk, n);
+  wg_signal(sg, true);
+}
+
+template <int W, int ND>
+__global__ __launch_bounds__(kBlock) void unpack_batch_kernel(const BatchArgs<ND> b, const Sig sg) {
   const uint32_t i = find_item<ND>(b, blockIdx.x), n = b.first[i + 1] - b.first[i];
   const uint32_t blk = xcd_tile(blockIdx.x - b.first[i], n, b.item[i].flags); // (within the item: balanced)
   unpack_body<W, ND>(b.item[i], blk, n);
+  wg_signal(sg, needs_release(b.item[i].flags, blk, n));
 }
 
 // ---------------------------------------------------------------- host side
@@ -938,10 +946,9 @@ bool scatter_write_through(const Norm &n) {
 // the kernel's Sig for a launch of `blocks` workgroups: the fold when one is
 // offered and the grid is small enough (counted on the host as the kernel
 // will count on the device), else none
-Sig take_fold(uint32_t blocks, bool writeThrough) {
+Sig take_fold_from(tempi_ticket::Fold *f, uint32_t blocks, bool writeThrough) {
   using tempi_ticket::kShards;
   Sig sg{};
-  tempi_ticket::Fold *f = gFold;
   if (!f || f->taken || !f->t || !f->t->counter || blocks == 0 ||
       blocks > (writeThrough ? f->max_blocks_wt : f->max_blocks))
     return sg;
@@ -958,6 +965,7 @@ Sig take_fold(uint32_t blocks, bool writeThrough) {
   sg.ticket = f->ticket;
   return sg;
 }
+Sig take_fold(uint32_t blocks, bool writeThrough) { return take_fold_from(gFold, blocks, writeThrough); }
 
 // descriptor + workgroup count of one object
 template <int W, int ND>
@@ -1011,24 +1019,37 @@ struct Job {
   uint32_t flags;
 };
 
-template <int W, int ND> int launch_batch_nd(bool pack, const std::vector<Job> &jobs, hipStream_t s) {
+// fold: offered to this group's last launch (the caller passes it to the
+// batch's last group only, so that the ticket follows every launch of it)
+template <int W, int ND>
+int launch_batch_nd(bool pack, const std::vector<Job> &jobs, hipStream_t s, tempi_ticket::Fold *fold) {
   const bool il = il_width(pack, W); // il kernels: one kBlock x 16-byte tile per workgroup
   BatchArgs<ND> b;
+  bool wt[BatchArgs<ND>::kMax]; // item may store write-through if the launch folds a ticket
   b.nitems = 0;
   uint32_t total = 0;
-  auto flush = [&]() -> int {
+  auto flush = [&](bool last) -> int {
     if (!b.nitems) return 0;
     b.first[b.nitems] = total;
+    Sig sg{};
+    if (last && fold && total) {
+      bool all = true;
+      for (uint32_t k = 0; k < b.nitems; ++k) all &= wt[k];
+      sg = take_fold_from(fold, total, all);
+      if (sg.flag)
+        for (uint32_t k = 0; k < b.nitems; ++k)
+          if (wt[k]) b.item[k].flags |= kWriteThrough;
+    }
     if (total) {
       if (il)
         if (pack)
-          hipLaunchKernelGGL((pack_il_batch_kernel<W, ND>), dim3(total), dim3(kBlock), 0, s, b);
+          hipLaunchKernelGGL((pack_il_batch_kernel<W, ND>), dim3(total), dim3(kBlock), 0, s, b, sg);
         else
-          hipLaunchKernelGGL((unpack_il_batch_kernel<W, ND>), dim3(total), dim3(kBlock), 0, s, b);
+          hipLaunchKernelGGL((unpack_il_batch_kernel<W, ND>), dim3(total), dim3(kBlock), 0, s, b, sg);
       else if (pack)
-        hipLaunchKernelGGL((pack_batch_kernel<W, ND>), dim3(total), dim3(kBlock), 0, s, b);
+        hipLaunchKernelGGL((pack_batch_kernel<W, ND>), dim3(total), dim3(kBlock), 0, s, b, sg);
       else
-        hipLaunchKernelGGL((unpack_batch_kernel<W, ND>), dim3(total), dim3(kBlock), 0, s, b);
+        hipLaunchKernelGGL((unpack_batch_kernel<W, ND>), dim3(total), dim3(kBlock), 0, s, b, sg);
     }
     b.nitems = 0;
     total = 0;
@@ -1044,25 +1065,29 @@ template <int W, int ND> int launch_batch_nd(bool pack, const std::vector<Job> &
     if (il) blocks = (a.nchunks + kBlock - 1) / kBlock;
     if (!blocks) continue;
     if (uint64_t(total) + blocks >= (uint64_t(1) << 31))
-      if (int e = flush()) return e;
+      if (int e = flush(false)) return e;
     b.first[b.nitems] = total;
     b.item[b.nitems] = a;
+    // gathers write whole packed chunks; scatters of 16-byte words write-through
+    // only where st_scatter allows it (the il scatters never: narrow words)
+    wt[b.nitems] = pack || (!il && W == 16 && scatter_write_through(j.n));
     b.nitems++;
     total += blocks;
     if (b.nitems == uint32_t(BatchArgs<ND>::kMax))
-      if (int e = flush()) return e;
+      if (int e = flush(false)) return e;
   }
-  return flush();
+  return flush(true);
 }
 
-template <int W> int launch_batch_w(bool pack, int nd, const std::vector<Job> &jobs, hipStream_t s) {
+template <int W>
+int launch_batch_w(bool pack, int nd, const std::vector<Job> &jobs, hipStream_t s, tempi_ticket::Fold *fold) {
   switch (nd) {
-  case 0: return launch_batch_nd<W, 0>(pack, jobs, s);
-  case 1: return launch_batch_nd<W, 1>(pack, jobs, s);
-  case 2: return launch_batch_nd<W, 2>(pack, jobs, s);
-  case 3: return launch_batch_nd<W, 3>(pack, jobs, s);
-  case 4: return launch_batch_nd<W, 4>(pack, jobs, s);
-  case 5: return launch_batch_nd<W, 5>(pack, jobs, s);
+  case 0: return launch_batch_nd<W, 0>(pack, jobs, s, fold);
+  case 1: return launch_batch_nd<W, 1>(pack, jobs, s, fold);
+  case 2: return launch_batch_nd<W, 2>(pack, jobs, s, fold);
+  case 3: return launch_batch_nd<W, 3>(pack, jobs, s, fold);
+  case 4: return launch_batch_nd<W, 4>(pack, jobs, s, fold);
+  case 5: return launch_batch_nd<W, 5>(pack, jobs, s, fold);
   default: return int(hipErrorInvalidValue);
   }
 }
@@ -1209,7 +1234,10 @@ int launch_split(bool pack, char *packed, char *first, const Norm &n, hipStream_
   return 0;
 }
 
-int run_batch(bool pack, const tempi_hip_batch_item *items, int n, hipStream_t s) {
+// fold (optional): a completion ticket, offered to the batch's LAST launch
+// only: the stream runs launches in order, so its ticket follows all of them
+int run_batch(bool pack, const tempi_hip_batch_item *items, int n, hipStream_t s,
+              tempi_ticket::Fold *fold = nullptr) {
   // group by (word width, rank): one launch per group and per kMax objects
   std::vector<Job> groups[5][TEMPI_HIP_MAX_DIMS + 1];
   for (int i = 0; i < n; ++i) {
@@ -1231,17 +1259,21 @@ int run_batch(bool pack, const tempi_hip_batch_item *items, int n, hipStream_t s
     const int wi = w == 1 ? 0 : w == 2 ? 1 : w == 4 ? 2 : w == 8 ? 3 : 4;
     groups[wi][j.n.nd].push_back(j);
   }
+  int lastGroup = -1;
+  for (int g = 0; g < 5 * (TEMPI_HIP_MAX_DIMS + 1); ++g)
+    if (!groups[g / (TEMPI_HIP_MAX_DIMS + 1)][g % (TEMPI_HIP_MAX_DIMS + 1)].empty()) lastGroup = g;
   for (int wi = 0; wi < 5; ++wi)
     for (int nd = 0; nd <= TEMPI_HIP_MAX_DIMS; ++nd) {
       const std::vector<Job> &g = groups[wi][nd];
       if (g.empty()) continue;
+      tempi_ticket::Fold *f = wi * (TEMPI_HIP_MAX_DIMS + 1) + nd == lastGroup ? fold : nullptr;
       int e = 0;
       switch (wi) {
-      case 0: e = launch_batch_w<1>(pack, nd, g, s); break;
-      case 1: e = launch_batch_w<2>(pack, nd, g, s); break;
-      case 2: e = launch_batch_w<4>(pack, nd, g, s); break;
-      case 3: e = launch_batch_w<8>(pack, nd, g, s); break;
-      default: e = launch_batch_w<16>(pack, nd, g, s); break;
+      case 0: e = launch_batch_w<1>(pack, nd, g, s, f); break;
+      case 1: e = launch_batch_w<2>(pack, nd, g, s, f); break;
+      case 2: e = launch_batch_w<4>(pack, nd, g, s, f); break;
+      case 3: e = launch_batch_w<8>(pack, nd, g, s, f); break;
+      default: e = launch_batch_w<16>(pack, nd, g, s, f); break;
       }
       if (e) return e;
     }
@@ -1384,8 +1416,9 @@ template <int W> __device__ __forceinline__ void copy_body(const CArgs &a, uint3
   }
 }
 
-template <int W> __global__ __launch_bounds__(kCopyBlock) void copy_kernel(const CArgs a) {
+template <int W> __global__ __launch_bounds__(kCopyBlock) void copy_kernel(const CArgs a, const Sig sg) {
   copy_body<W>(a, xcd_tile(blockIdx.x, gridDim.x, a.flags), gridDim.x);
+  wg_signal(sg, true);
 }
 
 constexpr int kCopyMax = int((kBatchBytes - 8) / (sizeof(CArgs) + 4));
@@ -1395,7 +1428,7 @@ struct CBatchArgs {
   CArgs item[kCopyMax];
 };
 
-template <int W> __global__ __launch_bounds__(kCopyBlock) void copy_batch_kernel(const CBatchArgs b) {
+template <int W> __global__ __launch_bounds__(kCopyBlock) void copy_batch_kernel(const CBatchArgs b, const Sig sg) {
   uint32_t lo = 0, hi = b.nitems;
   while (hi - lo > 1) {
     const uint32_t mid = (lo + hi) >> 1;
@@ -1406,6 +1439,7 @@ template <int W> __global__ __launch_bounds__(kCopyBlock) void copy_batch_kernel
   }
   const uint32_t n = b.first[lo + 1] - b.first[lo];
   copy_body<W>(b.item[lo], xcd_tile(blockIdx.x - b.first[lo], n, b.item[lo].flags), n); // (within the item)
+  wg_signal(sg, true);
 }
 
 bool make_side(char *first, const Norm &n, int W, CSide *c) {
@@ -1497,17 +1531,19 @@ uint32_t copy_blocks(const CopyJob &j) {
   return uint32_t(b);
 }
 
-template <int W> int launch_copy_group(const std::vector<CopyJob> &jobs, hipStream_t s) {
+// fold: offered to this group's last launch (see run_batch)
+template <int W> int launch_copy_group(const std::vector<CopyJob> &jobs, hipStream_t s, tempi_ticket::Fold *fold) {
   CBatchArgs b;
   b.nitems = 0;
   uint32_t total = 0;
-  auto flush = [&]() -> int {
+  auto flush = [&](bool last) -> int {
     if (!b.nitems) return 0;
     b.first[b.nitems] = total;
+    const Sig sg = last && fold ? take_fold_from(fold, total, false) : Sig{};
     if (b.nitems == 1)
-      hipLaunchKernelGGL(copy_kernel<W>, dim3(total), dim3(kCopyBlock), 0, s, b.item[0]);
+      hipLaunchKernelGGL(copy_kernel<W>, dim3(total), dim3(kCopyBlock), 0, s, b.item[0], sg);
     else
-      hipLaunchKernelGGL(copy_batch_kernel<W>, dim3(total), dim3(kCopyBlock), 0, s, b);
+      hipLaunchKernelGGL(copy_batch_kernel<W>, dim3(total), dim3(kCopyBlock), 0, s, b, sg);
     b.nitems = 0;
     total = 0;
     return int(hipGetLastError());
@@ -1516,15 +1552,47 @@ template <int W> int launch_copy_group(const std::vector<CopyJob> &jobs, hipStre
     const uint32_t blocks = copy_blocks(j);
     if (!blocks) continue;
     if (uint64_t(total) + blocks >= (uint64_t(1) << 31))
-      if (int e = flush()) return e;
+      if (int e = flush(false)) return e;
     b.first[b.nitems] = total;
     b.item[b.nitems] = j.a;
     b.nitems++;
     total += blocks;
     if (b.nitems == uint32_t(kCopyMax))
-      if (int e = flush()) return e;
+      if (int e = flush(false)) return e;
   }
-  return flush();
+  return flush(true);
+}
+
+// the copy batch; fold: a completion ticket for its last launch (run_batch)
+int copy_batch(const tempi_hip_copy_item *items, int n, void *stream, tempi_ticket::Fold *fold) {
+  std::vector<CopyJob> groups[5];
+  for (int i = 0; i < n; ++i) {
+    CopyJob j;
+    if (!plan_copy(items[i].dst_first, items[i].src_first, &items[i].dst, &items[i].src, &j))
+      return int(hipErrorInvalidValue);
+    j.a.flags |= items[i].flags & TEMPI_HIP_ITEM_REMOTE;
+    if (j.a.nwords == 0) continue;
+    const int wi = j.w == 1 ? 0 : j.w == 2 ? 1 : j.w == 4 ? 2 : j.w == 8 ? 3 : 4;
+    groups[wi].push_back(j);
+  }
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  int lastGroup = -1;
+  for (int wi = 0; wi < 5; ++wi)
+    if (!groups[wi].empty()) lastGroup = wi;
+  for (int wi = 0; wi < 5; ++wi) {
+    if (groups[wi].empty()) continue;
+    tempi_ticket::Fold *f = wi == lastGroup ? fold : nullptr;
+    int e = 0;
+    switch (wi) {
+    case 0: e = launch_copy_group<1>(pair_jobs(groups[wi]), s, f); break;
+    case 1: e = launch_copy_group<2>(pair_jobs(groups[wi]), s, f); break;
+    case 2: e = launch_copy_group<4>(pair_jobs(groups[wi]), s, f); break;
+    case 3: e = launch_copy_group<8>(pair_jobs(groups[wi]), s, f); break;
+    default: e = launch_copy_group<16>(pair_jobs(groups[wi]), s, f); break;
+    }
+    if (e) return e;
+  }
+  return 0;
 }
 
 } // namespace
@@ -1538,30 +1606,7 @@ int tempi_hip_copy_supported(void *dst_first, const void *src_first, const tempi
 }
 
 int tempi_hip_copy_batch(const tempi_hip_copy_item *items, int n, void *stream) {
-  std::vector<CopyJob> groups[5];
-  for (int i = 0; i < n; ++i) {
-    CopyJob j;
-    if (!plan_copy(items[i].dst_first, items[i].src_first, &items[i].dst, &items[i].src, &j))
-      return int(hipErrorInvalidValue);
-    j.a.flags |= items[i].flags & TEMPI_HIP_ITEM_REMOTE;
-    if (j.a.nwords == 0) continue;
-    const int wi = j.w == 1 ? 0 : j.w == 2 ? 1 : j.w == 4 ? 2 : j.w == 8 ? 3 : 4;
-    groups[wi].push_back(j);
-  }
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  for (int wi = 0; wi < 5; ++wi) {
-    if (groups[wi].empty()) continue;
-    int e = 0;
-    switch (wi) {
-    case 0: e = launch_copy_group<1>(pair_jobs(groups[wi]), s); break;
-    case 1: e = launch_copy_group<2>(pair_jobs(groups[wi]), s); break;
-    case 2: e = launch_copy_group<4>(pair_jobs(groups[wi]), s); break;
-    case 3: e = launch_copy_group<8>(pair_jobs(groups[wi]), s); break;
-    default: e = launch_copy_group<16>(pair_jobs(groups[wi]), s); break;
-    }
-    if (e) return e;
-  }
-  return 0;
+  return copy_batch(items, n, stream, nullptr);
 }
 
 int tempi_hip_pack(void *packed, const void *first, const tempi_hip_desc *d, void *stream) {
@@ -1612,6 +1657,36 @@ int with_ticket(bool pack, char *packed, char *first, const tempi_hip_desc *d, h
   if (fold.taken) tempi_ticket::stats().folded++;
   return fold.taken ? 0 : int(tempi_ticket::queue_kernel(*t, s, fold.ticket));
 }
+// A batch with a completion ticket folded into its last launch (run_batch,
+// copy_batch). When that launch is too large to fold, *flag stays NULL and
+// the caller waits as it would without a ticket: a batch never costs a
+// second launch (a queued ticket kernel per batch made the halo 1-3 %
+// slower, round 2).
+template <typename F> int batch_with_ticket(hipStream_t s, const uint32_t **flag, uint32_t *ticket, F &&run) {
+  *flag = nullptr;
+  *ticket = 0;
+  std::lock_guard<std::mutex> lock(tempi_ticket::mutex());
+  tempi_ticket::Ticket *t = tempi_ticket::of(s);
+  if (!t) return run(nullptr);
+  tempi_ticket::Fold fold;
+  fold.t = t;
+  fold.ticket = t->next + 1; // issued only if a launch takes it
+  fold.max_blocks = tempi_ticket::fold_max_blocks();
+  fold.max_blocks_wt = tempi_ticket::fold_max_blocks_wt();
+  const int e = run(&fold);
+  if (e) {
+    if (fold.taken) t->broken = true; // the host counted a launch that may never run
+    return e;
+  }
+  if (fold.taken) {
+    t->next = fold.ticket;
+    *flag = t->host;
+    *ticket = fold.ticket;
+    tempi_ticket::stats().folded++;
+  }
+  return 0;
+}
+
 } // namespace
 
 extern "C" {
@@ -1626,6 +1701,24 @@ int tempi_hip_unpack_ticket(void *first, const void *packed, const tempi_hip_des
                             const uint32_t **flag, uint32_t *ticket) {
   return with_ticket(false, const_cast<char *>(static_cast<const char *>(packed)), static_cast<char *>(first), d,
                      static_cast<hipStream_t>(stream), flag, ticket);
+}
+
+int tempi_hip_pack_batch_ticket(const tempi_hip_batch_item *items, int n, void *stream, const uint32_t **flag,
+                                uint32_t *ticket) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  return batch_with_ticket(s, flag, ticket, [&](tempi_ticket::Fold *f) { return run_batch(true, items, n, s, f); });
+}
+
+int tempi_hip_unpack_batch_ticket(const tempi_hip_batch_item *items, int n, void *stream, const uint32_t **flag,
+                                  uint32_t *ticket) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  return batch_with_ticket(s, flag, ticket, [&](tempi_ticket::Fold *f) { return run_batch(false, items, n, s, f); });
+}
+
+int tempi_hip_copy_batch_ticket(const tempi_hip_copy_item *items, int n, void *stream, const uint32_t **flag,
+                                uint32_t *ticket) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  return batch_with_ticket(s, flag, ticket, [&](tempi_ticket::Fold *f) { return copy_batch(items, n, stream, f); });
 }
 
 int tempi_hip_pack_batch(const tempi_hip_batch_item *items, int n, void *stream) {

@@ -112,6 +112,15 @@ int tempi_hip_stream_destroy(void *stream) { RET(hipStreamDestroy(static_cast<hi
 int tempi_hip_stream_synchronize(void *stream) {
   RET(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
 }
+int tempi_hip_stream_query(void *stream) {
+  const hipError_t e = hipStreamQuery(static_cast<hipStream_t>(stream));
+  if (e == hipSuccess) return 0;
+  if (e == hipErrorNotReady) {
+    (void)hipGetLastError();
+    return 1;
+  }
+  RET(e);
+}
 
 } // extern "C"
 
