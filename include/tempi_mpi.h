@@ -40,14 +40,25 @@
  *                                                    with its payload size and received
  *                                                    as its payload, into host or device
  *                                                    memory
- *   MPI_Ssend / MPI_Bsend / MPI_Rsend / MPI_Issend / MPI_Ibsend / MPI_Irsend /
+ *   MPI_Ssend / MPI_Bsend / MPI_Rsend / MPI_Issend / MPI_Ibsend / MPI_Irsend
+ *                    (not interposed)                device objects take the TEMPI
+ *                                                    transport, handing the library
+ *                                                    their message with the same send
+ *                                                    mode; host buffers: the library's
+ *                                                    call, in send order
  *   MPI_Send_init / MPI_Ssend_init / MPI_Bsend_init / MPI_Rsend_init /
- *   MPI_Recv_init / MPI_Sendrecv_replace
- *                    (not interposed)                forwarded; when they concern
- *                                                    this same rank, TEMPI's self
- *                                                    channel hands what it holds to
- *                                                    the library first (keeps MPI
- *                                                    matching order)
+ *   MPI_Recv_init / MPI_Start / MPI_Startall
+ *                    (not interposed)                with TEMPI active beside a GPU,
+ *                                                    TEMPI persistent requests: each
+ *                                                    start posts the interposed
+ *                                                    non-blocking call; the request
+ *                                                    stays, inactive, after its
+ *                                                    wait / test
+ *   MPI_Sendrecv_replace
+ *                    (not interposed)                through MPI_Sendrecv when the
+ *                                                    receive is TEMPI's; otherwise
+ *                                                    forwarded (the self channel
+ *                                                    spills first: matching order)
  *   MPI_Barrier      (not interposed)                keeps TEMPI operations moving
  *                                                    while it waits (a peer may need
  *                                                    this rank's progress)
@@ -140,6 +151,8 @@ int MPI_Rsend_init(const void *buf, int count, MPI_Datatype datatype, int dest, 
                    MPI_Request *request);
 int MPI_Recv_init(void *buf, int count, MPI_Datatype datatype, int source, int tag, MPI_Comm comm,
                   MPI_Request *request);
+int MPI_Start(MPI_Request *request);
+int MPI_Startall(int count, MPI_Request array_of_requests[]);
 int MPI_Sendrecv_replace(void *buf, int count, MPI_Datatype datatype, int dest, int sendtag, int source,
                          int recvtag, MPI_Comm comm, MPI_Status *status);
 int MPI_Barrier(MPI_Comm comm);

@@ -76,6 +76,7 @@ TEMPI_EXPORT void tempi_get_counters(tempi_counters_t *o) {
   o->ticket_waits = c.ticket_waits;
   o->sync_waits = c.sync_waits;
   o->ticket_batches = c.ticket_batches;
+  o->persistent_starts = c.persistent_starts;
 }
 
 TEMPI_EXPORT void tempi_reset_counters(void) {
@@ -115,7 +116,7 @@ TEMPI_EXPORT int64_t tempi_mpi_constant(const char *name, int *found) {
       H(MPI_REQUEST_NULL), H(MPI_ORDER_C), H(MPI_ORDER_FORTRAN), H(MPI_ANY_SOURCE), H(MPI_ANY_TAG),
       H(MPI_PROC_NULL), H(MPI_SUM), H(MPI_MAX), H(MPI_MIN), H(MPI_THREAD_SINGLE),
       H(MPI_THREAD_FUNNELED), H(MPI_THREAD_SERIALIZED), H(MPI_THREAD_MULTIPLE),
-      H(MPI_MAX_PROCESSOR_NAME), H(MPI_UNDEFINED),
+      H(MPI_MAX_PROCESSOR_NAME), H(MPI_UNDEFINED), H(MPI_BSEND_OVERHEAD), H(MPI_ERR_REQUEST),
       P(MPI_STATUS_IGNORE), P(MPI_STATUSES_IGNORE), P(MPI_IN_PLACE), P(MPI_UNWEIGHTED), P(MPI_WEIGHTS_EMPTY), H(MPI_INFO_NULL),
       H(MPI_ERRORS_RETURN), H(MPI_ERRORS_ARE_FATAL), H(MPI_MESSAGE_NULL), H(MPI_MESSAGE_NO_PROC),
       {"sizeof(MPI_Message)", int64_t(sizeof(MPI_Message))},

@@ -10,6 +10,7 @@
 #include "log.hpp"
 #include "next_mpi.hpp"
 #include "p2p.hpp"
+#include "gpu.hpp"
 #include "state.hpp"
 
 #include "tempi_mpi.h"
@@ -208,7 +209,7 @@ TEMPI_EXPORT int MPI_Testany(int count, MPI_Request requests[], int *index, int 
   p2p::progress();
   bool anyActive = false;
   for (int i = 0; i < count; ++i) {
-    if (requests[i] == MPI_REQUEST_NULL) continue;
+    if (requests[i] == MPI_REQUEST_NULL || p2p::inactive(requests[i])) continue;
     anyActive = true;
     int err = MPI_SUCCESS;
     if (test_one(&requests[i], status, &err)) {
@@ -242,7 +243,7 @@ TEMPI_EXPORT int MPI_Testsome(int incount, MPI_Request requests[], int *outcount
   bool anyActive = false;
   int n = 0, err = MPI_SUCCESS;
   for (int i = 0; i < incount; ++i) {
-    if (requests[i] == MPI_REQUEST_NULL) continue;
+    if (requests[i] == MPI_REQUEST_NULL || p2p::inactive(requests[i])) continue;
     anyActive = true;
     int e = MPI_SUCCESS;
     if (test_one(&requests[i], at(statuses, n), &e)) {
@@ -362,63 +363,139 @@ TEMPI_EXPORT int MPI_Imrecv(void *buf, int count, MPI_Datatype datatype, MPI_Mes
   return p2p::imrecv(buf, count, datatype, message, request);
 }
 
-// The send modes and persistent requests TEMPI does not carry go to the
-// library unchanged -- after the self channel of the communicator spills when
-// they concern this same rank (p2p.hpp: self_spill), since the library would
-// otherwise hold a message to this rank that a receive waiting in TEMPI never
-// sees.
+// The send modes: the reference interposes only standard sends, so a
+// device-buffer MPI_Ssend / MPI_Bsend / MPI_Rsend (and their I-forms) would
+// reach a library that cannot read GPU memory. Here they take the TEMPI path
+// with the matching library call (p2p.hpp: SendMode); host buffers keep the
+// library's call, after the self channel spills and gated sends drain, as for
+// MPI_Send.
+namespace {
+int mode_send(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm,
+              MPI_Request *request, p2p::SendMode mode) {
+  resolve_next();
+  p2p::Route route;
+  if (p2p::handles(buf, count, datatype, dest, &route)) {
+    counters.sends++;
+    MPI_Request r;
+    const bool blocking = request == nullptr;
+    const int rc = p2p::isend(buf, count, datatype, dest, tag, comm, request ? request : &r, route, -1, blocking,
+                              mode);
+    if (rc != MPI_SUCCESS || !blocking) return rc;
+    return p2p::wait(&r, MPI_STATUS_IGNORE);
+  }
+  counters.lib_sends++;
+  if (state.active) {
+    if (request) p2p::progress(false);
+    p2p::self_spill(comm, dest);
+    if (p2p::send_gated(comm, dest)) p2p::drain_sends(comm, dest); // keep send order
+  }
+  using M = p2p::SendMode;
+  if (request) {
+    if (mode == M::SYNC) return next.MPI_Issend(buf, count, datatype, dest, tag, comm, request);
+    if (mode == M::BUFFERED) return next.MPI_Ibsend(buf, count, datatype, dest, tag, comm, request);
+    return next.MPI_Irsend(buf, count, datatype, dest, tag, comm, request);
+  }
+  if (mode == M::SYNC) return next.MPI_Ssend(buf, count, datatype, dest, tag, comm);
+  if (mode == M::BUFFERED) return next.MPI_Bsend(buf, count, datatype, dest, tag, comm);
+  return next.MPI_Rsend(buf, count, datatype, dest, tag, comm);
+}
+} // namespace
+
+TEMPI_EXPORT int MPI_Ssend(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm) {
+  TEMPI_RANGE("MPI_Ssend");
+  return mode_send(buf, count, datatype, dest, tag, comm, nullptr, p2p::SendMode::SYNC);
+}
+TEMPI_EXPORT int MPI_Bsend(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm) {
+  TEMPI_RANGE("MPI_Bsend");
+  return mode_send(buf, count, datatype, dest, tag, comm, nullptr, p2p::SendMode::BUFFERED);
+}
+TEMPI_EXPORT int MPI_Rsend(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm) {
+  TEMPI_RANGE("MPI_Rsend");
+  return mode_send(buf, count, datatype, dest, tag, comm, nullptr, p2p::SendMode::READY);
+}
+TEMPI_EXPORT int MPI_Issend(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm,
+                            MPI_Request *request) {
+  return mode_send(buf, count, datatype, dest, tag, comm, request, p2p::SendMode::SYNC);
+}
+TEMPI_EXPORT int MPI_Ibsend(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm,
+                            MPI_Request *request) {
+  return mode_send(buf, count, datatype, dest, tag, comm, request, p2p::SendMode::BUFFERED);
+}
+TEMPI_EXPORT int MPI_Irsend(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm,
+                            MPI_Request *request) {
+  return mode_send(buf, count, datatype, dest, tag, comm, request, p2p::SendMode::READY);
+}
+
+// Persistent requests: TEMPI's while it is active beside a GPU (p2p.hpp:
+// persistent_init; MPI_Start posts through the interposed non-blocking calls,
+// so device objects take the transport and host buffers keep send order and
+// see descriptors), the library's otherwise. Not interposed by the reference.
+namespace {
+int persistent_init(bool send, const void *buf, int count, MPI_Datatype datatype, int peer, int tag, MPI_Comm comm,
+                    MPI_Request *request, p2p::SendMode mode) {
+  if (state.active && gpu::available())
+    return p2p::persistent_init(send, buf, count, datatype, peer, tag, comm, mode, request);
+  if (state.active) p2p::self_spill(comm, peer);
+  using M = p2p::SendMode;
+  if (!send) return next.MPI_Recv_init(const_cast<void *>(buf), count, datatype, peer, tag, comm, request);
+  if (mode == M::SYNC) return next.MPI_Ssend_init(buf, count, datatype, peer, tag, comm, request);
+  if (mode == M::BUFFERED) return next.MPI_Bsend_init(buf, count, datatype, peer, tag, comm, request);
+  if (mode == M::READY) return next.MPI_Rsend_init(buf, count, datatype, peer, tag, comm, request);
+  return next.MPI_Send_init(buf, count, datatype, peer, tag, comm, request);
+}
+} // namespace
+
+TEMPI_EXPORT int MPI_Send_init(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm,
+                               MPI_Request *request) {
+  resolve_next();
+  return persistent_init(true, buf, count, datatype, dest, tag, comm, request, p2p::SendMode::STANDARD);
+}
+TEMPI_EXPORT int MPI_Ssend_init(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm,
+                                MPI_Request *request) {
+  resolve_next();
+  return persistent_init(true, buf, count, datatype, dest, tag, comm, request, p2p::SendMode::SYNC);
+}
+TEMPI_EXPORT int MPI_Bsend_init(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm,
+                                MPI_Request *request) {
+  resolve_next();
+  return persistent_init(true, buf, count, datatype, dest, tag, comm, request, p2p::SendMode::BUFFERED);
+}
+TEMPI_EXPORT int MPI_Rsend_init(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm,
+                                MPI_Request *request) {
+  resolve_next();
+  return persistent_init(true, buf, count, datatype, dest, tag, comm, request, p2p::SendMode::READY);
+}
+TEMPI_EXPORT int MPI_Recv_init(void *buf, int count, MPI_Datatype datatype, int source, int tag, MPI_Comm comm,
+                               MPI_Request *request) {
+  resolve_next();
+  if (state.active && !gpu::available() && p2p::holds(source, tag, comm))
+    LOG_WARN("MPI_Recv_init: a message it matches is held by an earlier MPI_Probe; the library's persistent "
+             "receive will not see it");
+  return persistent_init(false, buf, count, datatype, source, tag, comm, request, p2p::SendMode::STANDARD);
+}
+
+TEMPI_EXPORT int MPI_Start(MPI_Request *request) {
+  resolve_next();
+  if (state.active && p2p::is_tempi_request(*request)) return p2p::start(request);
+  return next.MPI_Start(request);
+}
+
+TEMPI_EXPORT int MPI_Startall(int count, MPI_Request requests[]) {
+  resolve_next();
+  if (!state.active || !any_tempi(count, requests)) return next.MPI_Startall(count, requests);
+  int err = MPI_SUCCESS;
+  for (int i = 0; i < count; ++i) { // (a burst of starts shares the transport's launches)
+    const int rc = MPI_Start(&requests[i]);
+    if (rc != MPI_SUCCESS && err == MPI_SUCCESS) err = rc;
+  }
+  return err;
+}
+
 #define TEMPI_SPILL_THEN(peer, call)                                                               \
   resolve_next();                                                                                  \
   if (state.active) p2p::self_spill(comm, peer);                                                   \
   return call;
 
-TEMPI_EXPORT int MPI_Ssend(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm) {
-  TEMPI_SPILL_THEN(dest, next.MPI_Ssend(buf, count, datatype, dest, tag, comm))
-}
-TEMPI_EXPORT int MPI_Bsend(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm) {
-  TEMPI_SPILL_THEN(dest, next.MPI_Bsend(buf, count, datatype, dest, tag, comm))
-}
-TEMPI_EXPORT int MPI_Rsend(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm) {
-  TEMPI_SPILL_THEN(dest, next.MPI_Rsend(buf, count, datatype, dest, tag, comm))
-}
-TEMPI_EXPORT int MPI_Issend(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm,
-                            MPI_Request *request) {
-  TEMPI_SPILL_THEN(dest, next.MPI_Issend(buf, count, datatype, dest, tag, comm, request))
-}
-TEMPI_EXPORT int MPI_Ibsend(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm,
-                            MPI_Request *request) {
-  TEMPI_SPILL_THEN(dest, next.MPI_Ibsend(buf, count, datatype, dest, tag, comm, request))
-}
-TEMPI_EXPORT int MPI_Irsend(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm,
-                            MPI_Request *request) {
-  TEMPI_SPILL_THEN(dest, next.MPI_Irsend(buf, count, datatype, dest, tag, comm, request))
-}
-TEMPI_EXPORT int MPI_Send_init(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm,
-                               MPI_Request *request) {
-  TEMPI_SPILL_THEN(dest, next.MPI_Send_init(buf, count, datatype, dest, tag, comm, request))
-}
-TEMPI_EXPORT int MPI_Ssend_init(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm,
-                                MPI_Request *request) {
-  TEMPI_SPILL_THEN(dest, next.MPI_Ssend_init(buf, count, datatype, dest, tag, comm, request))
-}
-TEMPI_EXPORT int MPI_Bsend_init(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm,
-                                MPI_Request *request) {
-  TEMPI_SPILL_THEN(dest, next.MPI_Bsend_init(buf, count, datatype, dest, tag, comm, request))
-}
-TEMPI_EXPORT int MPI_Rsend_init(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm,
-                                MPI_Request *request) {
-  TEMPI_SPILL_THEN(dest, next.MPI_Rsend_init(buf, count, datatype, dest, tag, comm, request))
-}
-TEMPI_EXPORT int MPI_Recv_init(void *buf, int count, MPI_Datatype datatype, int source, int tag, MPI_Comm comm,
-                               MPI_Request *request) {
-  resolve_next();
-  // (a persistent receive is the library's: a message a probe holds, or a
-  // descriptor from a co-located device send, never reaches it -- DESIGN §6)
-  if (state.active && p2p::holds(source, tag, comm))
-    LOG_WARN("MPI_Recv_init: a message it matches is held by an earlier MPI_Probe; the persistent receive "
-             "will not see it");
-  TEMPI_SPILL_THEN(source, next.MPI_Recv_init(buf, count, datatype, source, tag, comm, request))
-}
 // MPI_Sendrecv_replace: when the receive is TEMPI's (a device object, or a
 // host buffer a descriptor or a held message may reach: p2p::host_recv_aware)
 // the outgoing element is packed into a host buffer first and the exchange

@@ -53,6 +53,8 @@
   X(MPI_Bsend_init)                                                            \
   X(MPI_Rsend_init)                                                            \
   X(MPI_Recv_init)                                                             \
+  X(MPI_Start)                                                                 \
+  X(MPI_Startall)                                                              \
   X(MPI_Sendrecv_replace)                                                      \
   X(MPI_Alltoallv)                                                             \
   X(MPI_Neighbor_alltoallv)                                                    \

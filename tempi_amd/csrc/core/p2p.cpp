@@ -158,14 +158,14 @@ bool handles(const void *buf, int count, MPI_Datatype dt, int peer, Route *route
 
 
 int isend(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Comm comm, MPI_Request *req,
-          const Route &route, int force, bool blocking) {
+          const Route &route, int force, bool blocking, SendMode mode) {
   const TypeRecord *rec = route.rec;
   ScopedNs timer(counters.ns_isend);
   if (pendingPack.size() >= kMaxPending) flush(); // (no progress(): consecutive Isends share a launch)
   counters.isends++;
   if (!rec->packer) {
     self_spill(comm, dest);
-    *req = add(new_lib_isend(buf, count, dt, dest, tag, comm));
+    *req = add(new_lib_isend(buf, count, dt, dest, tag, comm, mode));
     return MPI_SUCCESS;
   }
   const gpu::Ptr &p = route.ptr;
@@ -174,7 +174,8 @@ int isend(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Co
   const int destWorld = topology::world_rank(comm, dest);
   // a non-blocking send to this same process: the receiver copies directly
   tempi_hip_desc flat;
-  if (directEnabled && !blocking && force < 0 && destWorld == state.worldRank && rec->flat(count, &flat)) {
+  if (directEnabled && !blocking && mode != SendMode::SYNC && mode != SendMode::BUFFERED && force < 0 && destWorld == state.worldRank &&
+      rec->flat(count, &flat)) {
     counters.send_direct++;
     *req = add(new_isend_direct(rec, origin, count, dt, dest, tag, comm, p.device, bytes, flat));
     return MPI_SUCCESS;
@@ -186,6 +187,8 @@ int isend(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Co
   if (force >= 0) m = Method(force);
   if (m == Method::IPC && (!colocated || ipc_broken(destWorld))) m = Method::ONESHOT;
   if (m == Method::DEVICE && !gpuAwareLibrary) m = colocated ? Method::IPC : Method::STAGED;
+  // a buffered send must fit the buffer the application attached for its bytes
+  if (mode == SendMode::BUFFERED && m == Method::IPC && bytes < int64_t(sizeof(IpcDesc))) m = Method::ONESHOT;
   switch (m) {
   case Method::ONESHOT: counters.send_oneshot++; break;
   case Method::STAGED: counters.send_staged++; break;
@@ -196,7 +199,7 @@ int isend(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Co
   // IPC COPY: a large message of wide rows is copied by the receiver straight
   // out of this process's object (no gather, no slab)
   const int64_t copyMin = (collectiveDepth > 0 && collCopyEnabled) ? 1 : ipcCopyMinBytes;
-  if (m == Method::IPC && ipcCopyEnabled && bytes >= copyMin && rec->flat(count, &flat) &&
+  if (m == Method::IPC && ipcCopyEnabled && mode != SendMode::BUFFERED && bytes >= copyMin && rec->flat(count, &flat) &&
       flat.ndims <= 3 && flat.block >= ipcCopyMinBlock && bytes < (int64_t(1) << 31)) {
     IpcCopyDesc d{};
     d.magic[0] = kMagicCopy;
@@ -219,7 +222,7 @@ int isend(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Co
   int cur = 0;
   tempi_hip_get_device(&cur);
   if (cur != p.device) tempi_hip_set_device(p.device);
-  *req = add(new_isend(rec, origin, count, dt, dest, tag, comm, p.device, m, bytes));
+  *req = add(new_isend(rec, origin, count, dt, dest, tag, comm, p.device, m, bytes, mode));
   if (cur != p.device) tempi_hip_set_device(cur);
   return MPI_SUCCESS;
 }
@@ -319,15 +322,29 @@ bool is_tempi_request(MPI_Request r) {
   return h != 0 && h < kHandleSpace && active.count(h);
 }
 
+namespace detail {
+Op *find_op(MPI_Request r) {
+  const uint32_t h = uint32_t(r);
+  if (h == 0 || h >= kHandleSpace) return nullptr;
+  auto it = active.find(h);
+  return it == active.end() ? nullptr : it->second.get();
+}
+} // namespace detail
+
 bool peek(MPI_Request r) {
   auto it = active.find(uint32_t(r));
-  return it != active.end() && it->second->done;
+  if (it == active.end()) return false;
+  if (PersistentOp *p = it->second->persistent()) return persistent_peek(p);
+  return it->second->done;
 }
 
 void release(MPI_Request *req) {
   auto it = active.find(uint32_t(*req));
   if (it != active.end()) {
-    if (it->second->done) {
+    if (PersistentOp *p = it->second->persistent()) {
+      persistent_free(p);
+      active.erase(uint32_t(*req)); // (the iterator may have moved: freeing the inner request touched the table)
+    } else if (it->second->done) {
       active.erase(it);
     } else {
       it->second->detached = true;
@@ -340,6 +357,7 @@ void release(MPI_Request *req) {
 int get_status(MPI_Request r, int *flag, MPI_Status *status) {
   auto it = active.find(uint32_t(r));
   if (it == active.end()) return next.MPI_Request_get_status(r, flag, status);
+  if (PersistentOp *p = it->second->persistent()) return persistent_get_status(p, flag, status);
   progress();
   *flag = it->second->done ? 1 : 0;
   if (*flag) it->second->status(status);
@@ -348,7 +366,9 @@ int get_status(MPI_Request r, int *flag, MPI_Status *status) {
 
 int cancel(MPI_Request r) {
   auto it = active.find(uint32_t(r));
-  if (it != active.end()) it->second->cancel();
+  if (it == active.end()) return MPI_SUCCESS;
+  if (PersistentOp *p = it->second->persistent()) return persistent_cancel(p);
+  it->second->cancel();
   return MPI_SUCCESS;
 }
 
@@ -541,7 +561,8 @@ bool progress(bool full) {
   return moved;
 }
 
-bool busy() { return !active.empty() || !pendingAcks.empty(); }
+// (idle persistent requests are not work; started ones have an inner request)
+bool busy() { return active.size() > size_t(persistent_count) || !pendingAcks.empty(); }
 
 namespace {
 // a completed operation's error, raised on its communicator's handler (as
@@ -556,6 +577,7 @@ int wait(MPI_Request *req, MPI_Status *status) {
   const uint32_t h = uint32_t(*req);
   auto it = active.find(h);
   if (it == active.end()) return next.MPI_Wait(req, status);
+  if (PersistentOp *p = it->second->persistent()) return persistent_wait(p, status);
   ScopedNs timer(counters.ns_wait);
   Op *op = it->second.get();
   while (!op->done) {
@@ -574,6 +596,7 @@ int test(MPI_Request *req, int *flag, MPI_Status *status) {
   const uint32_t h = uint32_t(*req);
   auto it = active.find(h);
   if (it == active.end()) return next.MPI_Test(req, flag, status);
+  if (PersistentOp *p = it->second->persistent()) return persistent_test(p, flag, status);
   progress();
   if (!it->second->done) it->second->stalled();
   *flag = it->second->done ? 1 : 0;

@@ -73,12 +73,22 @@ struct CollectiveScope {
   CollectiveScope &operator=(const CollectiveScope &) = delete;
 };
 
+// MPI's send modes. A TEMPI send hands the library one message (the packed
+// bytes or a descriptor) with the matching library call: MPI_Issend for
+// SYNC (the send completes once a receive has matched it), MPI_Ibsend for
+// BUFFERED (local completion, from the application's attached buffer),
+// MPI_Isend for STANDARD and READY (a standard send is a valid ready send).
+// SYNC never takes the DIRECT route (a stalled direct send completes alone);
+// BUFFERED takes neither DIRECT nor IPC COPY (rendezvous) nor a descriptor
+// larger than its payload (the attached buffer is sized for the payload).
+enum class SendMode { STANDARD, SYNC, BUFFERED, READY };
+
 // force: -1 = choose by TEMPI_DATATYPE_* / AUTO; else a forced method
 // (0 ONESHOT, 1 STAGED, 2 DEVICE, 3 IPC)
 // blocking = true (MPI_Send) never takes the DIRECT route, whose completion
 // needs the matching receive
 int isend(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Comm comm, MPI_Request *req,
-          const Route &route, int force = -1, bool blocking = false);
+          const Route &route, int force = -1, bool blocking = false, SendMode mode = SendMode::STANDARD);
 int irecv(void *buf, int count, MPI_Datatype dt, int source, int tag, MPI_Comm comm, MPI_Request *req,
           const Route &route);
 
@@ -121,6 +131,17 @@ void self_forget(MPI_Comm comm);
 bool send_gated(MPI_Comm comm, int dest);
 int isend_host(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Comm comm, MPI_Request *req);
 void drain_sends(MPI_Comm comm, int dest);
+
+// Persistent requests (p2p_persistent.cpp): a TEMPI request remembering its
+// arguments; start() posts the operation through the interposed MPI_Isend /
+// MPI_Issend / MPI_Ibsend / MPI_Irsend / MPI_Irecv. wait / test / peek /
+// get_status / cancel / release understand them; a completed one stays,
+// inactive (inactive(): skipped like MPI_REQUEST_NULL by MPI_Testany,
+// MPI_Waitany, MPI_Testsome, MPI_Waitsome).
+int persistent_init(bool send, const void *buf, int count, MPI_Datatype dt, int peer, int tag, MPI_Comm comm,
+                    SendMode mode, MPI_Request *req);
+int start(MPI_Request *req);
+bool inactive(MPI_Request r);
 
 bool is_tempi_request(MPI_Request r);
 // complete? (no progress, no release: MPI_Testall's all-or-nothing rule)

@@ -266,8 +266,11 @@ struct GpuBatch {
 };
 extern std::deque<std::shared_ptr<GpuBatch>> batches; // launch order
 
+struct PersistentOp; // p2p_persistent.cpp
+
 struct Op {
   virtual ~Op() {}
+  virtual PersistentOp *persistent() { return nullptr; }
   static void *operator new(size_t n) { return op_pool().allocate(n, alignof(std::max_align_t)); }
   // (virtual destructor: `n` is the size of the object's dynamic type)
   static void operator delete(void *p, size_t n) { op_pool().deallocate(p, n, alignof(std::max_align_t)); }
@@ -362,13 +365,17 @@ void flush();
 
 // the send state machines (p2p_ops.cpp)
 std::unique_ptr<Op> new_isend(const TypeRecord *r, const char *origin, int count, MPI_Datatype dt, int dest, int tag,
-                              MPI_Comm comm, int dev, Method m, int64_t bytes);
+                              MPI_Comm comm, int dev, Method m, int64_t bytes, SendMode mode);
 std::unique_ptr<Op> new_isend_direct(const TypeRecord *r, const char *origin, int count, MPI_Datatype dt, int dest,
                                      int tag, MPI_Comm comm, int dev, int64_t bytes, const tempi_hip_desc &flat);
 std::unique_ptr<Op> new_isend_copy(const TypeRecord *r, const char *origin, int count, MPI_Datatype dt, int dest,
                                    int tag, MPI_Comm comm, int dev, int64_t bytes, int peerWorld,
                                    const IpcCopyDesc &filled);
-std::unique_ptr<Op> new_lib_isend(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Comm comm);
+std::unique_ptr<Op> new_lib_isend(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Comm comm,
+                                  SendMode mode);
+// the library send of a TEMPI message in the application's send mode
+int lib_isend(SendMode mode, const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Comm comm,
+              MPI_Request *req);
 std::unique_ptr<Op> new_host_isend(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Comm comm);
 std::unique_ptr<Op> new_local_copies(const LocalCopies &plan);
 
@@ -410,6 +417,17 @@ void clear_channels();
 // ---------------------------------------------------- request table (p2p.cpp)
 
 MPI_Request add(std::unique_ptr<Op> op);
+
+// the op behind a TEMPI request (nullptr: not one)
+Op *find_op(MPI_Request r);
+// persistent requests (p2p_persistent.cpp): the completion family's side
+extern int persistent_count; // PersistentOps in the request table
+int persistent_wait(PersistentOp *p, MPI_Status *status);
+int persistent_test(PersistentOp *p, int *flag, MPI_Status *status);
+bool persistent_peek(PersistentOp *p);
+int persistent_get_status(PersistentOp *p, int *flag, MPI_Status *status);
+int persistent_cancel(PersistentOp *p);
+void persistent_free(PersistentOp *p); // before the request is dropped
 
 } // namespace detail
 } // namespace p2p

@@ -278,10 +278,12 @@ struct IsendOp : Op {
 
   uint64_t key;
 
+  SendMode mode;
+
   IsendOp(const TypeRecord *r, const char *o, int c, MPI_Datatype d, int de, int t, MPI_Comm cm, int dev,
-          Method m, int64_t b)
+          Method m, int64_t b, SendMode md)
       : rec(r->ref()), origin(o), count(c), dest(de), tag(t), dt(d), comm(cm), method(m), bytes(b),
-        key(gate_key(cm, de)) {
+        key(gate_key(cm, de)), mode(md) {
     device = dev;
     gate_enter(key, this);
     if (method == Method::ONESHOT) {
@@ -306,11 +308,11 @@ struct IsendOp : Op {
     switch (method) {
     case Method::ONESHOT:
     case Method::STAGED:
-      next.MPI_Isend(hslab->host, int(bytes), MPI_PACKED, dest, tag, comm, &lib);
+      lib_isend(mode, hslab->host, int(bytes), MPI_PACKED, dest, tag, comm, &lib);
       watch(this);
       break;
     case Method::DEVICE:
-      next.MPI_Isend(dslab->dev, int(bytes), MPI_PACKED, dest, tag, comm, &lib);
+      lib_isend(mode, dslab->dev, int(bytes), MPI_PACKED, dest, tag, comm, &lib);
       watch(this);
       break;
     case Method::IPC: {
@@ -336,7 +338,7 @@ struct IsendOp : Op {
       PendingAck &pa = *pendingAcks.back();
       if (slot < 0) next.MPI_Irecv(&pa.code, 1, MPI_INT, peer, desc.ackTag, ctrlComm, &pa.req);
       dslab = nullptr;
-      next.MPI_Isend(&desc, int(sizeof desc), MPI_PACKED, dest, tag, comm, &lib);
+      lib_isend(mode, &desc, int(sizeof desc), MPI_PACKED, dest, tag, comm, &lib);
       watch(this);
       break;
     }
@@ -549,13 +551,15 @@ struct LibIsendOp : Op {
   MPI_Datatype dt;
   int n = 0, dest, tag;
   MPI_Comm comm;
-  LibIsendOp(const void *b, int c, MPI_Datatype d, int de, int t, MPI_Comm cm) : dt(d), dest(de), tag(t), comm(cm) {
+  SendMode mode;
+  LibIsendOp(const void *b, int c, MPI_Datatype d, int de, int t, MPI_Comm cm, SendMode md)
+      : dt(d), dest(de), tag(t), comm(cm), mode(md) {
     buf.resize(size_t(std::max<int64_t>(pack_size(c, d, comm), 1)));
     tempi::pack(b, c, d, buf.data(), int(buf.size()), &n, comm);
     post_or_queue(gate_key(comm, dest), this);
   }
   void post() override {
-    next.MPI_Isend(buf.data(), n, MPI_PACKED, dest, tag, comm, &lib);
+    lib_isend(mode, buf.data(), n, MPI_PACKED, dest, tag, comm, &lib);
     watch(this);
   }
   void lib_done(const MPI_Status &) override { done = true; }
@@ -616,8 +620,8 @@ struct LocalCopyOp : Op {
 } // namespace
 
 std::unique_ptr<Op> new_isend(const TypeRecord *r, const char *origin, int count, MPI_Datatype dt, int dest, int tag,
-                              MPI_Comm comm, int dev, Method m, int64_t bytes) {
-  return std::make_unique<IsendOp>(r, origin, count, dt, dest, tag, comm, dev, m, bytes);
+                              MPI_Comm comm, int dev, Method m, int64_t bytes, SendMode mode) {
+  return std::make_unique<IsendOp>(r, origin, count, dt, dest, tag, comm, dev, m, bytes, mode);
 }
 std::unique_ptr<Op> new_isend_direct(const TypeRecord *r, const char *origin, int count, MPI_Datatype dt, int dest,
                                      int tag, MPI_Comm comm, int dev, int64_t bytes, const tempi_hip_desc &flat) {
@@ -628,8 +632,18 @@ std::unique_ptr<Op> new_isend_copy(const TypeRecord *r, const char *origin, int 
                                    const IpcCopyDesc &filled) {
   return std::make_unique<IsendCopyOp>(r, origin, count, dt, dest, tag, comm, dev, bytes, peerWorld, filled);
 }
-std::unique_ptr<Op> new_lib_isend(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Comm comm) {
-  return std::make_unique<LibIsendOp>(buf, count, dt, dest, tag, comm);
+std::unique_ptr<Op> new_lib_isend(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Comm comm,
+                                  SendMode mode) {
+  return std::make_unique<LibIsendOp>(buf, count, dt, dest, tag, comm, mode);
+}
+
+int lib_isend(SendMode mode, const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Comm comm,
+              MPI_Request *req) {
+  switch (mode) {
+  case SendMode::SYNC: return next.MPI_Issend(buf, count, dt, dest, tag, comm, req);
+  case SendMode::BUFFERED: return next.MPI_Ibsend(buf, count, dt, dest, tag, comm, req);
+  default: return next.MPI_Isend(buf, count, dt, dest, tag, comm, req);
+  }
 }
 std::unique_ptr<Op> new_host_isend(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Comm comm) {
   return std::make_unique<HostIsendOp>(buf, count, dt, dest, tag, comm);

@@ -42,7 +42,7 @@ _COUNTER_FIELDS = [
     "send_ipc", "lib_sends", "lib_recvs", "send_direct", "direct_fallbacks",
     "neighbor_colls", "send_ipc_copy", "copy_resends", "ipc_maps_replaced", "canary_ok", "canary_fail",
     "self_matched", "staged_packs", "staged_unpacks", "ticket_waits", "sync_waits",
-    "ticket_batches",
+    "ticket_batches", "persistent_starts",
 ]
 
 
@@ -268,6 +268,83 @@ class MPI:
         self._call("MPI_Irecv", ctypes.c_void_p(buf), count, self.h(t), source, tag,
                    self.h(self.COMM_WORLD if comm is None else comm), ctypes.byref(r))
         return r.value
+
+    # send modes (device objects: TEMPI's transport with the library call of
+    # the same mode)
+    def _mode_send(self, fn, buf, count, t, dest, tag, comm, nonblocking):
+        comm = self.h(self.COMM_WORLD if comm is None else comm)
+        if not nonblocking:
+            self._call(fn, ctypes.c_void_p(buf), count, self.h(t), dest, tag, comm)
+            return None
+        r = self.Request()
+        self._call(fn, ctypes.c_void_p(buf), count, self.h(t), dest, tag, comm, ctypes.byref(r))
+        return r.value
+
+    def Ssend(self, buf, count, t, dest, tag, comm=None):
+        self._mode_send("MPI_Ssend", buf, count, t, dest, tag, comm, False)
+
+    def Bsend(self, buf, count, t, dest, tag, comm=None):
+        self._mode_send("MPI_Bsend", buf, count, t, dest, tag, comm, False)
+
+    def Rsend(self, buf, count, t, dest, tag, comm=None):
+        self._mode_send("MPI_Rsend", buf, count, t, dest, tag, comm, False)
+
+    def Issend(self, buf, count, t, dest, tag, comm=None):
+        return self._mode_send("MPI_Issend", buf, count, t, dest, tag, comm, True)
+
+    def Ibsend(self, buf, count, t, dest, tag, comm=None):
+        return self._mode_send("MPI_Ibsend", buf, count, t, dest, tag, comm, True)
+
+    def Irsend(self, buf, count, t, dest, tag, comm=None):
+        return self._mode_send("MPI_Irsend", buf, count, t, dest, tag, comm, True)
+
+    def Buffer_attach(self, nbytes):
+        """attach a host buffer of nbytes for buffered sends (kept alive here)"""
+        self._bsend_buf = (ctypes.c_char * nbytes)()
+        self._call("MPI_Buffer_attach", self._bsend_buf, nbytes)
+
+    def Buffer_detach(self):
+        p, n = ctypes.c_void_p(), ctypes.c_int(0)
+        self._call("MPI_Buffer_detach", ctypes.byref(p), ctypes.byref(n))
+        self._bsend_buf = None
+        return n.value
+
+    # persistent requests
+    def _init(self, fn, buf, count, t, peer, tag, comm):
+        r = self.Request()
+        self._call(fn, ctypes.c_void_p(buf), count, self.h(t), peer, tag,
+                   self.h(self.COMM_WORLD if comm is None else comm), ctypes.byref(r))
+        return r.value
+
+    def Send_init(self, buf, count, t, dest, tag, comm=None):
+        return self._init("MPI_Send_init", buf, count, t, dest, tag, comm)
+
+    def Ssend_init(self, buf, count, t, dest, tag, comm=None):
+        return self._init("MPI_Ssend_init", buf, count, t, dest, tag, comm)
+
+    def Bsend_init(self, buf, count, t, dest, tag, comm=None):
+        return self._init("MPI_Bsend_init", buf, count, t, dest, tag, comm)
+
+    def Rsend_init(self, buf, count, t, dest, tag, comm=None):
+        return self._init("MPI_Rsend_init", buf, count, t, dest, tag, comm)
+
+    def Recv_init(self, buf, count, t, source, tag, comm=None):
+        return self._init("MPI_Recv_init", buf, count, t, source, tag, comm)
+
+    def Start(self, req):
+        r = self.Request(req)
+        self._call("MPI_Start", ctypes.byref(r))
+        return r.value
+
+    def Start_rc(self, req):
+        """MPI_Start's return code (errors return under MPI_ERRORS_RETURN)"""
+        r = self.Request(req)
+        return self.L.MPI_Start(ctypes.byref(r))
+
+    def Startall(self, reqs):
+        arr = self._reqs(reqs)
+        self._call("MPI_Startall", len(reqs), arr)
+        return list(arr)[:len(reqs)]
 
     def Wait(self, req):
         r = self.Request(req)

@@ -1,0 +1,199 @@
+"""Run under mpiexec -n 1 or 2: persistent requests (MPI_Send_init /
+MPI_Ssend_init / MPI_Bsend_init / MPI_Rsend_init / MPI_Recv_init, MPI_Start /
+MPI_Startall) and the send modes (MPI_Ssend / MPI_Bsend / MPI_Rsend and their
+I-forms), which the reference does not interpose. Each rank sends to
+(rank + 1) % size and receives from (rank - 1) % size, so one rank exercises
+messages to itself. Every received byte is checked against the oracle.
+--device puts the strided buffers on the GPU. With TEMPI holding the
+persistent requests (a GPU, or TEMPI_TEST_HOST_ONLY) it also checks that a
+second MPI_Start of an active request is an error and that the starts were
+counted."""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), "..", ".."))
+sys.path.insert(0, ROOT)
+
+import tempi_amd  # noqa: E402
+from oracle import pyoracle  # noqa: E402
+from tests import typezoo  # noqa: E402
+
+device = "--device" in sys.argv
+mpi = tempi_amd.get_mpi()
+if device:
+    import torch
+
+    torch.cuda.set_device(0)
+mpi.Init()
+mpi.Comm_set_errhandler(mpi.ERRORS_RETURN)
+rank, size = mpi.Comm_rank(), mpi.Comm_size()
+peer, src = (rank + 1) % size, (rank - 1) % size
+recipe, count = "subarray(C,[40,38,512],[30,3,24],[5,3,24],byte)", 2  # 4320 packed bytes
+tm = pyoracle.TypeMap(recipe)
+origin, buflen = tm.geometry(count)
+t, temps, basic = typezoo.build(mpi, recipe)
+packed = mpi.Pack_size(count, t)
+tempi_holds = device or os.environ.get("TEMPI_TEST_HOST_ONLY") == "1"
+errors = 0
+mpi.Buffer_attach(8 * (packed + mpi.const("MPI_BSEND_OVERHEAD")) + 4096)
+mpi.reset_counters()
+
+
+def fail(msg):
+    global errors
+    errors += 1
+    print(f"[{rank}] {msg}", flush=True)
+
+
+def rand(seed):
+    return np.random.default_rng(seed).integers(0, 256, buflen, dtype=np.uint8)
+
+
+def buf(seed):
+    h = rand(seed)
+    return torch.from_numpy(h).cuda() if device else h
+
+
+def ptr(b):
+    return b.data_ptr() if device else b.ctypes.data
+
+
+def host(b):
+    if device:
+        torch.cuda.synchronize()
+        return b.cpu().numpy()
+    return b
+
+
+def refill(b, seed):
+    h = rand(seed)
+    if device:
+        b.copy_(torch.from_numpy(h))
+        torch.cuda.synchronize()
+    else:
+        b[:] = h
+
+
+def check(label, rbuf, canvas_seed, src_seed):
+    exp = rand(canvas_seed)
+    tm.unpack(tm.pack(rand(src_seed), origin, count), exp, origin, count)
+    if not np.array_equal(host(rbuf), exp):
+        fail(f"{label}: wrong bytes")
+
+
+# ---------------------------------------------------------------- persistent
+INITS = {"send": mpi.Send_init, "ssend": mpi.Ssend_init, "bsend": mpi.Bsend_init, "rsend": mpi.Rsend_init}
+for m, (mode, init) in enumerate(INITS.items()):
+    tag = 20 + m
+    dup = mpi.Type_dup(t)
+    mpi.Type_commit(dup)
+    sbuf, rbuf = buf(1), buf(2)
+    rreq = mpi.Recv_init(ptr(rbuf) + origin, count, dup, src, tag)
+    sreq = init(ptr(sbuf) + origin, count, dup, peer, tag)
+    mpi.Type_free(dup)  # the persistent requests keep what they need
+    for it in range(3):
+        refill(sbuf, 1000 * rank + 10 * it + m)
+        refill(rbuf, 500 + it)
+        r2 = mpi.Start(rreq)
+        mpi.Barrier()  # (ready mode: every receive is posted before its send starts)
+        s2 = mpi.Start(sreq)
+        assert r2 == rreq and s2 == sreq
+        r2, (s_src, s_tag, n) = mpi.Wait_status(rreq, t)
+        if r2 != rreq:
+            fail(f"{mode}: the wait released the persistent receive")
+        if (s_src, s_tag, n) != (src, tag, count):
+            fail(f"{mode} it {it}: status {(s_src, s_tag, n)} != {(src, tag, count)}")
+        if mpi.Wait(sreq) != sreq:
+            fail(f"{mode}: the wait released the persistent send")
+        check(f"{mode} it {it}", rbuf, 500 + it, 1000 * src + 10 * it + m)
+    # inactive: completes at once, skipped by the any / some family
+    flag, r2 = mpi.Test(rreq)
+    if not flag or r2 != rreq:
+        fail(f"{mode}: inactive test {flag} {r2}")
+    flag, st = mpi.Request_get_status(rreq, t)
+    if not flag:
+        fail(f"{mode}: inactive get_status not complete")
+    idx, flag, reqs = mpi.Testany([rreq, sreq])
+    if not flag or idx != mpi.UNDEFINED or reqs != [rreq, sreq]:
+        fail(f"{mode}: Testany over inactive requests gave {(idx, flag)}")
+    idx, reqs = mpi.Waitany([rreq, sreq])
+    if idx != mpi.UNDEFINED:
+        fail(f"{mode}: Waitany over inactive requests gave {idx}")
+    got, reqs = mpi.Testsome([rreq, sreq])
+    if got is not None:
+        fail(f"{mode}: Testsome over inactive requests gave {got}")
+    flag, reqs = mpi.Testall([rreq, sreq])
+    if not flag or reqs != [rreq, sreq]:
+        fail(f"{mode}: Testall over inactive requests gave {flag}")
+    # MPI_Startall + MPI_Waitall: the handles stay
+    refill(sbuf, 77 + rank)
+    refill(rbuf, 78)
+    rreq, = mpi.Startall([rreq])
+    mpi.Barrier()
+    reqs = mpi.Startall([sreq])
+    reqs = mpi.Waitall([rreq, sreq])
+    if reqs != [rreq, sreq]:
+        fail(f"{mode}: Waitall released persistent requests")
+    check(f"{mode} startall", rbuf, 78, 77 + src)
+    if mpi.Request_free(rreq) != mpi.REQUEST_NULL or mpi.Request_free(sreq) != mpi.REQUEST_NULL:
+        fail(f"{mode}: Request_free did not null the handle")
+    mpi.Barrier()
+
+# a started receive nothing matches: cancelled, the handle stays
+rbuf = buf(3)
+rreq = mpi.Recv_init(ptr(rbuf) + origin, count, t, src, 777)
+mpi.Start(rreq)
+if tempi_holds and mpi.Start_rc(rreq) == 0:
+    fail("a second MPI_Start of an active request succeeded")
+mpi.Cancel(rreq)
+r2, cancelled = mpi.Wait_cancelled(rreq)
+if not cancelled or r2 != rreq:
+    fail(f"cancel of a started persistent receive: cancelled={cancelled}")
+mpi.Request_free(rreq)
+mpi.Barrier()
+
+# a persistent host receive of a device send (a co-located device send may
+# travel as a descriptor, which the persistent receive must land)
+if device:
+    sbuf = buf(4)
+    refill(sbuf, 4000 + rank)
+    hrecv = rand(41)
+    rreq = mpi.Recv_init(hrecv.ctypes.data + origin, count, t, src, 30)
+    mpi.Start(rreq)
+    s = mpi.Isend(ptr(sbuf) + origin, count, t, peer, 30)
+    mpi.Wait(rreq)
+    mpi.Wait(s)
+    check("host persistent receive of a device send", hrecv, 41, 4000 + src)
+    mpi.Request_free(rreq)
+    mpi.Barrier()
+
+# ---------------------------------------------------------------- send modes
+for m, mode in enumerate(("ssend", "bsend", "rsend", "issend", "ibsend", "irsend")):
+    tag = 40 + m
+    sbuf, rbuf = buf(5), buf(6)
+    refill(sbuf, 3000 + 10 * rank + m)
+    r = mpi.Irecv(ptr(rbuf) + origin, count, t, src, tag)
+    mpi.Barrier()  # (ready mode)
+    fn = getattr(mpi, mode.capitalize())
+    s = fn(ptr(sbuf) + origin, count, t, peer, tag)
+    mpi.Wait(r)
+    if s is not None:
+        mpi.Wait(s)
+    check(mode, rbuf, 6, 3000 + 10 * src + m)
+    mpi.Barrier()
+
+c = mpi.counters()
+starts, sends = c["persistent_starts"], c["sends"]
+if tempi_holds and starts < 4 * 4:
+    fail(f"persistent_starts = {starts}")
+if device and sends < 6:
+    fail(f"device send modes not carried by TEMPI: sends = {sends}")
+mpi.Buffer_detach()
+typezoo.free(mpi, t, temps, basic)
+total = mpi.Allreduce_double(float(errors), op=mpi.SUM)
+if rank == 0:
+    print(f"RESULT errors={int(total)} persistent_starts={starts} sends={sends}", flush=True)
+mpi.Finalize()
+sys.exit(1 if total else 0)

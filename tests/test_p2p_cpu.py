@@ -41,6 +41,14 @@ def test_send_order_host(n):
     assert rc == 0 and "RESULT errors=0" in out, out[-3000:]
 
 
+@pytest.mark.parametrize("n", [1, 2])
+def test_persistent_and_send_modes_library(n):
+    """persistent requests and the send modes with TEMPI inactive (no GPU):
+    the library's, through the interposer unchanged"""
+    rc, out = mpi_launch.run(n, mpi_launch.py("persistent.py"), timeout=180)
+    assert rc == 0 and "RESULT errors=0" in out, out[-3000:]
+
+
 def test_completion_family_host():
     """MPI_Testall/Testany/Waitany/Testsome/Waitsome/Request_free through the
     interposer with host buffers (library requests only)."""
@@ -51,7 +59,8 @@ def test_completion_family_host():
 @pytest.mark.parametrize("n,prog", [(2, ("p2p_world.py",)), (2, ("alltoallv.py", "--nnz", "2", "--scale", "100")),
                                     (1, ("neighbor.py",)), (3, ("neighbor.py",)), (1, ("status.py",)),
                                     (2, ("status.py",)), (1, ("order.py",)), (2, ("order.py",)),
-                                    (2, ("completion.py",)), (1, ("probe_order.py",)), (2, ("probe_order.py",))])
+                                    (2, ("completion.py",)), (1, ("probe_order.py",)), (2, ("probe_order.py",)),
+                                    (1, ("persistent.py",)), (2, ("persistent.py",))])
 def test_tempi_host_paths_without_gpu(n, prog):
     """TEMPI's own host-side paths -- descriptor-aware host receives, the probe
     family and its held messages, send gates, host collectives -- which run

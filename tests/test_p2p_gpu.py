@@ -242,6 +242,17 @@ def test_completion_family_device(gpu, method):
     assert rc == 0 and "RESULT errors=0" in out, out[-3000:]
 
 
+@pytest.mark.parametrize("n,method", [(1, "AUTO"), (2, "AUTO"), (2, "ONESHOT"), (2, "IPC"), (2, "STAGED"),
+                                      (2, "XCOPY")])
+def test_persistent_and_send_modes_device(gpu, n, method):
+    """device objects through persistent requests (every init call, MPI_Start /
+    MPI_Startall, inactive requests in the completion family, cancel, a
+    persistent host receive of a device send) and MPI_Ssend / Bsend / Rsend /
+    Issend / Ibsend / Irsend; one rank sends to itself"""
+    rc, out = mpi_launch.run(n, mpi_launch.py("persistent.py", "--device"), env=METHODS[method], timeout=240)
+    assert rc == 0 and "RESULT errors=0" in out, out[-3000:]
+
+
 @pytest.mark.parametrize("env", [METHODS["XCOPY"], dict(METHODS["XCOPY"], TEMPI_FAULT_IPC_OPEN="1"),
                                  dict(METHODS["XCOPY"], TEMPI_STREAMS="3"),
                                  dict(METHODS["XCOPY"], TEMPI_FAKE_FOREIGN_GPU="1")],
