@@ -77,6 +77,7 @@ TEMPI_EXPORT void tempi_get_counters(tempi_counters_t *o) {
   o->sync_waits = c.sync_waits;
   o->ticket_batches = c.ticket_batches;
   o->persistent_starts = c.persistent_starts;
+  o->direct_pregathers = c.direct_pregathers;
 }
 
 TEMPI_EXPORT void tempi_reset_counters(void) {

@@ -141,6 +141,7 @@ struct DirectShared {
   DirectDesc desc{}; // the library's send buffer: alive until the receiver claims it
   enum State { PENDING, CLAIMED, PACKED, DONE } state = PENDING;
   Slab *slab = nullptr; // PACKED: the sender's gather (released by the receiver)
+  bool gathered = false; // PACKED: that gather's batch has been seen complete
   int device = 0;
   Op *sender = nullptr; // while the send is incomplete
 };
@@ -360,6 +361,13 @@ extern size_t firstFlush;      // TEMPI_FIRST_FLUSH: the same while no scatter b
 extern int scattersInFlight;   // scatter / copy batches launched and not yet seen complete
 extern bool eagerFlush;        // TEMPI_EAGER_FLUSH (A/B)
 extern bool batchTickets;      // !TEMPI_NO_BATCH_TICKET: batches complete by a folded ticket when they can
+// Pre-gather (TEMPI_PREGATHER_BYTES, 0 = off): a direct send to this process
+// whose receive is not posted yet, of rows <= pregatherMaxBlock bytes, is
+// gathered into a slab at once while no scatter batch is in flight (the GPU
+// would idle through a send burst), up to pregatherBytes per burst; queued
+// pre-gathers launch every pregatherFlush bytes
+extern int64_t pregatherBytes, pregatherMaxBlock, pregatherFlush;
+extern int64_t pregatherUsed, pregatherQueued;
 void flush_list(PendingList &list, bool pack);
 void flush();
 

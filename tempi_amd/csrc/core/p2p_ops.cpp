@@ -163,6 +163,8 @@ size_t firstFlush = 16;
 int scattersInFlight = 0;
 bool eagerFlush = false;
 bool batchTickets = true;
+int64_t pregatherBytes = 0, pregatherMaxBlock = 64, pregatherFlush = int64_t(4) << 20;
+int64_t pregatherUsed = 0, pregatherQueued = 0;
 
 namespace {
 template <typename T> const T *select(const std::vector<T> &v, const std::vector<int> &dev, int d, bool all,
@@ -238,7 +240,10 @@ void flush_list(PendingList &list, bool pack) {
     b->lane = lane;
     b->scatter = !pack;
     b->stream = s;
-    if (!pack) ++scattersInFlight;
+    if (!pack) {
+      ++scattersInFlight;
+      pregatherUsed = 0; // the receives have come: the next send burst has its own budget
+    }
     if (flag) {
       counters.ticket_batches++;
       b->flag = flag;
@@ -398,6 +403,13 @@ struct IsendDirectOp : Op {
   MPI_Comm comm;
   void post() override {
     if (self_send(sh, comm, tag)) {
+      if (sh->state == DirectShared::PENDING && pregatherBytes > 0 && scattersInFlight == 0 &&
+          rec->desc.block <= pregatherMaxBlock && pregatherUsed + bytes <= pregatherBytes) {
+        pregatherUsed += bytes;
+        pregatherQueued += bytes;
+        counters.direct_pregathers++;
+        gather();
+      }
       maybe_done();
       return;
     }
@@ -418,6 +430,7 @@ struct IsendDirectOp : Op {
   }
   void gpu_done() override {
     packDone = true;
+    sh->gathered = true;
     maybe_done();
   }
   void peer_done() override { maybe_done(); }
@@ -426,6 +439,9 @@ struct IsendDirectOp : Op {
     // waited on before its receive exists: gather into a slab the receiver
     // will unpack, so the send can complete on its own
     counters.direct_fallbacks++;
+    gather();
+  }
+  void gather() {
     sh->state = DirectShared::PACKED;
     sh->slab = device_pool().get(size_t(bytes), device);
     pendingPack.add_items(this, *rec->packer, sh->slab->dev, origin, count);

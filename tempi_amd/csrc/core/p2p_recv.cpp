@@ -188,8 +188,9 @@ struct IrecvOp : Op {
         pendingUnpack.add_copy(this, c);
       } else if (direct->state == DirectShared::PACKED && sameDevice) {
         // the sender's gather runs on lane 0: so does this scatter, after it
+        // (unless that gather is already seen complete)
         pendingUnpack.add_items(this, packer, direct->slab->dev, origin, elems);
-        pendingUnpack.afterPack = true;
+        if (!direct->gathered) pendingUnpack.afterPack = true;
       } else { // another device, or a shape the copy kernel does not take
         if (!hslab) hslab = pinned_pool().get(std::max<size_t>(size_t(bytes), kDescCap), device);
         const DirectDesc copy = dd; // (materialise_direct releases the shared state)

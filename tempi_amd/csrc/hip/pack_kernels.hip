@@ -679,7 +679,10 @@ template <int W, int ND> __global__ __launch_bounds__(kBlock) void unpack_il_ker
 // inside it is shorter than 64 bytes between two payload bytes, so no byte
 // outside pages the type already touches is read. Byte-for-byte identical to
 // pack_body (type-map order).
-constexpr int kDenseRatio = 4;
+#ifndef TEMPI_DENSE_RATIO
+#define TEMPI_DENSE_RATIO 4
+#endif
+constexpr int kDenseRatio = TEMPI_DENSE_RATIO;
 constexpr int kDenseLds = kBlock * 16 * kDenseRatio + 512;
 constexpr int kDenseMaxBlock = 32;
 // a workgroup's window must fit the CU's 160 KiB of LDS with room for a
@@ -1115,7 +1118,7 @@ bool dense_ok(const Norm &n, int w) {
   // sector bound on the per-word path, and wider windows lose
   if (!TEMPI_DENSE || w > 2 || n.nd < 1 || n.block > kDenseMaxBlock) return false;
   const int64_t s = n.str[n.nd - 1], b = n.block; // innermost dimension
-  if (s <= 0 || s > kDenseRatio * b) return false;
+  if (s <= 0 || s > kDenseRatio * b || s - b >= 64) return false; // (gaps inside sectors the type touches)
   // outer dimensions: inner segments long enough that few tiles straddle two
   return n.nd == 1 || n.cnt[n.nd - 1] * b >= 4 * 4096;
 }

@@ -4,9 +4,11 @@ of messages for every (sender, receiver) pair, the receiver included:
 strided or irregular types, counts from tiny to past the 128 KiB IPC COPY
 limit, narrow and wide rows, device or host buffers on either side, tags from
 a small set (so MPI's non-overtaking order between messages with one tag is
-exercised). Every rank posts its receives and sends in a random interleaving,
-waits for all with one MPI_Waitall, and checks every received byte against
-the oracle.  usage: fuzz.py [rounds] [seed]"""
+exercised), send modes (MPI_Isend / MPI_Issend / MPI_Ibsend, and persistent
+MPI_Send_init + MPI_Start) and receive kinds (MPI_Irecv, persistent
+MPI_Recv_init + MPI_Start). Every rank posts its receives and sends in a
+random interleaving, waits for all with one MPI_Waitall, and checks every
+received byte against the oracle.  usage: fuzz.py [rounds] [seed]"""
 import os
 import random
 import sys
@@ -26,6 +28,7 @@ torch.cuda.set_device(0)
 mpi = tempi_amd.get_mpi()
 mpi.Init()
 rank, size = mpi.Comm_rank(), mpi.Comm_size()
+mpi.Buffer_attach(256 << 20)  # (MPI_Ibsend: every round's buffered sends fit)
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 6
 seed0 = int(sys.argv[2]) if len(sys.argv) > 2 else 7
 errors = 0
@@ -50,11 +53,12 @@ def plan(rnd, src, dst):
         ti = rng.randrange(len(RECIPES))
         count = rng.choice([1, 2, 3, 9, 40]) if ti != 3 else rng.choice([1, 8, 40])
         sdev = rng.random() < 0.85
-        # a non-blocking host receive of a TEMPI device send is unsupported
-        # (INTEGRATION.md): host receives only meet host sends
-        rdev = True if sdev else rng.random() < 0.5
+        # (host receives of device sends: descriptors landed by the host receive)
+        rdev = rng.random() < (0.8 if sdev else 0.5)
+        smode = rng.choice(["isend", "isend", "issend", "ibsend", "persist"])
+        rkind = rng.choice(["irecv", "irecv", "persist"])
         msgs.append(dict(ti=ti, count=count, tag=rng.choice([3, 4]), sdev=sdev, rdev=rdev,
-                         seed=rng.randrange(1 << 30)))
+                         seed=rng.randrange(1 << 30), smode=smode, rkind=rkind))
     return msgs
 
 
@@ -75,7 +79,7 @@ for rnd in range(rounds):
             origin, n = tm.geometry(m["count"])
             _, b = buffer(n, m["seed"], m["sdev"])
             keep.append(b)
-            ops.append(("send", addr(b) + origin, m["count"], TYPES[m["ti"]][0], dst, m["tag"]))
+            ops.append((m["smode"], addr(b) + origin, m["count"], TYPES[m["ti"]][0], dst, m["tag"]))
     recvs_by_src = []
     for src in range(size):
         for m in plan(rnd, src, rank):
@@ -86,7 +90,8 @@ for rnd in range(rounds):
             exp = canvas.copy()
             tm.unpack(tm.pack(src_bytes, origin, m["count"]), exp, origin, m["count"])
             keep.append(b)
-            recvs_by_src.append(("recv", addr(b) + origin, m["count"], TYPES[m["ti"]][0], src, m["tag"]))
+            recvs_by_src.append(("recv_" + m["rkind"], addr(b) + origin, m["count"], TYPES[m["ti"]][0], src,
+                                 m["tag"]))
             checks.append((b, exp, f"round {rnd} {RECIPES[m['ti']][:22]} x{m['count']} from {src} tag {m['tag']}"))
     # a random interleaving that keeps each list's own order (MPI order per
     # (peer, tag) is what the messages are matched by)
@@ -100,13 +105,27 @@ for rnd in range(rounds):
             seq.append(recvs_by_src[j])
             j += 1
     torch.cuda.synchronize()
-    reqs = []
+    reqs, persistent = [], []
     for kind, p, count, t, peer, tag in seq:
-        if kind == "send":
+        if kind == "isend":
             reqs.append(mpi.Isend(p, count, t, peer, tag))
+        elif kind == "issend":
+            reqs.append(mpi.Issend(p, count, t, peer, tag))
+        elif kind == "ibsend":
+            reqs.append(mpi.Ibsend(p, count, t, peer, tag))
+        elif kind == "persist":
+            r = mpi.Send_init(p, count, t, peer, tag)
+            persistent.append(r)
+            reqs.append(mpi.Start(r))
+        elif kind == "recv_persist":
+            r = mpi.Recv_init(p, count, t, peer, tag)
+            persistent.append(r)
+            reqs.append(mpi.Start(r))
         else:
             reqs.append(mpi.Irecv(p, count, t, peer, tag))
     mpi.Waitall(reqs)
+    for r in persistent:
+        mpi.Request_free(r)
     torch.cuda.synchronize()
     for b, exp, what in checks:
         got = b.cpu().numpy() if isinstance(b, torch.Tensor) else b
@@ -117,6 +136,7 @@ for rnd in range(rounds):
 
 for t in TYPES:
     typezoo.free(mpi, *t)
+mpi.Buffer_detach()
 c = mpi.counters()
 print(f"rank {rank} routes: direct={c['send_direct']} ipc={c['send_ipc']} copy={c['send_ipc_copy']} "
       f"oneshot={c['send_oneshot']} lib={c['lib_sends']}", flush=True)
