@@ -34,6 +34,7 @@
 #include <hip/hip_runtime.h>
 
 #include "tempi_hip.h"
+#include "aql.hpp"
 #include "ticket.hpp"
 
 #include <cstdint>
@@ -934,6 +935,27 @@ thread_local uint32_t gItemFlags = 0;
 // the completion-ticket fold offered to this thread's next single-object
 // launch (the *_ticket entry points set it around their launch)
 thread_local tempi_ticket::Fold *gFold = nullptr;
+// the AQL queue this thread's next folded single-object launch is dispatched
+// on instead of its stream (with_ticket sets it; aql.hpp)
+thread_local tempi_aql::Queue *gAql = nullptr;
+bool gAqlAllowed = true; // tempi_hip_aql_allow: off while HIP events time the launches
+
+// launch `kernel` (a, sg) over `blocks` workgroups of kBlock lanes: on the
+// AQL queue when one is offered and the launch stores the ticket itself,
+// else on stream s
+template <typename A>
+void launch_ks(void (*kernel)(const A, const Sig), uint32_t blocks, hipStream_t s, const A &a, const Sig &sg) {
+  if (gAql && sg.flag) {
+    struct P {
+      A a;
+      Sig sg;
+    } p{a, sg};
+    if (tempi_aql::dispatch(gAql, reinterpret_cast<const void *>(kernel), s, blocks, kBlock, &p,
+                            offsetof(P, sg) + sizeof(Sig)))
+      return;
+  }
+  hipLaunchKernelGGL(kernel, dim3(blocks), dim3(kBlock), 0, s, a, sg);
+}
 
 // a 16-byte-word scatter may store write-through (st_scatter): every stride
 // >= 0 and the object's span below 2 GiB
@@ -1010,9 +1032,9 @@ int launch_nd(bool pack, char *packed, char *first, const Norm &n, hipStream_t s
   const Sig sg = take_fold(blocks, wt);
   if (sg.flag && wt) a.flags |= kWriteThrough;
   if (pack)
-    hipLaunchKernelGGL((pack_kernel<W, ND>), dim3(blocks), dim3(kBlock), 0, s, a, sg);
+    launch_ks<KArgs<ND>>(pack_kernel<W, ND>, blocks, s, a, sg);
   else
-    hipLaunchKernelGGL((unpack_kernel<W, ND>), dim3(blocks), dim3(kBlock), 0, s, a, sg);
+    launch_ks<KArgs<ND>>(unpack_kernel<W, ND>, blocks, s, a, sg);
   return int(hipGetLastError());
 }
 
@@ -1130,7 +1152,7 @@ template <int ND> int launch_dense_nd(char *packed, char *first, const Norm &n, 
   if (blocks == 0) return 0;
   const Sig sg = take_fold(blocks, true);
   if (sg.flag) a.flags |= kWriteThrough;
-  hipLaunchKernelGGL((pack_dense_kernel<ND>), dim3(blocks), dim3(kBlock), 0, s, a, sg);
+  launch_ks<KArgs<ND>>(pack_dense_kernel<ND>, blocks, s, a, sg);
   return int(hipGetLastError());
 }
 
@@ -1155,9 +1177,9 @@ template <int W, int ND> int launch_il_nd(bool pack, char *packed, char *first, 
   const Sig sg = take_fold(blocks, pack);
   if (sg.flag && pack) a.flags |= kWriteThrough;
   if (pack)
-    hipLaunchKernelGGL((pack_il_kernel<W, ND>), dim3(blocks), dim3(kBlock), 0, s, a, sg);
+    launch_ks<KArgs<ND>>(pack_il_kernel<W, ND>, blocks, s, a, sg);
   else
-    hipLaunchKernelGGL((unpack_il_kernel<W, ND>), dim3(blocks), dim3(kBlock), 0, s, a, sg);
+    launch_ks<KArgs<ND>>(unpack_il_kernel<W, ND>, blocks, s, a, sg);
   return int(hipGetLastError());
 }
 
@@ -1641,7 +1663,14 @@ int with_ticket(bool pack, char *packed, char *first, const tempi_hip_desc *d, h
   bool single = norm_bytes(n) < kMaxLaunchBytes; // launch_split makes exactly one launch
   for (int k = 0; k < n.nd; ++k) single &= n.cnt[k] < (int64_t(1) << 32);
   std::lock_guard<std::mutex> lock(tempi_ticket::mutex());
-  tempi_ticket::Ticket *t = tempi_ticket::of(s);
+  // one launch that stores its own ticket may go to the AQL queue (aql.hpp);
+  // the call then completes on that queue's ticket, whichever way it launched
+  tempi_aql::Queue *aq = single && gAqlAllowed ? tempi_aql::for_stream(s) : nullptr;
+  tempi_ticket::Ticket *t = aq ? tempi_ticket::of_aql(aq, s) : nullptr;
+  if (!t) {
+    aq = nullptr;
+    t = tempi_ticket::of(s);
+  }
   if (!t) return int(hipErrorOutOfMemory);
   tempi_ticket::Fold fold;
   fold.t = t;
@@ -1649,8 +1678,10 @@ int with_ticket(bool pack, char *packed, char *first, const tempi_hip_desc *d, h
   fold.max_blocks = single ? tempi_ticket::fold_max_blocks() : 0;
   fold.max_blocks_wt = single ? tempi_ticket::fold_max_blocks_wt() : 0;
   gFold = &fold;
+  gAql = aq;
   const int e = launch_split(pack, packed, first, n, s);
   gFold = nullptr;
+  gAql = nullptr;
   if (e) {
     if (fold.taken) t->broken = true; // the host counted a launch that never ran
     return e;
@@ -1693,6 +1724,17 @@ template <typename F> int batch_with_ticket(hipStream_t s, const uint32_t **flag
 } // namespace
 
 extern "C" {
+
+void tempi_hip_aql_allow(int on) {
+  std::lock_guard<std::mutex> lock(tempi_ticket::mutex());
+  gAqlAllowed = on != 0;
+}
+
+void tempi_hip_aql_stats(uint64_t *dispatched, uint64_t *refused) {
+  const tempi_aql::Stats st = tempi_aql::stats();
+  *dispatched = st.dispatched;
+  *refused = st.refused;
+}
 
 int tempi_hip_pack_ticket(void *packed, const void *first, const tempi_hip_desc *d, void *stream,
                           const uint32_t **flag, uint32_t *ticket) {
