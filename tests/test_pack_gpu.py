@@ -679,6 +679,9 @@ def test_synchronous_ticket_visible_device_wide(mpi, gpu, rows, block, stride, f
         mpi.Type_free(t)
 
 
+@pytest.mark.skipif(os.environ.get("TEMPI_TEST_AQL") != "1",
+                    reason="TEMPI_AQL is opt-in and not yet run on this pool's GPUs (DESIGN §6): "
+                           "set TEMPI_TEST_AQL=1 (tools/gpu_aql_session.sh does)")
 def test_synchronous_calls_through_aql_packets(gpu):
     """TEMPI_AQL=1: synchronous MPI_Pack / MPI_Unpack launched by TEMPI's own
     AQL dispatch packets (hip/aql.hpp), every result visible device-wide right

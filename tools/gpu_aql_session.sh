@@ -12,7 +12,7 @@ echo "== probe"
 timeout -k 10 90 tools/_variants/aqlbench tools/_variants/aqlbench.hsaco 2000 > $O/aql.jsonl 2> $O/aql.err
 rc=$?; cat $O/aql.err $O/aql.jsonl; [ $rc -eq 0 ] || exit $rc
 echo "== aql test"
-timeout -k 10 300 python -u -m pytest tests/test_pack_gpu.py -q -x --timeout 200 --timeout-method thread -k aql \
+TEMPI_TEST_AQL=1 timeout -k 10 300 python -u -m pytest tests/test_pack_gpu.py -q -x --timeout 200 --timeout-method thread -k aql \
   > $O/aql_test.log 2>&1
 rc=$?; tail -n 5 $O/aql_test.log; [ $rc -eq 0 ] || exit $rc
 echo "== config 1 A/B"
