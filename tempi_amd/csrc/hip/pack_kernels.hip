@@ -940,18 +940,24 @@ thread_local tempi_ticket::Fold *gFold = nullptr;
 thread_local tempi_aql::Queue *gAql = nullptr;
 bool gAqlAllowed = true; // tempi_hip_aql_allow: off while HIP events time the launches
 
+// a kernel's (A a, Sig sg) arguments as the host lays them out for an AQL
+// packet: a at 0, sg behind it at its alignment (the kernel ABI's by-value
+// layout; tests/test_aql_layout_cpu.py checks it against the code object)
+template <typename A> struct KernelArgs {
+  A a;
+  Sig sg;
+  static constexpr size_t bytes() { return offsetof(KernelArgs, sg) + sizeof(Sig); }
+};
+
 // launch `kernel` (a, sg) over `blocks` workgroups of kBlock lanes: on the
 // AQL queue when one is offered and the launch stores the ticket itself,
 // else on stream s
 template <typename A>
 void launch_ks(void (*kernel)(const A, const Sig), uint32_t blocks, hipStream_t s, const A &a, const Sig &sg) {
   if (gAql && sg.flag) {
-    struct P {
-      A a;
-      Sig sg;
-    } p{a, sg};
+    const KernelArgs<A> p{a, sg};
     if (tempi_aql::dispatch(gAql, reinterpret_cast<const void *>(kernel), s, blocks, kBlock, &p,
-                            offsetof(P, sg) + sizeof(Sig)))
+                            KernelArgs<A>::bytes()))
       return;
   }
   hipLaunchKernelGGL(kernel, dim3(blocks), dim3(kBlock), 0, s, a, sg);
@@ -1728,6 +1734,18 @@ extern "C" {
 void tempi_hip_aql_allow(int on) {
   std::lock_guard<std::mutex> lock(tempi_ticket::mutex());
   gAqlAllowed = on != 0;
+}
+
+int64_t tempi_hip_aql_arg_bytes(int nd) {
+  switch (nd) {
+  case 0: return int64_t(KernelArgs<KArgs<0>>::bytes());
+  case 1: return int64_t(KernelArgs<KArgs<1>>::bytes());
+  case 2: return int64_t(KernelArgs<KArgs<2>>::bytes());
+  case 3: return int64_t(KernelArgs<KArgs<3>>::bytes());
+  case 4: return int64_t(KernelArgs<KArgs<4>>::bytes());
+  case 5: return int64_t(KernelArgs<KArgs<5>>::bytes());
+  default: return -1;
+  }
 }
 
 void tempi_hip_aql_stats(uint64_t *dispatched, uint64_t *refused) {

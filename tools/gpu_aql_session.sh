@@ -7,10 +7,17 @@
 # persistent-request GPU tests. gpurun_out/aql.jsonl, aql_ab.jsonl.
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp HYDRA_LAUNCHER=fork
-O=gpurun_out; mkdir -p $O
+O=gpurun_out; mkdir -p $O; : > $O/aql_sync.jsonl
 echo "== probe"
 timeout -k 10 90 tools/_variants/aqlbench tools/_variants/aqlbench.hsaco 2000 > $O/aql.jsonl 2> $O/aql.err
 rc=$?; cat $O/aql.err $O/aql.jsonl; [ $rc -eq 0 ] || exit $rc
+echo "== syncbench (C ABI): HIP launches vs TEMPI_AQL=1"
+for v in hip aql; do
+  E="TEMPI_X=1"; [ $v = aql ] && E="TEMPI_AQL=1"
+  env $E timeout -k 10 60 tools/_variants/syncbench tempi_amd/lib/libtempi_hip.so 2000 \
+    | sed "s/^{/{\"variant\": \"$v\", /" >> $O/aql_sync.jsonl || exit 5
+done
+grep -o '"variant": "[a-z]*", "shape": "[^"]*".*"ticket_fold_us": [0-9.]*' $O/aql_sync.jsonl | sed 's/"packed.*"ticket_fold_us"/ fold_us/'
 echo "== aql test"
 TEMPI_TEST_AQL=1 timeout -k 10 300 python -u -m pytest tests/test_pack_gpu.py -q -x --timeout 200 --timeout-method thread -k aql \
   > $O/aql_test.log 2>&1
