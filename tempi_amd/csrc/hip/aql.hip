@@ -106,6 +106,40 @@ hsa_status_t find_kernarg(hsa_region_t r, void *d) {
   return HSA_STATUS_SUCCESS;
 }
 
+// a device-memory pool the CPU may be given access to (kernel arguments the
+// host writes through the BAR, read by the GPU from its own memory)
+struct PoolFind {
+  hsa_amd_memory_pool_t pool{};
+  bool found = false;
+};
+
+hsa_status_t find_device_pool(hsa_amd_memory_pool_t p, void *d) {
+  auto *f = static_cast<PoolFind *>(d);
+  hsa_amd_segment_t seg;
+  if (hsa_amd_memory_pool_get_info(p, HSA_AMD_MEMORY_POOL_INFO_SEGMENT, &seg) != HSA_STATUS_SUCCESS ||
+      seg != HSA_AMD_SEGMENT_GLOBAL)
+    return HSA_STATUS_SUCCESS;
+  uint32_t flags = 0;
+  bool alloc = false;
+  hsa_amd_memory_pool_get_info(p, HSA_AMD_MEMORY_POOL_INFO_GLOBAL_FLAGS, &flags);
+  hsa_amd_memory_pool_get_info(p, HSA_AMD_MEMORY_POOL_INFO_RUNTIME_ALLOC_ALLOWED, &alloc);
+  if (alloc && (flags & HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_FINE_GRAINED)) {
+    f->pool = p;
+    f->found = true;
+    return HSA_STATUS_INFO_BREAK;
+  }
+  return HSA_STATUS_SUCCESS;
+}
+
+hsa_status_t find_cpu(hsa_agent_t a, void *d) {
+  hsa_device_type_t t;
+  if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) == HSA_STATUS_SUCCESS && t == HSA_DEVICE_TYPE_CPU) {
+    *static_cast<hsa_agent_t *>(d) = a;
+    return HSA_STATUS_INFO_BREAK;
+  }
+  return HSA_STATUS_SUCCESS;
+}
+
 struct SymFind {
   const char *name;
   hsa_agent_t agent;
@@ -131,6 +165,7 @@ struct Queue {
   hsa_agent_t agent{};
   hsa_queue_t *q = nullptr;
   char *kargs = nullptr; // kQueueSize slots of kSlot bytes, kernarg memory
+  bool deviceKargs = false; // kargs in device memory (TEMPI_AQL_DEVICE_KERNARG=1)
   std::unordered_map<const void *, Kernel> kernels;
 };
 
@@ -159,7 +194,23 @@ Queue *make_queue(int dev) {
                        &q) != HSA_STATUS_SUCCESS)
     return nullptr;
   void *k = nullptr;
-  if (hsa_memory_allocate(f.kernarg, size_t(q->size) * kSlot, &k) != HSA_STATUS_SUCCESS) {
+  bool deviceKargs = false;
+  if (std::getenv("TEMPI_AQL_DEVICE_KERNARG")) {
+    PoolFind pf;
+    hsa_agent_t cpu{};
+    hsa_amd_agent_iterate_memory_pools(f.agent, find_device_pool, &pf);
+    hsa_iterate_agents(find_cpu, &cpu);
+    if (pf.found && cpu.handle &&
+        hsa_amd_memory_pool_allocate(pf.pool, size_t(q->size) * kSlot, 0, &k) == HSA_STATUS_SUCCESS) {
+      if (hsa_amd_agents_allow_access(1, &cpu, nullptr, k) == HSA_STATUS_SUCCESS) {
+        deviceKargs = true;
+      } else {
+        hsa_amd_memory_pool_free(k);
+        k = nullptr;
+      }
+    }
+  }
+  if (!k && hsa_memory_allocate(f.kernarg, size_t(q->size) * kSlot, &k) != HSA_STATUS_SUCCESS) {
     hsa_queue_destroy(q);
     return nullptr;
   }
@@ -169,6 +220,7 @@ Queue *make_queue(int dev) {
   Q->agent = f.agent;
   Q->q = q;
   Q->kargs = static_cast<char *>(k);
+  Q->deviceKargs = deviceKargs;
   return Q;
 }
 
@@ -254,6 +306,10 @@ bool dispatch(Queue *Q, const void *kernel, hipStream_t s, uint32_t blocks, uint
     std::memcpy(h, count, sizeof count);
     std::memcpy(h + kGroupSizeAt, size, sizeof size);
     std::memcpy(h + kGridDimsAt, &dims, sizeof dims); // (remainders and global offsets stay 0)
+  }
+  if (Q->deviceKargs) { // the writes through the BAR land before the packet becomes valid
+    __atomic_thread_fence(__ATOMIC_SEQ_CST);
+    (void)*reinterpret_cast<volatile char *>(ka + k->kargSize - 1);
   }
   auto *pkt = static_cast<hsa_kernel_dispatch_packet_t *>(q->base_address) + (idx % q->size);
   pkt->workgroup_size_x = uint16_t(wg);

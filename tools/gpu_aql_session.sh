@@ -12,8 +12,8 @@ echo "== probe"
 timeout -k 10 90 tools/_variants/aqlbench tools/_variants/aqlbench.hsaco 2000 > $O/aql.jsonl 2> $O/aql.err
 rc=$?; cat $O/aql.err $O/aql.jsonl; [ $rc -eq 0 ] || exit $rc
 echo "== syncbench (C ABI): HIP launches vs TEMPI_AQL=1"
-for v in hip aql; do
-  E="TEMPI_X=1"; [ $v = aql ] && E="TEMPI_AQL=1"
+for v in hip aql aqldev; do
+  E="TEMPI_X=1"; [ $v = aql ] && E="TEMPI_AQL=1"; [ $v = aqldev ] && E="TEMPI_AQL=1 TEMPI_AQL_DEVICE_KERNARG=1"
   env $E timeout -k 10 60 tools/_variants/syncbench tempi_amd/lib/libtempi_hip.so 2000 \
     | sed "s/^{/{\"variant\": \"$v\", /" >> $O/aql_sync.jsonl || exit 5
 done
@@ -25,8 +25,8 @@ rc=$?; tail -n 5 $O/aql_test.log; [ $rc -eq 0 ] || exit $rc
 echo "== config 1 A/B"
 OUT=$O/aql_ab.jsonl; : > $OUT
 for r in 1 2 3; do
-  for v in hip aql; do
-    E="TEMPI_X=1"; [ $v = aql ] && E="TEMPI_AQL=1"
+  for v in hip aql aqldev; do
+    E="TEMPI_X=1"; [ $v = aql ] && E="TEMPI_AQL=1"; [ $v = aqldev ] && E="TEMPI_AQL=1 TEMPI_AQL_DEVICE_KERNARG=1"
     env $E TEMPI_PRINT_COUNTERS=1 timeout -k 10 60 /opt/conda/bin/mpiexec -n 1 tempi_amd/lib/mpi_pack 1000 --shape 1024:512:1024 --pin \
       2>> $O/aql_ab.err | sed "s/^{/{\"round\": $r, \"bench\": \"config1\", \"variant\": \"$v\", /" >> $OUT || exit 4
     env $E timeout -k 10 60 /opt/conda/bin/mpiexec -n 1 tempi_amd/lib/mpi_pack 1000 --shape 2:512:1024 --pin \
