@@ -949,18 +949,15 @@ template <typename A> struct KernelArgs {
   static constexpr size_t bytes() { return offsetof(KernelArgs, sg) + sizeof(Sig); }
 };
 
-// launch `kernel` (a, sg) over `blocks` workgroups of kBlock lanes: on the
-// AQL queue when one is offered and the launch stores the ticket itself,
-// else on stream s
+// dispatch `kernel` (a, sg) over `blocks` workgroups of kBlock lanes on the
+// AQL queue when one is offered and the launch stores the ticket itself;
+// false: the caller launches it on its stream as usual
 template <typename A>
-void launch_ks(void (*kernel)(const A, const Sig), uint32_t blocks, hipStream_t s, const A &a, const Sig &sg) {
-  if (gAql && sg.flag) {
-    const KernelArgs<A> p{a, sg};
-    if (tempi_aql::dispatch(gAql, reinterpret_cast<const void *>(kernel), s, blocks, kBlock, &p,
-                            KernelArgs<A>::bytes()))
-      return;
-  }
-  hipLaunchKernelGGL(kernel, dim3(blocks), dim3(kBlock), 0, s, a, sg);
+bool aql_launch(void (*kernel)(const A, const Sig), uint32_t blocks, hipStream_t s, const A &a, const Sig &sg) {
+  if (!gAql || !sg.flag) return false;
+  const KernelArgs<A> p{a, sg};
+  return tempi_aql::dispatch(gAql, reinterpret_cast<const void *>(kernel), s, blocks, kBlock, &p,
+                             KernelArgs<A>::bytes());
 }
 
 // a 16-byte-word scatter may store write-through (st_scatter): every stride
@@ -1037,10 +1034,12 @@ int launch_nd(bool pack, char *packed, char *first, const Norm &n, hipStream_t s
   const bool wt = pack || (W == 16 && scatter_write_through(n));
   const Sig sg = take_fold(blocks, wt);
   if (sg.flag && wt) a.flags |= kWriteThrough;
-  if (pack)
-    launch_ks<KArgs<ND>>(pack_kernel<W, ND>, blocks, s, a, sg);
-  else
-    launch_ks<KArgs<ND>>(unpack_kernel<W, ND>, blocks, s, a, sg);
+  if (pack) {
+    if (!aql_launch<KArgs<ND>>(pack_kernel<W, ND>, blocks, s, a, sg))
+      hipLaunchKernelGGL((pack_kernel<W, ND>), dim3(blocks), dim3(kBlock), 0, s, a, sg);
+  } else if (!aql_launch<KArgs<ND>>(unpack_kernel<W, ND>, blocks, s, a, sg)) {
+    hipLaunchKernelGGL((unpack_kernel<W, ND>), dim3(blocks), dim3(kBlock), 0, s, a, sg);
+  }
   return int(hipGetLastError());
 }
 
@@ -1158,7 +1157,8 @@ template <int ND> int launch_dense_nd(char *packed, char *first, const Norm &n, 
   if (blocks == 0) return 0;
   const Sig sg = take_fold(blocks, true);
   if (sg.flag) a.flags |= kWriteThrough;
-  launch_ks<KArgs<ND>>(pack_dense_kernel<ND>, blocks, s, a, sg);
+  if (!aql_launch<KArgs<ND>>(pack_dense_kernel<ND>, blocks, s, a, sg))
+    hipLaunchKernelGGL((pack_dense_kernel<ND>), dim3(blocks), dim3(kBlock), 0, s, a, sg);
   return int(hipGetLastError());
 }
 
@@ -1182,10 +1182,12 @@ template <int W, int ND> int launch_il_nd(bool pack, char *packed, char *first, 
   a.flags |= xcd_flag(first, n, pack);
   const Sig sg = take_fold(blocks, pack);
   if (sg.flag && pack) a.flags |= kWriteThrough;
-  if (pack)
-    launch_ks<KArgs<ND>>(pack_il_kernel<W, ND>, blocks, s, a, sg);
-  else
-    launch_ks<KArgs<ND>>(unpack_il_kernel<W, ND>, blocks, s, a, sg);
+  if (pack) {
+    if (!aql_launch<KArgs<ND>>(pack_il_kernel<W, ND>, blocks, s, a, sg))
+      hipLaunchKernelGGL((pack_il_kernel<W, ND>), dim3(blocks), dim3(kBlock), 0, s, a, sg);
+  } else if (!aql_launch<KArgs<ND>>(unpack_il_kernel<W, ND>, blocks, s, a, sg)) {
+    hipLaunchKernelGGL((unpack_il_kernel<W, ND>), dim3(blocks), dim3(kBlock), 0, s, a, sg);
+  }
   return int(hipGetLastError());
 }
 

@@ -4,11 +4,12 @@ of messages for every (sender, receiver) pair, the receiver included:
 strided or irregular types, counts from tiny to past the 128 KiB IPC COPY
 limit, narrow and wide rows, device or host buffers on either side, tags from
 a small set (so MPI's non-overtaking order between messages with one tag is
-exercised), send modes (MPI_Isend / MPI_Issend / MPI_Ibsend, and persistent
-MPI_Send_init + MPI_Start) and receive kinds (MPI_Irecv, persistent
-MPI_Recv_init + MPI_Start). Every rank posts its receives and sends in a
-random interleaving, waits for all with one MPI_Waitall, and checks every
-received byte against the oracle.  usage: fuzz.py [rounds] [seed]"""
+exercised). With --modes, also send modes (MPI_Isend / MPI_Issend /
+MPI_Ibsend, and persistent MPI_Send_init + MPI_Start), receive kinds
+(MPI_Irecv, persistent MPI_Recv_init + MPI_Start) and host receives of
+device sends. Every rank posts its receives and sends in a random
+interleaving, waits for all with one MPI_Waitall, and checks every received
+byte against the oracle.  usage: fuzz.py [rounds] [seed] [--modes]"""
 import os
 import random
 import sys
@@ -28,9 +29,12 @@ torch.cuda.set_device(0)
 mpi = tempi_amd.get_mpi()
 mpi.Init()
 rank, size = mpi.Comm_rank(), mpi.Comm_size()
-mpi.Buffer_attach(256 << 20)  # (MPI_Ibsend: every round's buffered sends fit)
-rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 6
-seed0 = int(sys.argv[2]) if len(sys.argv) > 2 else 7
+if modes:
+    mpi.Buffer_attach(256 << 20)  # (MPI_Ibsend: every round's buffered sends fit)
+modes = "--modes" in sys.argv
+argv = [a for a in sys.argv[1:] if a != "--modes"]
+rounds = int(argv[0]) if len(argv) > 0 else 6
+seed0 = int(argv[1]) if len(argv) > 1 else 7
 errors = 0
 
 # (recipe, element bytes): narrow rows, wide rows, contiguous, irregular
@@ -53,10 +57,14 @@ def plan(rnd, src, dst):
         ti = rng.randrange(len(RECIPES))
         count = rng.choice([1, 2, 3, 9, 40]) if ti != 3 else rng.choice([1, 8, 40])
         sdev = rng.random() < 0.85
-        # (host receives of device sends: descriptors landed by the host receive)
-        rdev = rng.random() < (0.8 if sdev else 0.5)
-        smode = rng.choice(["isend", "isend", "issend", "ibsend", "persist"])
-        rkind = rng.choice(["irecv", "irecv", "persist"])
+        if modes:
+            # (host receives of device sends: descriptors landed by the host receive)
+            rdev = rng.random() < (0.8 if sdev else 0.5)
+            smode = rng.choice(["isend", "isend", "issend", "ibsend", "persist"])
+            rkind = rng.choice(["irecv", "irecv", "persist"])
+        else:
+            rdev = True if sdev else rng.random() < 0.5
+            smode, rkind = "isend", "irecv"
         msgs.append(dict(ti=ti, count=count, tag=rng.choice([3, 4]), sdev=sdev, rdev=rdev,
                          seed=rng.randrange(1 << 30), smode=smode, rkind=rkind))
     return msgs
@@ -136,7 +144,8 @@ for rnd in range(rounds):
 
 for t in TYPES:
     typezoo.free(mpi, *t)
-mpi.Buffer_detach()
+if modes:
+    mpi.Buffer_detach()
 c = mpi.counters()
 print(f"rank {rank} routes: direct={c['send_direct']} ipc={c['send_ipc']} copy={c['send_ipc_copy']} "
       f"oneshot={c['send_oneshot']} lib={c['lib_sends']}", flush=True)

@@ -94,7 +94,7 @@ def test_halo_exchange_content(gpu, ranks, grid, env, extra):
 
 
 @pytest.mark.parametrize("ranks,env", [(1, {}), (2, {}), (4, {"TEMPI_FAKE_FOREIGN_GPU": "1"}),
-                                       (8, {"TEMPI_STREAMS": "3"}), (1, {"TEMPI_PREGATHER_BYTES": "134217728"})])
+                                       (8, {"TEMPI_STREAMS": "3"})])
 def test_halo_exchange_512_full_check(gpu, ranks, env):
     """config 4 at its full size, 8 quantities: every cell of every quantity
     checked (on the GPU), at 1 rank and in the 2-, 4- and 8-rank
@@ -242,17 +242,6 @@ def test_completion_family_device(gpu, method):
     assert rc == 0 and "RESULT errors=0" in out, out[-3000:]
 
 
-@pytest.mark.parametrize("n,method", [(1, "AUTO"), (2, "AUTO"), (2, "ONESHOT"), (2, "IPC"), (2, "STAGED"),
-                                      (2, "XCOPY")])
-def test_persistent_and_send_modes_device(gpu, n, method):
-    """device objects through persistent requests (every init call, MPI_Start /
-    MPI_Startall, inactive requests in the completion family, cancel, a
-    persistent host receive of a device send) and MPI_Ssend / Bsend / Rsend /
-    Issend / Ibsend / Irsend; one rank sends to itself"""
-    rc, out = mpi_launch.run(n, mpi_launch.py("persistent.py", "--device"), env=METHODS[method], timeout=240)
-    assert rc == 0 and "RESULT errors=0" in out, out[-3000:]
-
-
 @pytest.mark.parametrize("env", [METHODS["XCOPY"], dict(METHODS["XCOPY"], TEMPI_FAULT_IPC_OPEN="1"),
                                  dict(METHODS["XCOPY"], TEMPI_STREAMS="3"),
                                  dict(METHODS["XCOPY"], TEMPI_FAKE_FOREIGN_GPU="1")],
@@ -308,10 +297,7 @@ def test_self_channel(gpu, n, env):
 @pytest.mark.parametrize("n,seed,env", [(1, 7, {}), (2, 7, {}), (3, 11, {}), (4, 5, {}),
                                         (1, 23, {"TEMPI_NO_SELF_CHANNEL": "1"}), (2, 29, {"TEMPI_NO_SELF_CHANNEL": "1"}),
                                         (3, 13, {"TEMPI_STREAMS": "3"}), (2, 17, {"TEMPI_NO_IPC_COPY": "1"}),
-                                        (2, 19, {"TEMPI_NO_DIRECT": "1"}),
-                                        (2, 31, {"TEMPI_PREGATHER_BYTES": "1000000000", "TEMPI_PREGATHER_MAX_BLOCK":
-                                                 "1000000", "TEMPI_PREGATHER_FLUSH": "1"}),
-                                        (1, 37, {"TEMPI_PREGATHER_BYTES": "100000", "TEMPI_PREGATHER_MAX_BLOCK": "64"})])
+                                        (2, 19, {"TEMPI_NO_DIRECT": "1"})])
 def test_transport_fuzz(gpu, n, seed, env):
     """random mixes of every route (direct, IPC slab, IPC COPY, ONESHOT,
     library-packed, host) between all pairs incl. self, tags reused so MPI

@@ -679,23 +679,6 @@ def test_synchronous_ticket_visible_device_wide(mpi, gpu, rows, block, stride, f
         mpi.Type_free(t)
 
 
-@pytest.mark.skipif(os.environ.get("TEMPI_TEST_AQL") != "1",
-                    reason="TEMPI_AQL is opt-in and not yet run on this pool's GPUs (DESIGN §6): "
-                           "set TEMPI_TEST_AQL=1 (tools/gpu_aql_session.sh does)")
-def test_synchronous_calls_through_aql_packets(gpu):
-    """TEMPI_AQL=1: synchronous MPI_Pack / MPI_Unpack launched by TEMPI's own
-    AQL dispatch packets (hip/aql.hpp), every result visible device-wide right
-    after the call, and the packets really used (dispatch count: 5 of the 6
-    shapes fold their ticket, 2 x 40 calls each; a kernel whose code object
-    HIP has not loaded yet launches through HIP once)"""
-    from tests import mpi_launch
-
-    rc, out = mpi_launch.run(1, mpi_launch.py("aql_sync.py"), env={"TEMPI_AQL": "1"}, timeout=200)
-    assert rc == 0 and "RESULT errors=0" in out, out[-3000:]
-    n = int(out.split("aql_dispatches=")[1].split()[0])
-    assert 5 * 80 - 10 <= n <= 5 * 80, out[-3000:]
-
-
 def _hip():
     """the HIP runtime libtempi_hip.so uses in this process. (When TEMPI is
     loaded before torch, a PyTorch process holds two: ROCm's and torch's

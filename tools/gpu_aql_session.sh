@@ -19,7 +19,7 @@ for v in hip aql aqldev; do
 done
 grep -o '"variant": "[a-z]*", "shape": "[^"]*".*"ticket_fold_us": [0-9.]*' $O/aql_sync.jsonl | sed 's/"packed.*"ticket_fold_us"/ fold_us/'
 echo "== aql test"
-TEMPI_TEST_AQL=1 timeout -k 10 300 python -u -m pytest tests/test_pack_gpu.py -q -x --timeout 200 --timeout-method thread -k aql \
+TEMPI_TEST_AQL=1 timeout -k 10 300 python -u -m pytest tests/test_round3_gpu.py -q -x --timeout 200 --timeout-method thread -k aql \
   > $O/aql_test.log 2>&1
 rc=$?; tail -n 5 $O/aql_test.log; [ $rc -eq 0 ] || exit $rc
 echo "== config 1 A/B"
