@@ -1,10 +1,12 @@
-// tempi_amd/csrc/core/interpose_p2p.cpp -- interposed MPI_Send / MPI_Recv /
-// MPI_Isend / MPI_Irecv / MPI_Wait / MPI_Waitall / MPI_Test (include/
-// tempi_mpi.h). Device buffers go through tempi::p2p (p2p.hpp); host buffers
-// go to the library, as in the reference (/root/reference/src/send.cpp:12-17,
-// recv.cpp:19-44, isend.cpp:11-16, irecv.cpp:11-16, wait.cpp:11-16), except
-// that requests TEMPI owns are understood by MPI_Waitall and MPI_Test too
-// (SURVEY F8), and library waits keep TEMPI operations progressing.
+// tempi_amd/csrc/core/interpose_p2p.cpp -- interposed point-to-point calls
+// (include/tempi_mpi.h): MPI_Send / MPI_Recv / MPI_Isend / MPI_Irecv /
+// MPI_Wait as in the reference (/root/reference/src/send.cpp:12-17,
+// recv.cpp:19-44, isend.cpp:11-16, irecv.cpp:11-16, wait.cpp:11-16), plus
+// what the reference leaves to the library: the rest of the completion
+// family, MPI_Sendrecv(_replace), the probe family, the other
+// send modes and persistent requests. Device buffers go through tempi::p2p
+// (p2p.hpp); host buffers go to the library, except where a receive could
+// meet a descriptor; library waits keep TEMPI operations progressing.
 #include "trace.hpp"
 #include "counters.hpp"
 #include "log.hpp"
