@@ -4,6 +4,8 @@
 # misaligned rows the config-2 sweep reports worst (2 B rows at stride 18 in
 # 2D and 3D with a 3-row pad, 3 B at 19, 1 B at 17) and controls (1 B : 2,
 # 4-byte words, 8-byte rows). Two alternations, gpurun_out/dense_ab.jsonl.
+# Build the variants first, on the CPU side:
+#   tools/build_ab.sh "r9:-DTEMPI_DENSE_RATIO=9" "r16:-DTEMPI_DENSE_RATIO=16" "r24:-DTEMPI_DENSE_RATIO=24"
 set -o pipefail
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
