@@ -59,6 +59,11 @@
  *                                                    receive is TEMPI's; otherwise
  *                                                    forwarded (the self channel
  *                                                    spills first: matching order)
+ *   MPI_Buffer_detach
+ *                    (not interposed)                first waits until every buffered-
+ *                                                    mode send of a device object has
+ *                                                    been handed to the library (it
+ *                                                    goes only after its gather)
  *   MPI_Barrier      (not interposed)                keeps TEMPI operations moving
  *                                                    while it waits (a peer may need
  *                                                    this rank's progress)
@@ -155,6 +160,7 @@ int MPI_Start(MPI_Request *request);
 int MPI_Startall(int count, MPI_Request array_of_requests[]);
 int MPI_Sendrecv_replace(void *buf, int count, MPI_Datatype datatype, int dest, int sendtag, int source,
                          int recvtag, MPI_Comm comm, MPI_Status *status);
+int MPI_Buffer_detach(void *buffer_addr, int *size);
 int MPI_Barrier(MPI_Comm comm);
 int MPI_Alltoallv(const void *sendbuf, const int sendcounts[], const int sdispls[],
                   MPI_Datatype sendtype, void *recvbuf, const int recvcounts[], const int rdispls[],

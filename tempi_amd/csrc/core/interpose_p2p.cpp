@@ -222,6 +222,13 @@ TEMPI_EXPORT int MPI_Testany(int count, MPI_Request requests[], int *index, int 
   }
   *index = MPI_UNDEFINED;
   *flag = anyActive ? 0 : 1;
+  if (!anyActive && status != MPI_STATUS_IGNORE) { // every request null or inactive: an empty status
+    status->MPI_SOURCE = MPI_ANY_SOURCE;
+    status->MPI_TAG = MPI_ANY_TAG;
+    status->MPI_ERROR = MPI_SUCCESS;
+    MPI_Status_set_elements(status, MPI_BYTE, 0);
+    MPI_Status_set_cancelled(status, 0);
+  }
   return MPI_SUCCESS;
 }
 
@@ -428,6 +435,16 @@ TEMPI_EXPORT int MPI_Irsend(const void *buf, int count, MPI_Datatype datatype, i
   return mode_send(buf, count, datatype, dest, tag, comm, request, p2p::SendMode::READY);
 }
 
+// MPI_Buffer_detach waits until every buffered-mode message has been handed
+// to the library: a device object's MPI_Ibsend reaches it only after its
+// gather has run, and the attached buffer must still be there then (the
+// library's own detach then waits for the library's copies to drain).
+TEMPI_EXPORT int MPI_Buffer_detach(void *buffer_addr, int *size) {
+  resolve_next();
+  if (state.active) p2p::drain_buffered();
+  return next.MPI_Buffer_detach(buffer_addr, size);
+}
+
 // Persistent requests: TEMPI's while it is active beside a GPU (p2p.hpp:
 // persistent_init; MPI_Start posts through the interposed non-blocking calls,
 // so device objects take the transport and host buffers keep send order and
@@ -508,7 +525,8 @@ TEMPI_EXPORT int MPI_Sendrecv_replace(void *buf, int count, MPI_Datatype datatyp
   resolve_next();
   p2p::Route rr;
   if (state.active && count > 0 &&
-      (p2p::handles(buf, count, datatype, source, &rr) || p2p::host_recv_aware(source, recvtag, comm))) {
+      (p2p::handles(buf, count, datatype, source, &rr) || p2p::handles(buf, count, datatype, dest, &rr) ||
+       p2p::host_recv_aware(source, recvtag, comm))) {
     int size = 0, pos = 0;
     MPI_Pack_size(count, datatype, comm, &size);
     std::vector<char> tmp(size_t(size > 0 ? size : 1));

@@ -56,6 +56,7 @@
   X(MPI_Start)                                                                 \
   X(MPI_Startall)                                                              \
   X(MPI_Sendrecv_replace)                                                      \
+  X(MPI_Buffer_detach)                                                         \
   X(MPI_Alltoallv)                                                             \
   X(MPI_Neighbor_alltoallv)                                                    \
   X(MPI_Neighbor_alltoallw)                                                    \

@@ -326,6 +326,10 @@ void drain_sends(MPI_Comm comm, int dest) {
   while (gate_busy(key)) progress();
 }
 
+void drain_buffered() {
+  while (bufferedUnposted > 0) progress();
+}
+
 bool is_tempi_request(MPI_Request r) {
   const uint32_t h = uint32_t(r);
   return h != 0 && h < kHandleSpace && active.count(h);

@@ -131,6 +131,8 @@ void self_forget(MPI_Comm comm);
 bool send_gated(MPI_Comm comm, int dest);
 int isend_host(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Comm comm, MPI_Request *req);
 void drain_sends(MPI_Comm comm, int dest);
+// progress until every buffered-mode send TEMPI holds has reached the library
+void drain_buffered();
 
 // Persistent requests (p2p_persistent.cpp): a TEMPI request remembering its
 // arguments; start() posts the operation through the interposed MPI_Isend /

@@ -47,6 +47,9 @@ int board_take(int peer) {
   return s;
 }
 
+// a slot taken for a message that was never sent
+void board_give(int slot) { board.freeSlots.push_back(slot); }
+
 // the ack code in this rank's slot (and the slot freed), or -1 until it arrives
 int board_poll(int slot) {
   uint32_t *p = board.of[size_t(state.worldRank)] + slot;

@@ -174,6 +174,7 @@ struct AckBoard {
 extern AckBoard board;
 // a free slot of this rank's board for a message to world rank `peer`, or -1
 int board_take(int peer);
+void board_give(int slot); // a slot taken for a message that was never sent
 // the ack code in this rank's slot (and the slot freed), or -1 until it arrives
 int board_poll(int slot);
 void board_init();
@@ -355,6 +356,7 @@ struct PendingList {
   }
 };
 extern PendingList pendingPack, pendingUnpack;
+extern int64_t bufferedUnposted; // MPI_Ibsend-mode sends not yet handed to the library (MPI_Buffer_detach waits)
 constexpr size_t kMaxPending = 512;
 extern size_t earlyFlush;      // TEMPI_EARLY_FLUSH
 extern size_t firstFlush;      // TEMPI_FIRST_FLUSH: the same while no scatter batch is in flight

@@ -158,6 +158,7 @@ void PendingList::add_items(const Op *op, const Packer &pk, void *packed, const 
 }
 
 PendingList pendingPack, pendingUnpack;
+int64_t bufferedUnposted = 0;
 size_t earlyFlush = 32;
 size_t firstFlush = 16;
 int scattersInFlight = 0;
@@ -290,6 +291,7 @@ struct IsendOp : Op {
       : rec(r->ref()), origin(o), count(c), dest(de), tag(t), dt(d), comm(cm), method(m), bytes(b),
         key(gate_key(cm, de)), mode(md) {
     device = dev;
+    if (mode == SendMode::BUFFERED) ++bufferedUnposted;
     gate_enter(key, this);
     if (method == Method::ONESHOT) {
       hslab = pinned_pool().get(size_t(bytes), device);
@@ -309,17 +311,21 @@ struct IsendOp : Op {
     ready = true;
     gate_advance(key);
   }
+  // the library refused the send (MPI_Ibsend with too small an attached
+  // buffer, ...): the op completes with that error, its slabs released
+  void post_failed(int rc) {
+    lib = MPI_REQUEST_NULL;
+    err = rc;
+    errComm = comm;
+    lib_done(MPI_Status{});
+  }
   void post() override {
+    if (mode == SendMode::BUFFERED) --bufferedUnposted;
+    int rc = MPI_SUCCESS;
     switch (method) {
     case Method::ONESHOT:
-    case Method::STAGED:
-      lib_isend(mode, hslab->host, int(bytes), MPI_PACKED, dest, tag, comm, &lib);
-      watch(this);
-      break;
-    case Method::DEVICE:
-      lib_isend(mode, dslab->dev, int(bytes), MPI_PACKED, dest, tag, comm, &lib);
-      watch(this);
-      break;
+    case Method::STAGED: rc = lib_isend(mode, hslab->host, int(bytes), MPI_PACKED, dest, tag, comm, &lib); break;
+    case Method::DEVICE: rc = lib_isend(mode, dslab->dev, int(bytes), MPI_PACKED, dest, tag, comm, &lib); break;
     case Method::IPC: {
       desc.magic[0] = kMagic0;
       desc.magic[1] = kMagic1;
@@ -333,23 +339,32 @@ struct IsendOp : Op {
       std::memcpy(desc.handle, slab_ipc_handle(dslab), sizeof desc.handle);
       // the slab is reused once the receiver acknowledges: in a board slot,
       // or as a library message on the private communicator (those tags take
-      // [board.slots, tagUb/2); IPC COPY's the upper half)
+      // [board.slots, tagUb/2); IPC COPY's the upper half). The ack's receive
+      // is posted after the descriptor's send (the library holds an early ack
+      // as an unexpected message), so a refused send leaves nothing behind.
       const int peer = topology::world_rank(comm, dest);
       const int slot = board_take(peer);
       const uint32_t span = uint32_t(std::max(1, tagUb / 2 - board.slots));
       desc.ackTag = slot >= 0 ? slot : board.slots + int32_t(dslab->id % span);
+      rc = lib_isend(mode, &desc, int(sizeof desc), MPI_PACKED, dest, tag, comm, &lib);
+      if (rc != MPI_SUCCESS) {
+        if (slot >= 0) board_give(slot);
+        break;
+      }
       pendingAcks.push_back(
           std::unique_ptr<PendingAck>(new PendingAck{MPI_REQUEST_NULL, dslab, peer, desc.ackTag, bytes, -1, slot >= 0}));
       PendingAck &pa = *pendingAcks.back();
       if (slot < 0) next.MPI_Irecv(&pa.code, 1, MPI_INT, peer, desc.ackTag, ctrlComm, &pa.req);
       dslab = nullptr;
-      lib_isend(mode, &desc, int(sizeof desc), MPI_PACKED, dest, tag, comm, &lib);
-      watch(this);
       break;
     }
     default:
-      break;
+      return;
     }
+    if (rc != MPI_SUCCESS)
+      post_failed(rc);
+    else
+      watch(this);
   }
   void lib_done(const MPI_Status &) override {
     if (dslab) device_pool().put(dslab);
@@ -361,7 +376,7 @@ struct IsendOp : Op {
     if (s != MPI_STATUS_IGNORE) {
       s->MPI_SOURCE = MPI_ANY_SOURCE;
       s->MPI_TAG = MPI_ANY_TAG;
-      s->MPI_ERROR = MPI_SUCCESS;
+      s->MPI_ERROR = err;
       MPI_Status_set_elements(s, MPI_BYTE, 0);
     }
   }
@@ -572,16 +587,25 @@ struct LibIsendOp : Op {
       : dt(d), dest(de), tag(t), comm(cm), mode(md) {
     buf.resize(size_t(std::max<int64_t>(pack_size(c, d, comm), 1)));
     tempi::pack(b, c, d, buf.data(), int(buf.size()), &n, comm);
+    if (mode == SendMode::BUFFERED) ++bufferedUnposted;
     post_or_queue(gate_key(comm, dest), this);
   }
   void post() override {
-    lib_isend(mode, buf.data(), n, MPI_PACKED, dest, tag, comm, &lib);
-    watch(this);
+    if (mode == SendMode::BUFFERED) --bufferedUnposted;
+    const int rc = lib_isend(mode, buf.data(), n, MPI_PACKED, dest, tag, comm, &lib);
+    if (rc == MPI_SUCCESS) {
+      watch(this);
+      return;
+    }
+    lib = MPI_REQUEST_NULL;
+    err = rc;
+    errComm = comm;
+    done = true;
   }
   void lib_done(const MPI_Status &) override { done = true; }
   void status(MPI_Status *s) const override {
     if (s != MPI_STATUS_IGNORE) {
-      s->MPI_ERROR = MPI_SUCCESS;
+      s->MPI_ERROR = err;
       MPI_Status_set_elements(s, MPI_BYTE, 0);
     }
   }

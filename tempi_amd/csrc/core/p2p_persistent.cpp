@@ -146,6 +146,9 @@ int persistent_test(PersistentOp *p, int *flag, MPI_Status *status) {
   MPI_Status st;
   empty_status(&st);
   const int rc = MPI_Test(&p->inner, flag, &st);
+  // an error before the inner request completed: that request is let go
+  // (it finishes in the background) and the persistent one is inactive again
+  if (rc != MPI_SUCCESS && !*flag && p->inner != MPI_REQUEST_NULL) MPI_Request_free(&p->inner);
   if (*flag || rc != MPI_SUCCESS) p->finished(st, status);
   return rc;
 }

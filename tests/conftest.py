@@ -13,6 +13,21 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: long-running CPU test")
 
 
+# The hot path's parity evidence (MPICH goldens, library MPI_Pack, full-size
+# exact checks) runs before anything else, so that under `pytest -x` a failure
+# in a transport or tool test can never hide it (round 3: one NameError in a
+# fuzz script stopped the run before test_pack_gpu.py was reached).
+FIRST = ("test_oracle.py", "test_pack_gpu.py", "test_dense_gpu.py", "test_direct_gpu.py")
+
+
+def pytest_collection_modifyitems(session, config, items):
+    def rank(item):
+        name = os.path.basename(str(item.fspath))
+        return FIRST.index(name) if name in FIRST else len(FIRST)
+
+    items[:] = sorted(items, key=rank)  # (stable: file order kept inside each group)
+
+
 @pytest.fixture(scope="session")
 def mpi():
     """MPI initialised (singleton) through libtempi.so for the whole session."""

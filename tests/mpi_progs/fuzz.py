@@ -9,7 +9,10 @@ MPI_Ibsend, and persistent MPI_Send_init + MPI_Start), receive kinds
 (MPI_Irecv, persistent MPI_Recv_init + MPI_Start) and host receives of
 device sends. Every rank posts its receives and sends in a random
 interleaving, waits for all with one MPI_Waitall, and checks every received
-byte against the oracle.  usage: fuzz.py [rounds] [seed] [--modes]"""
+byte against the oracle. --host keeps every buffer in host memory (no GPU
+needed: the CPU suite runs it under TEMPI_TEST_HOST_ONLY so that a script
+that cannot start fails there, not on the GPU box).
+usage: fuzz.py [rounds] [seed] [--modes] [--host]"""
 import os
 import random
 import sys
@@ -23,16 +26,18 @@ import tempi_amd  # noqa: E402
 from oracle import pyoracle  # noqa: E402
 from tests import typezoo  # noqa: E402
 
-import torch  # noqa: E402
+host_only = "--host" in sys.argv
+if not host_only:
+    import torch
 
-torch.cuda.set_device(0)
+    torch.cuda.set_device(0)
 mpi = tempi_amd.get_mpi()
 mpi.Init()
 rank, size = mpi.Comm_rank(), mpi.Comm_size()
+modes = "--modes" in sys.argv
 if modes:
     mpi.Buffer_attach(256 << 20)  # (MPI_Ibsend: every round's buffered sends fit)
-modes = "--modes" in sys.argv
-argv = [a for a in sys.argv[1:] if a != "--modes"]
+argv = [a for a in sys.argv[1:] if a not in ("--modes", "--host")]
 rounds = int(argv[0]) if len(argv) > 0 else 6
 seed0 = int(argv[1]) if len(argv) > 1 else 7
 errors = 0
@@ -65,6 +70,8 @@ def plan(rnd, src, dst):
         else:
             rdev = True if sdev else rng.random() < 0.5
             smode, rkind = "isend", "irecv"
+        if host_only:
+            sdev = rdev = False
         msgs.append(dict(ti=ti, count=count, tag=rng.choice([3, 4]), sdev=sdev, rdev=rdev,
                          seed=rng.randrange(1 << 30), smode=smode, rkind=rkind))
     return msgs
@@ -76,7 +83,12 @@ def buffer(n, seed, dev):
 
 
 def addr(b):
-    return b.data_ptr() if isinstance(b, torch.Tensor) else b.ctypes.data
+    return b.ctypes.data if isinstance(b, np.ndarray) else b.data_ptr()
+
+
+def sync():
+    if not host_only:
+        torch.cuda.synchronize()
 
 
 for rnd in range(rounds):
@@ -112,7 +124,7 @@ for rnd in range(rounds):
         else:
             seq.append(recvs_by_src[j])
             j += 1
-    torch.cuda.synchronize()
+    sync()
     reqs, persistent = [], []
     for kind, p, count, t, peer, tag in seq:
         if kind == "isend":
@@ -134,9 +146,9 @@ for rnd in range(rounds):
     mpi.Waitall(reqs)
     for r in persistent:
         mpi.Request_free(r)
-    torch.cuda.synchronize()
+    sync()
     for b, exp, what in checks:
-        got = b.cpu().numpy() if isinstance(b, torch.Tensor) else b
+        got = b if isinstance(b, np.ndarray) else b.cpu().numpy()
         if not np.array_equal(got, exp):
             errors += 1
             print(f"rank {rank}: {what}: bytes differ", flush=True)

@@ -184,6 +184,36 @@ for m, mode in enumerate(("ssend", "bsend", "rsend", "issend", "ibsend", "irsend
     check(mode, rbuf, 6, 3000 + 10 * src + m)
     mpi.Barrier()
 
+# buffered mode against the attached buffer: a message that does not fit is
+# an error (returned: ERRORS_RETURN), not a hang -- a device object's
+# MPI_Ibsend reaches the library only after its gather
+bsize = 8 * (packed + mpi.const("MPI_BSEND_OVERHEAD")) + 4096
+mpi.Buffer_detach()
+mpi.Buffer_attach(mpi.const("MPI_BSEND_OVERHEAD") + 64)  # (MPICH refuses less than its overhead)
+sbuf = buf(7)
+try:
+    s = mpi.Ibsend(ptr(sbuf) + origin, count, t, peer, 60)
+    mpi.Wait(s)
+    fail("an MPI_Ibsend larger than the attached buffer succeeded")
+except tempi_amd.mpi.MPIError:
+    pass
+mpi.Barrier()
+mpi.Buffer_detach()
+mpi.Buffer_attach(bsize)
+# MPI_Buffer_detach right after MPI_Ibsend: the detach waits until the message
+# is the library's, and it still arrives
+sbuf, rbuf = buf(8), buf(9)
+refill(sbuf, 8000 + rank)
+r = mpi.Irecv(ptr(rbuf) + origin, count, t, src, 61)
+mpi.Barrier()
+s = mpi.Ibsend(ptr(sbuf) + origin, count, t, peer, 61)
+mpi.Buffer_detach()
+mpi.Wait(r)
+mpi.Wait(s)
+check("ibsend then detach", rbuf, 9, 8000 + src)
+mpi.Barrier()
+mpi.Buffer_attach(bsize)
+
 c = mpi.counters()
 starts, sends = c["persistent_starts"], c["sends"]
 if tempi_holds and starts < 4 * 4:
