@@ -699,6 +699,14 @@ def _hip():
     return hip
 
 
+# host arrays the registered case hipHostRegister'ed: kept for the whole
+# session, so that their addresses are never handed out again by malloc. (GPU
+# box, round 4: right after the registered case unregistered and freed its
+# arrays, the next case's first pageable torch copy -- a fresh 18 MiB numpy
+# array, likely at the freed address -- failed with an illegal address.)
+_REGISTERED_KEEP = []
+
+
 @pytest.mark.parametrize("kind", ["noncoherent", "registered", "coherent"])
 def test_application_pinned_memory_waits_with_stream_sync(mpi, gpu, kind):
     """a kernel writing the APPLICATION's pinned host memory --
@@ -713,14 +721,13 @@ def test_application_pinned_memory_waits_with_stream_sync(mpi, gpu, kind):
     ext = (rows - 1) * stride + block
     t = mpi.Type_commit(mpi.Type_vector(rows, block, stride, mpi.BYTE))
     ptrs = []
-    keep = []
 
     def host_buf(nbytes):
         if kind == "registered":
             a = np.zeros(nbytes + 4096, dtype=np.uint8)
             p = (a.ctypes.data + 4095) & ~4095
             assert hip.hipHostRegister(ctypes.c_void_p(p), nbytes, 0x2 | 0x1) == 0  # mapped, portable
-            keep.append(a)
+            _REGISTERED_KEEP.append(a)
             ptrs.append(("unreg", p))
         else:
             v = ctypes.c_void_p()
@@ -754,5 +761,7 @@ def test_application_pinned_memory_waits_with_stream_sync(mpi, gpu, kind):
         assert c1["sync_waits"] - c0["sync_waits"] == 80 and c1["ticket_waits"] == c0["ticket_waits"]
     finally:
         mpi.Type_free(t)
+        torch.cuda.synchronize()
         for how, p in ptrs:
-            (hip.hipHostUnregister if how == "unreg" else hip.hipHostFree)(ctypes.c_void_p(p))
+            rc = (hip.hipHostUnregister if how == "unreg" else hip.hipHostFree)(ctypes.c_void_p(p))
+            assert rc == 0, f"{how} of {p:#x}: hip error {rc}"

@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B builds of the gfx950 kernels: tools/_variants/libtempi_hip_<name>.so for
-# the working tree ("cur") and for each git REF given (its pack_kernels.hip
-# and runtime.hip), plus the kernel benches kbench / hbench.
+# the working tree ("cur") and for each git REF given (every file of its
+# tempi_amd/csrc/hip/), plus the kernel benches kbench / hbench.
 # An argument NAME:FLAGS instead builds the working tree with those compiler
 # flags (e.g. "nowave:-DTEMPI_WAVE_DECODE=0").
 # usage: tools/build_ab.sh [REF | NAME:FLAGS ...]   (then tools/kab.sh on the GPU box)
@@ -11,7 +11,7 @@ mkdir -p tools/_variants
 rm -f tools/_variants/*.so
 build() { # name dir [flags]
   hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Iinclude $3 \
-    -o tools/_variants/libtempi_hip_$1.so $2/pack_kernels.hip $2/runtime.hip -Wl,-rpath,/opt/rocm/lib
+    -o tools/_variants/libtempi_hip_$1.so $2/*.hip -Wl,-rpath,/opt/rocm/lib -L/opt/rocm/lib -lhsa-runtime64
 }
 build cur tempi_amd/csrc/hip &
 for ref in "$@"; do
@@ -20,8 +20,7 @@ for ref in "$@"; do
     continue
   fi
   d=$(mktemp -d)
-  git show "$ref:tempi_amd/csrc/hip/pack_kernels.hip" > $d/pack_kernels.hip
-  git show "$ref:tempi_amd/csrc/hip/runtime.hip" > $d/runtime.hip
+  git archive "$ref" tempi_amd/csrc/hip | tar -x -C $d --strip-components=3
   build "$(echo "$ref" | tr -c 'A-Za-z0-9_\n' '_')" $d &
 done
 wait
