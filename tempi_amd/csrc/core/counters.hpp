@@ -51,8 +51,8 @@ void settle_kernel_times();
 void *timing_event(int device);
 void timed(int device, bool pack, void *ev0, void *ev1, bool ok);
 void destroy_timing_events();
-// the ns_* host timers run only when asked for (TEMPI_PRINT_COUNTERS or
-// TEMPI_HOST_TIMING): a clock read is ~20 ns, several per message
+// the ns_* host timers run only when asked for (TEMPI_PRINT_COUNTERS): a
+// clock read is ~20 ns, several per message
 extern bool hostTiming;
 
 uint64_t now_ns();

@@ -20,7 +20,6 @@ void read_environment() {
   e.noPack = has("TEMPI_NO_PACK");
   e.noTypeCommit = has("TEMPI_NO_TYPE_COMMIT");
   e.faultPack = has("TEMPI_FAULT_PACK");
-  e.streamSync = has("TEMPI_STREAM_SYNC");
 
   if (has("TEMPI_ALLTOALLV_REMOTE_FIRST")) e.alltoallv = AlltoallvMethod::REMOTE_FIRST;
   if (has("TEMPI_ALLTOALLV_STAGED")) e.alltoallv = AlltoallvMethod::STAGED;

@@ -22,7 +22,6 @@ struct Environment {
   bool noPack = false;       // TEMPI_NO_PACK
   bool noTypeCommit = false; // TEMPI_NO_TYPE_COMMIT
   bool faultPack = false;    // TEMPI_FAULT_PACK (tests): every MPI_Pack / MPI_Unpack kernel launch "fails"
-  bool streamSync = false;   // TEMPI_STREAM_SYNC: synchronous calls wait with hipStreamSynchronize, not a ticket
   DatatypeMethod datatype = DatatypeMethod::AUTO;
   ContiguousMethod contiguous = ContiguousMethod::NONE;
   AlltoallvMethod alltoallv = AlltoallvMethod::AUTO;

@@ -17,7 +17,6 @@ int nDevices = 0;
 std::mutex mtx;
 std::vector<void *> streams; // [device * kMaxLanes + lane]
 int nLanes = 3;
-bool highPriority = true; // TEMPI_NO_STREAM_PRIORITY
 // TEMPI_TEST_HOST_ONLY (CPU tests): with no GPU visible, TEMPI still takes the
 // host-side paths it takes beside a GPU (descriptor-aware host receives, the
 // probe family, send gates), so they can be exercised on a machine without
@@ -43,7 +42,6 @@ void init() {
   std::lock_guard<std::mutex> g(mtx);
   streams.assign(size_t(n) * kMaxLanes, nullptr);
   nLanes = 1; // until choose_lanes()
-  highPriority = std::getenv("TEMPI_NO_STREAM_PRIORITY") == nullptr;
   LOG_DEBUG("visible GPUs: " << n);
 }
 
@@ -98,7 +96,7 @@ void *stream(int device, int lane) {
     void *s = nullptr;
     // with several lanes, lane 0 (gathers whose packed bytes a peer is
     // waiting for) outranks the scatter lanes
-    check(tempi_hip_stream_create_priority(&s, nLanes > 1 && lane == 0 && highPriority), "stream create");
+    check(tempi_hip_stream_create_priority(&s, nLanes > 1 && lane == 0), "stream create");
     if (cur != device) tempi_hip_set_device(cur);
     streams[i] = s;
   }

@@ -122,7 +122,7 @@ void init_after_mpi() {
   MPI_Comm_size(MPI_COMM_WORLD, &state.worldSize);
   logRank = state.worldRank;
   trace::init();
-  hostTiming = std::getenv("TEMPI_PRINT_COUNTERS") || std::getenv("TEMPI_HOST_TIMING");
+  hostTiming = std::getenv("TEMPI_PRINT_COUNTERS") != nullptr;
   gpu::init();
   types_init();
   state.active = true;
@@ -192,7 +192,7 @@ template <typename F> int on_device(int device, bool pack, bool ticketOk, F &&fn
     ev1 = timing_event(device);
   }
   if (ev0) tempi_hip_event_record(ev0, s);
-  const bool byTicket = ticketOk && !env.streamSync;
+  const bool byTicket = ticketOk;
   Packer::Completion done;
   int e = fn(s, byTicket ? &done : nullptr);
   if (ev1) tempi_hip_event_record(ev1, s);

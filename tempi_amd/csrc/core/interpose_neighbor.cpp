@@ -219,13 +219,7 @@ int isir(const void *sendbuf, const int *scounts, const MPI_Aint *sdispls, const
   // Receives, then sends (their gathers queue), then the self edges' copies:
   // one start launches the gathers first, so the peers' data leaves before
   // this rank's own copies run (on a GPU shared by several ranks, or a single
-  // lane, a stream runs them in that order). TEMPI_NBR_COPIES_FIRST (A/B):
-  // the copies first, as before.
-  static const bool copiesFirst = std::getenv("TEMPI_NBR_COPIES_FIRST") != nullptr;
-  if (copiesFirst && !plan.copies.items.empty()) {
-    reqs.push_back(p2p::start_local_copies(plan.copies));
-    p2p::start_queued();
-  }
+  // lane, a stream runs them in that order; profiles/r03/nbr_order_ab_s12.jsonl).
   for (size_t i = 0; i < in.size(); ++i) {
     if (in[i] == MPI_PROC_NULL || doneIn[i]) continue;
     MPI_Request r;
@@ -244,7 +238,7 @@ int isir(const void *sendbuf, const int *scounts, const MPI_Aint *sdispls, const
     if (rc != MPI_SUCCESS) return rc;
     reqs.push_back(r);
   }
-  if (!copiesFirst && !plan.copies.items.empty()) reqs.push_back(p2p::start_local_copies(plan.copies));
+  if (!plan.copies.items.empty()) reqs.push_back(p2p::start_local_copies(plan.copies));
   p2p::start_queued();
   return MPI_Waitall(int(reqs.size()), reqs.data(), MPI_STATUSES_IGNORE);
 }

@@ -63,24 +63,15 @@ int collectiveDepth = 0;
 void init() {
   gpu::choose_lanes(topology::ranks_on_node());
   gpuAwareLibrary = std::getenv("TEMPI_MPI_GPU_AWARE") != nullptr;
-  modelForIsend = std::getenv("TEMPI_AUTO_MODEL_ISEND") != nullptr;
   directEnabled = std::getenv("TEMPI_NO_DIRECT") == nullptr;
-  ipcSystemLoads = std::getenv("TEMPI_IPC_PLAIN_LOADS") == nullptr;
-  hostRecvAware = std::getenv("TEMPI_NO_HOST_RECV") == nullptr;
   selfChannelEnabled = directEnabled && std::getenv("TEMPI_NO_SELF_CHANNEL") == nullptr; // it carries direct sends
   clear_channels();
   faultCanary = std::getenv("TEMPI_FAULT_CANARY") != nullptr;
   clear_canary();
   ipcCopyEnabled = std::getenv("TEMPI_NO_IPC_COPY") == nullptr;
-  collCopyEnabled = std::getenv("TEMPI_NO_COLL_COPY") == nullptr;
   if (const char *s = std::getenv("TEMPI_IPC_COPY_MIN_BYTES")) ipcCopyMinBytes = std::atoll(s);
   if (const char *s = std::getenv("TEMPI_IPC_COPY_MIN_BLOCK")) ipcCopyMinBlock = std::atoll(s);
-  if (const char *s = std::getenv("TEMPI_EARLY_FLUSH")) earlyFlush = size_t(std::max(1, std::atoi(s)));
-  firstFlush = std::min<size_t>(16, earlyFlush);
-  if (const char *s = std::getenv("TEMPI_FIRST_FLUSH")) firstFlush = size_t(std::max(1, std::atoi(s)));
   scattersInFlight = 0;
-  eagerFlush = std::getenv("TEMPI_EAGER_FLUSH") != nullptr;
-  batchTickets = std::getenv("TEMPI_NO_BATCH_TICKET") == nullptr;
   pregatherBytes = 0;
   if (const char *s = std::getenv("TEMPI_PREGATHER_BYTES")) pregatherBytes = std::atoll(s);
   if (const char *s = std::getenv("TEMPI_PREGATHER_MAX_BLOCK")) pregatherMaxBlock = std::atoll(s);
@@ -91,7 +82,6 @@ void init() {
   active.reserve(2048);
   systemPerformanceLoaded = import_system_performance(&systemPerformance);
   clear_model_cache();
-  if (const char *s = std::getenv("TEMPI_IPC_MIN_BYTES")) ipcMinBytes = std::atoll(s);
   MPI_Comm_dup(MPI_COMM_WORLD, &ctrlComm);
   int flag = 0;
   int *ub = nullptr;
@@ -207,7 +197,7 @@ int isend(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Co
   }
   // IPC COPY: a large message of wide rows is copied by the receiver straight
   // out of this process's object (no gather, no slab)
-  const int64_t copyMin = (collectiveDepth > 0 && collCopyEnabled) ? 1 : ipcCopyMinBytes;
+  const int64_t copyMin = collectiveDepth > 0 ? 1 : ipcCopyMinBytes;
   if (m == Method::IPC && ipcCopyEnabled && mode != SendMode::BUFFERED && bytes >= copyMin && rec->flat(count, &flat) &&
       flat.ndims <= 3 && flat.block >= ipcCopyMinBlock && bytes < (int64_t(1) << 31)) {
     IpcCopyDesc d{};
@@ -257,7 +247,7 @@ int irecv(void *buf, int count, MPI_Datatype dt, int source, int tag, MPI_Comm c
   // keep the GPU busy while the caller is still posting: launch arrived
   // messages' copies / unpacks once a launch's worth has queued up
   // (sooner while the GPU has no scatter work: the first batch starts early)
-  if (pendingUnpack.size() >= (scattersInFlight ? earlyFlush : firstFlush)) flush_list(pendingUnpack, false);
+  if (pendingUnpack.size() >= (scattersInFlight ? kEarlyFlush : kFirstFlush)) flush_list(pendingUnpack, false);
   tock(counters.ns_irecv, t0);
   return MPI_SUCCESS;
 }
@@ -392,7 +382,7 @@ namespace {
 // share a launch instead of each taking one (a cheap pass -- no library
 // request to test -- would otherwise launch every arrival on its own).
 bool scatter_flush_due() {
-  return eagerFlush || scattersInFlight < std::max(1, gpu::lanes() - 1) || pendingUnpack.size() >= earlyFlush;
+  return scattersInFlight < std::max(1, gpu::lanes() - 1) || pendingUnpack.size() >= kEarlyFlush;
 }
 } // namespace
 

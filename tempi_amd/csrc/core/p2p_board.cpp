@@ -34,7 +34,7 @@ namespace detail {
 // (acquire). No library message per ack, and no library request in the
 // sender's MPI_Testsome for it. Tags below `slots` are board slots; acks that
 // travel as library messages (a peer outside the node communicator, no free
-// slot, TEMPI_NO_SHM_ACKS) keep tags at or above it.
+// slot) keep tags at or above it.
 AckBoard board;
 
 // a free slot of this rank's board for a message to world rank `peer`, or -1
@@ -62,7 +62,6 @@ int board_poll(int slot) {
 
 void board_init() {
   board = AckBoard();
-  if (std::getenv("TEMPI_NO_SHM_ACKS")) return;
   const int half = std::max(1, tagUb / 2);
   const int slots = std::min(16384, half / 2); // (library-message ack tags stay above)
   if (slots < 64) return;

@@ -148,8 +148,6 @@ struct DirectShared {
 extern std::unordered_map<uint64_t, std::shared_ptr<DirectShared>> directShared; // sent, not yet matched
 extern uint64_t nextDirectToken;
 extern bool directEnabled;
-extern bool ipcSystemLoads; // TEMPI_IPC_PLAIN_LOADS=1 turns off TEMPI_HIP_ITEM_REMOTE (A/B only)
-extern bool hostRecvAware;  // TEMPI_NO_HOST_RECV=1: host receives go straight to the library (A/B only)
 
 extern MPI_Comm ctrlComm; // private duplicate of MPI_COMM_WORLD for acks
 extern int tagUb;
@@ -205,7 +203,6 @@ enum { kCopyDone = 0, kCopyResend = 1, kCopyUnmapped = 2 };
 // ------------------------------------------------------ routes (p2p_routes)
 
 extern bool ipcCopyEnabled;     // TEMPI_NO_IPC_COPY
-extern bool collCopyEnabled;    // TEMPI_NO_COLL_COPY
 extern int64_t ipcCopyMinBytes; // TEMPI_IPC_COPY_MIN_BYTES
 extern int64_t ipcCopyMinBlock; // TEMPI_IPC_COPY_MIN_BLOCK
 extern uint32_t nextCopyTag;
@@ -225,7 +222,6 @@ int64_t packed_bytes(const TypeRecord *rec, int count, MPI_Datatype dt, MPI_Comm
 // the method for a message (TEMPI_DATATYPE_* or AUTO; AUTO prices only
 // blocking sends by the measured model, see p2p_routes.cpp)
 Method choose(int64_t bytes, bool colocated, bool blocking);
-extern bool modelForIsend; // TEMPI_AUTO_MODEL_ISEND
 void clear_model_cache();
 
 bool ipc_broken(int world);
@@ -358,11 +354,11 @@ struct PendingList {
 extern PendingList pendingPack, pendingUnpack;
 extern int64_t bufferedUnposted; // MPI_Ibsend-mode sends not yet handed to the library (MPI_Buffer_detach waits)
 constexpr size_t kMaxPending = 512;
-extern size_t earlyFlush;      // TEMPI_EARLY_FLUSH
-extern size_t firstFlush;      // TEMPI_FIRST_FLUSH: the same while no scatter batch is in flight
+// queued scatters are launched by a light pass once this many have queued
+// (kFirstFlush while no scatter batch is in flight: the GPU is idle then)
+constexpr size_t kEarlyFlush = 32;
+constexpr size_t kFirstFlush = 16;
 extern int scattersInFlight;   // scatter / copy batches launched and not yet seen complete
-extern bool eagerFlush;        // TEMPI_EAGER_FLUSH (A/B)
-extern bool batchTickets;      // !TEMPI_NO_BATCH_TICKET: batches complete by a folded ticket when they can
 // Pre-gather (TEMPI_PREGATHER_BYTES, 0 = off): a direct send to this process
 // whose receive is not posted yet, of rows <= pregatherMaxBlock bytes, is
 // gathered into a slab at once while no scatter batch is in flight (the GPU

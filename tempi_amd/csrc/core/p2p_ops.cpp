@@ -159,11 +159,7 @@ void PendingList::add_items(const Op *op, const Packer &pk, void *packed, const 
 
 PendingList pendingPack, pendingUnpack;
 int64_t bufferedUnposted = 0;
-size_t earlyFlush = 32;
-size_t firstFlush = 16;
 int scattersInFlight = 0;
-bool eagerFlush = false;
-bool batchTickets = true;
 int64_t pregatherBytes = 0, pregatherMaxBlock = 64, pregatherFlush = int64_t(4) << 20;
 int64_t pregatherUsed = 0, pregatherQueued = 0;
 
@@ -219,7 +215,7 @@ void flush_list(PendingList &list, bool pack) {
     // (never after a staged copy, which is not a kernel)
     bool staged = false;
     for (const PendingList::Stage &st : list.stages) staged |= st.dev == dev;
-    const bool ticketed = batchTickets && !staged;
+    const bool ticketed = !staged;
     const uint32_t *flag = nullptr;
     uint32_t ticket = 0;
     if (nitems) {

@@ -101,7 +101,6 @@ bool holds(int source, int tag, MPI_Comm comm) {
 bool host_recv_aware(int source, int tag, MPI_Comm comm) {
   if (!state.active || !gpu::available() || source == MPI_PROC_NULL) return false;
   if (holds(source, tag, comm)) return true; // a probe holds a message it may match
-  if (!hostRecvAware) return false; // TEMPI_NO_HOST_RECV (A/B only): host receives straight to the library
   return source == MPI_ANY_SOURCE || topology::colocated(comm, source);
 }
 

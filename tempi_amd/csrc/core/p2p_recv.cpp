@@ -231,7 +231,7 @@ struct IrecvOp : Op {
         // with system-scope loads. (Memory of this same GPU is read through
         // its own L2, which holds the sender's latest writes: measured, the
         // system-scope loads could return stale bytes there.)
-        if (!local && ipcSystemLoads && xd.gpu != gpu::identity(device)) c.flags = TEMPI_HIP_ITEM_REMOTE;
+        if (!local && xd.gpu != gpu::identity(device)) c.flags = TEMPI_HIP_ITEM_REMOTE;
         pendingUnpack.add_copy(this, c);
         pendingUnpack.queue(this);
         return;
@@ -268,7 +268,7 @@ struct IrecvOp : Op {
       elems = size ? d.bytes / size : 0;
       const size_t first = pendingUnpack.items.size();
       pendingUnpack.add_items(this, packer, const_cast<char *>(peer), origin, elems);
-      if (ipcSystemLoads && d.gpu != gpu::identity(device)) // another GPU's slab, reused between messages
+      if (d.gpu != gpu::identity(device)) // another GPU's slab, reused between messages
         for (size_t i = first; i < pendingUnpack.items.size(); ++i) pendingUnpack.items[i].flags |= TEMPI_HIP_ITEM_REMOTE;
     } else {
       if (int64_t(n) > bytes) return truncate(n);

@@ -28,8 +28,6 @@ namespace detail {
 std::unordered_map<uint64_t, std::shared_ptr<DirectShared>> directShared;
 uint64_t nextDirectToken = 1;
 bool directEnabled = true;
-bool ipcSystemLoads = true;
-bool hostRecvAware = true;
 MPI_Comm ctrlComm = MPI_COMM_NULL;
 int tagUb = 32767;
 bool gpuAwareLibrary = false;
@@ -56,7 +54,6 @@ bool ipcCopyEnabled = true;             // TEMPI_NO_IPC_COPY
 // Inside MPI_Alltoallv every receive is posted before any send is waited on,
 // so a rendezvous send cannot deadlock there: IPC COPY takes messages of any
 // size (TEMPI_NO_COLL_COPY keeps the point-to-point threshold)
-bool collCopyEnabled = true;
 // above MPICH's own eager limit (MPIR_CVAR_CH3_EAGER_MAX_MSG_SIZE, 128 KiB):
 // a program that works with the library's rendezvous works with this one
 int64_t ipcCopyMinBytes = 128 * 1024 + 1; // TEMPI_IPC_COPY_MIN_BYTES
@@ -146,9 +143,8 @@ int64_t modelBlock = 512; // block length of the type being sent (set per call)
 // 512^3 halo from 1.56-1.67 ms into 2.0-2.4 ms per iteration, on whichever
 // boxes the quick measurement put the crossover there (round 3,
 // profiles/r03/n2_variants_s4.jsonl). So non-blocking
-// sends keep the built-in policy; TEMPI_AUTO_MODEL_ISEND=1 prices them by the
-// model too (the reference's rule, async_operation.cpp:334-389).
-bool modelForIsend = false;
+// sends keep the built-in policy (the reference prices them by the model too,
+// async_operation.cpp:334-389).
 
 Method choose(int64_t bytes, bool colocated, bool blocking) {
   switch (env.datatype) {
@@ -164,7 +160,7 @@ Method choose(int64_t bytes, bool colocated, bool blocking) {
   case DatatypeMethod::AUTO:
   default: {
     Method m;
-    if ((blocking || modelForIsend) && model_choice(bytes, colocated, modelBlock, &m)) return m;
+    if (blocking && model_choice(bytes, colocated, modelBlock, &m)) return m;
     if (colocated && bytes >= ipcMinBytes) return Method::IPC;
     return Method::ONESHOT;
   }

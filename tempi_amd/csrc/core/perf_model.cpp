@@ -386,14 +386,14 @@ static bool load_file(const std::string &path, SystemPerformance *sp) {
 
 bool import_system_performance(SystemPerformance *sp) {
   // this node's own measurement first (TEMPI_CACHE_DIR/perf.json, as in the
-  // reference), then the shipped MI355X model unless TEMPI_NO_SHIPPED_PERF;
-  // with neither, AUTO uses the built-in policy (the reference stops: F10)
+  // reference), then the shipped MI355X model; with neither, AUTO uses the
+  // built-in policy (the reference stops: F10)
   systemPerformanceSource.clear();
   if (load_file(perf_path(), sp)) {
     systemPerformanceSource = perf_path();
     return true;
   }
-  if (!std::getenv("TEMPI_NO_SHIPPED_PERF") && load_file(shipped_path(), sp)) {
+  if (load_file(shipped_path(), sp)) {
     systemPerformanceSource = shipped_path();
     return true;
   }

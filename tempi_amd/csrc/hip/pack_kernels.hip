@@ -884,7 +884,7 @@ int word_width(uintptr_t packed, uintptr_t first, const Norm &n) {
 // neighbouring rows share lines (gap < 128 B), with rows below kXcdMaxBlock:
 // isolated rows (the halo's x faces) have nothing to merge, and long rows
 // are whole-line streams, which the dealt order serves better.
-// (TEMPI_NO_XCD_MAP set: never, for A/B runs)
+// (a build with -DTEMPI_XCD_MAP=0: never, for A/B runs)
 #ifndef TEMPI_XCD_MAX_BLOCK
 #define TEMPI_XCD_MAX_BLOCK 1024
 #endif
@@ -917,8 +917,7 @@ bool partial_pages(const Norm &n) {
 }
 
 uint32_t xcd_flag(const char *first, const Norm &n, bool pack) {
-  static const bool off = std::getenv("TEMPI_NO_XCD_MAP") != nullptr;
-  if (!TEMPI_XCD_MAP || off) return 0;
+  if (!TEMPI_XCD_MAP) return 0;
   if (TEMPI_XCD_PAGES && (!pack || TEMPI_XCD_PAGES_PACK) && partial_pages(n)) return kXcdRange;
   if (pack || n.nd == 0 || n.block >= TEMPI_XCD_MAX_BLOCK) return 0;
   const int64_t inner = n.str[n.nd - 1];
