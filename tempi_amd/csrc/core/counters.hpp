@@ -41,6 +41,9 @@ struct Counters {
   uint64_t pack_timed = 0, unpack_timed = 0;
   // host time (ns) inside the transport, for TEMPI_PRINT_COUNTERS
   uint64_t ns_isend = 0, ns_irecv = 0, ns_flush = 0, ns_events = 0, ns_testsome = 0, ns_wait = 0;
+  // neighbourhood collectives: plan lookup + posting the per-edge operations,
+  // and the MPI_Waitall that completes them (the call is blocking)
+  uint64_t ns_nbr_post = 0, ns_nbr_wait = 0;
   uint64_t progress_passes = 0, batches = 0, batched_items = 0;
 };
 

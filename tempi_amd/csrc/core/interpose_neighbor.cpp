@@ -210,6 +210,7 @@ int isir(const void *sendbuf, const int *scounts, const MPI_Aint *sdispls, const
          void *recvbuf, const int *rcounts, const MPI_Aint *rdispls, const MPI_Datatype *rtypes, MPI_Comm comm,
          const Neighbours &nb) {
   const std::vector<int> &in = nb.in, &out = nb.out;
+  const uint64_t t0 = tick();
   const Plan &plan = plan_for(sendbuf, scounts, sdispls, stypes, recvbuf, rcounts, rdispls, rtypes, comm, nb);
   const MPI_Comm c = plan.priv;
   const int tag = 0x4E41; // "NA": alone on the private communicator
@@ -240,6 +241,8 @@ int isir(const void *sendbuf, const int *scounts, const MPI_Aint *sdispls, const
   }
   if (!plan.copies.items.empty()) reqs.push_back(p2p::start_local_copies(plan.copies));
   p2p::start_queued();
+  tock(counters.ns_nbr_post, t0);
+  ScopedNs timer(counters.ns_nbr_wait);
   return MPI_Waitall(int(reqs.size()), reqs.data(), MPI_STATUSES_IGNORE);
 }
 
