@@ -183,6 +183,13 @@ void mark_ipc_broken(int world) {
   ipcBroken[size_t(world)] = 1;
 }
 
+// a peer's IPC handle mapped here; fault injection (tests):
+// TEMPI_FAULT_IPC_OPEN makes every mapping fail
+int open_ipc_handle(void **p, const void *handle) {
+  static const bool injectFault = std::getenv("TEMPI_FAULT_IPC_OPEN") != nullptr;
+  return injectFault ? 1 : tempi_hip_ipc_open_handle(p, handle);
+}
+
 // the sender's slab mapped into this process, or nullptr when it cannot be
 void *peer_pointer(const IpcDesc &d) {
   if (d.senderPid == int32_t(getpid())) return reinterpret_cast<void *>(d.rawPtr);
@@ -190,9 +197,7 @@ void *peer_pointer(const IpcDesc &d) {
   auto it = ipcOpen.find(key);
   if (it != ipcOpen.end()) return it->second;
   void *p = nullptr;
-  // fault injection (tests): TEMPI_FAULT_IPC_OPEN makes every mapping fail
-  static const bool injectFault = std::getenv("TEMPI_FAULT_IPC_OPEN") != nullptr;
-  const int e = injectFault ? 1 : tempi_hip_ipc_open_handle(&p, d.handle);
+  const int e = open_ipc_handle(&p, d.handle);
   if (e != 0) {
     LOG_WARN("cannot map rank " << d.senderWorld << "'s slab: " << tempi_hip_error_string(e));
     mark_ipc_broken(d.senderWorld);
@@ -308,8 +313,7 @@ const char *peer_object(const IpcCopyDesc &d) {
   if (it == ipcAllocOpen.end()) {
     forget_freed_allocs(d);
     void *p = nullptr;
-    static const bool injectFault = std::getenv("TEMPI_FAULT_IPC_OPEN") != nullptr;
-    const int e = injectFault ? 1 : tempi_hip_ipc_open_handle(&p, d.handle);
+    const int e = open_ipc_handle(&p, d.handle);
     if (e != 0) {
       LOG_WARN("cannot map rank " << d.senderWorld << "'s buffer: " << tempi_hip_error_string(e));
       mark_ipc_broken(d.senderWorld);

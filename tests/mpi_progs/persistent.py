@@ -57,14 +57,14 @@ def buf(seed):
 
 
 def ptr(b):
-    return b.data_ptr() if device else b.ctypes.data
+    return b.ctypes.data if isinstance(b, np.ndarray) else b.data_ptr()
 
 
 def host(b):
-    if device:
-        torch.cuda.synchronize()
-        return b.cpu().numpy()
-    return b
+    if isinstance(b, np.ndarray):  # (host receives of device sends, too)
+        return b
+    torch.cuda.synchronize()
+    return b.cpu().numpy()
 
 
 def refill(b, seed):

@@ -9,7 +9,8 @@ export TMPDIR=/tmp HYDRA_LAUNCHER=fork
 O=gpurun_out
 mkdir -p $O
 echo "== tests"
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 250 --timeout-method thread > $O/gpu_tests.log 2>&1
+# (TESTS=path limits the run, e.g. tests/test_round3_gpu.py)
+timeout -k 10 900 python -u -m pytest ${TESTS:-tests} -m gpu -x -v --timeout 250 --timeout-method thread > $O/gpu_tests.log 2>&1
 rc=$?; tail -n 3 $O/gpu_tests.log; [ $rc -eq 0 ] || exit $rc
 echo "== kab 2:18"
 # 3D 2:18 of the sweep: 23170 planes x 23170 rows, pitch 18, plane 23173*18;
