@@ -289,29 +289,35 @@ template <typename T, int ND> __device__ __forceinline__ T ld_packed(const KArgs
 // object's partial first / last chunk, stored word by word, release L2 at the
 // end. The store's buffer base is the wave's first active lane, whose chunk is
 // the lowest (chunks ascend with the lane). Internal flag bit, never a
-// TEMPI_HIP_ITEM_*.
+// TEMPI_HIP_ITEM_*. The store path exists only in the WTC ("write-through
+// compiled") instantiations of the kernels, which the host picks for folded
+// launches alone: compiled into every kernel, it cost the large 3D narrow-row
+// gathers a third of their rate (2 B : 18, 1 205 -> 810-832 GB/s; register
+// pressure of the unused path, profiles/r04/kab_218_r4s1.jsonl).
 constexpr uint32_t kWriteThrough = 1u << 30;
-__device__ __forceinline__ void st_packed(uint32_t flags, uint4 *p, const uint4 &v) {
-  if (flags & kWriteThrough) {
-    uint32_t off;
-    const __amdgpu_buffer_rsrc_t r = remote_rsrc(p, &off);
-    u32x4 x;
-    __builtin_memcpy(&x, &v, 16);
-    __builtin_amdgcn_raw_buffer_store_b128(x, r, int(off), 0, kSysScope);
-  } else {
-    st(p, v, kNtPacked);
+template <bool WTC> __device__ __forceinline__ void st_packed(uint32_t flags, uint4 *p, const uint4 &v) {
+  if constexpr (WTC) {
+    if (flags & kWriteThrough) {
+      uint32_t off;
+      const __amdgpu_buffer_rsrc_t r = remote_rsrc(p, &off);
+      u32x4 x;
+      __builtin_memcpy(&x, &v, 16);
+      __builtin_amdgcn_raw_buffer_store_b128(x, r, int(off), 0, kSysScope);
+      return;
+    }
   }
+  st(p, v, kNtPacked);
 }
 
 // the scatter's store of one strided-side word: write-through for 16-byte
 // words of a folded launch (the host sets kWriteThrough only when every
 // stride is >= 0 and the object spans < 2 GiB, so a wave's addresses ascend
 // with the lane from its first active lane and fit the buffer offset)
-template <int W> __device__ __forceinline__ void st_scatter(uint32_t flags, typename Word<W>::T *p,
-                                                            const typename Word<W>::T &v) {
-  if constexpr (W == 16) {
+template <int W, bool WTC>
+__device__ __forceinline__ void st_scatter(uint32_t flags, typename Word<W>::T *p, const typename Word<W>::T &v) {
+  if constexpr (W == 16 && WTC) {
     if (flags & kWriteThrough) {
-      st_packed(flags, p, v);
+      st_packed<true>(flags, p, v);
       return;
     }
   }
@@ -401,7 +407,7 @@ __device__ void partial_chunk(uint32_t c, const KArgs<ND> &a) {
 // workgroup `blk` of `nblk` working on one object (grid-stride over its
 // chunks, U chunks per lane per step; U = 1 makes workgroup blk handle exactly
 // chunks [blk * kBlock, (blk + 1) * kBlock) when nblk covers the object)
-template <int W, int ND, int U = Unroll<W>::U>
+template <int W, int ND, bool WTC, int U = Unroll<W>::U>
 __device__ __forceinline__ void pack_body(const KArgs<ND> &a, uint32_t blk, uint32_t nblk) {
   typedef typename Word<W>::T WT;
   constexpr int CW = 16 / W;
@@ -461,7 +467,7 @@ __device__ __forceinline__ void pack_body(const KArgs<ND> &a, uint32_t blk, uint
     for (int u = 0; u < U; ++u) {
       const uint32_t c = base + u * kBlock + threadIdx.x;
       if (full[u]) {
-        st_packed(a.flags, reinterpret_cast<uint4 *>(a.chunk0 + size_t(c) * 16), buf[u].v);
+        st_packed<WTC>(a.flags, reinterpret_cast<uint4 *>(a.chunk0 + size_t(c) * 16), buf[u].v);
       } else if (c < a.nchunks) {
         partial_chunk<W, ND, true>(c, a);
       }
@@ -469,7 +475,7 @@ __device__ __forceinline__ void pack_body(const KArgs<ND> &a, uint32_t blk, uint
   }
 }
 
-template <int W, int ND, int U = Unroll<W>::U>
+template <int W, int ND, bool WTC, int U = Unroll<W>::U>
 __device__ __forceinline__ void unpack_body(const KArgs<ND> &a, uint32_t blk, uint32_t nblk) {
   typedef typename Word<W>::T WT;
   constexpr int CW = 16 / W;
@@ -501,7 +507,7 @@ __device__ __forceinline__ void unpack_body(const KArgs<ND> &a, uint32_t blk, ui
         if (CW == 1 || (CW <= 8 && one_run<ND>(row, mdiv(q + (CW - 1), a.mwpr), dig, a))) {
 #pragma unroll
           for (int j = 0; j < CW; ++j) {
-            st_scatter<W>(a.flags, reinterpret_cast<WT *>(a.strided + off + int64_t(w) * W), buf[u].w[j]);
+            st_scatter<W, WTC>(a.flags, reinterpret_cast<WT *>(a.strided + off + int64_t(w) * W), buf[u].w[j]);
             if (j + 1 < CW && ++w == a.wpr) {
               w = 0;
               if constexpr (ND >= 1) off += a.stride[0];
@@ -510,7 +516,7 @@ __device__ __forceinline__ void unpack_body(const KArgs<ND> &a, uint32_t blk, ui
         } else {
 #pragma unroll
           for (int j = 0; j < CW; ++j) {
-            st_scatter<W>(a.flags, reinterpret_cast<WT *>(a.strided + off + int64_t(w) * W), buf[u].w[j]);
+            st_scatter<W, WTC>(a.flags, reinterpret_cast<WT *>(a.strided + off + int64_t(w) * W), buf[u].w[j]);
             if (j + 1 < CW && ++w == a.wpr) {
               w = 0;
               next_row<ND>(off, dig, a);
@@ -531,17 +537,17 @@ __device__ __forceinline__ bool needs_release(uint32_t flags, uint32_t tile, uin
   return !(flags & kWriteThrough) || tile == 0 || tile + 1 == ntiles;
 }
 
-template <int W, int ND>
+template <int W, int ND, bool WTC>
 __global__ __launch_bounds__(kBlock) void pack_kernel(const KArgs<ND> a, const Sig sg) {
   const uint32_t tile = xcd_tile(blockIdx.x, gridDim.x, a.flags);
-  pack_body<W, ND>(a, tile, gridDim.x);
+  pack_body<W, ND, WTC>(a, tile, gridDim.x);
   wg_signal(sg, needs_release(a.flags, tile, gridDim.x));
 }
 
-template <int W, int ND>
+template <int W, int ND, bool WTC>
 __global__ __launch_bounds__(kBlock) void unpack_kernel(const KArgs<ND> a, const Sig sg) {
   const uint32_t tile = xcd_tile(blockIdx.x, gridDim.x, a.flags);
-  unpack_body<W, ND>(a, tile, gridDim.x);
+  unpack_body<W, ND, WTC>(a, tile, gridDim.x);
   wg_signal(sg, needs_release(a.flags, tile, gridDim.x));
 }
 
@@ -565,7 +571,7 @@ __device__ __forceinline__ void unpack_il_tile(const KArgs<ND> &a, uint32_t tile
   const bool clean = c1 - c0 == uint32_t(kBlock) && int64_t(c0) * CW - a.head >= 0 &&
                      int64_t(c1) * CW - a.head <= int64_t(a.nwords);
   if (!clean) { // uniform: this tile's chunks, one per lane
-    unpack_body<W, ND, 1>(a, tileIdx, ntiles);
+    unpack_body<W, ND, false, 1>(a, tileIdx, ntiles);
     return;
   }
   tile[threadIdx.x] = ld_packed(a, reinterpret_cast<const uint4 *>(a.chunk0 + size_t(c0 + threadIdx.x) * 16), kNtPacked);
@@ -604,7 +610,7 @@ __device__ __forceinline__ void unpack_il_tile(const KArgs<ND> &a, uint32_t tile
 // the gather twin of unpack_il_kernel: load instruction j of a wave reads 64
 // consecutive words (neighbouring rows), the words are transposed through LDS,
 // and every lane writes one 16-byte packed chunk
-template <int W, int ND>
+template <int W, int ND, bool WTC>
 __device__ __forceinline__ void pack_il_tile(const KArgs<ND> &a, uint32_t tileIdx, uint32_t ntiles) {
   typedef typename Word<W>::T WT;
   constexpr int CW = 16 / W;
@@ -614,7 +620,7 @@ __device__ __forceinline__ void pack_il_tile(const KArgs<ND> &a, uint32_t tileId
   const bool clean = c1 - c0 == uint32_t(kBlock) && int64_t(c0) * CW - a.head >= 0 &&
                      int64_t(c1) * CW - a.head <= int64_t(a.nwords);
   if (!clean) { // uniform: this tile's chunks, one per lane
-    pack_body<W, ND, 1>(a, tileIdx, ntiles);
+    pack_body<W, ND, WTC, 1>(a, tileIdx, ntiles);
     return;
   }
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -650,12 +656,13 @@ __device__ __forceinline__ void pack_il_tile(const KArgs<ND> &a, uint32_t tileId
 #pragma unroll
   for (int j = 0; j < CW; ++j) dst[uint32_t(j) * 64 + lane] = v[j];
   __syncthreads();
-  st_packed(a.flags, reinterpret_cast<uint4 *>(a.chunk0 + size_t(c0 + threadIdx.x) * 16), tile[threadIdx.x]);
+  st_packed<WTC>(a.flags, reinterpret_cast<uint4 *>(a.chunk0 + size_t(c0 + threadIdx.x) * 16), tile[threadIdx.x]);
 }
 
-template <int W, int ND> __global__ __launch_bounds__(kBlock) void pack_il_kernel(const KArgs<ND> a, const Sig sg) {
+template <int W, int ND, bool WTC>
+__global__ __launch_bounds__(kBlock) void pack_il_kernel(const KArgs<ND> a, const Sig sg) {
   const uint32_t tile = xcd_tile(blockIdx.x, gridDim.x, a.flags);
-  pack_il_tile<W, ND>(a, tile, gridDim.x);
+  pack_il_tile<W, ND, WTC>(a, tile, gridDim.x);
   wg_signal(sg, needs_release(a.flags, tile, gridDim.x));
 }
 template <int W, int ND> __global__ __launch_bounds__(kBlock) void unpack_il_kernel(const KArgs<ND> a, const Sig sg) {
@@ -690,7 +697,7 @@ constexpr int kDenseMaxBlock = 32;
 // second workgroup on the CU (so <= 64 KiB)
 static_assert(kDenseLds <= 64 * 1024, "dense window too large for LDS");
 
-template <int ND>
+template <int ND, bool WTC>
 __device__ __forceinline__ void pack_dense_tile(const KArgs<ND> &a, uint32_t blk) {
   __shared__ uint4 win[kDenseLds / 16];
   const uint32_t c0 = blk * kBlock; // first chunk of this tile
@@ -702,7 +709,7 @@ __device__ __forceinline__ void pack_dense_tile(const KArgs<ND> &a, uint32_t blk
   bool oneSegment = true;
   if (ND >= 2) oneSegment = mdiv(rl, a.mcnt[0]) == mdiv(rh, a.mcnt[0]);
   if (!oneSegment) { // uniform: the per-word path for this tile only
-    pack_body<1, ND, 1>(a, blk, gridDim.x);
+    pack_body<1, ND, WTC, 1>(a, blk, gridDim.x);
     return;
   }
   uint32_t dig[ND > 0 ? ND : 1];
@@ -739,7 +746,7 @@ __device__ __forceinline__ void pack_dense_tile(const KArgs<ND> &a, uint32_t blk
         ++idx;
       }
     }
-    st_packed(a.flags, reinterpret_cast<uint4 *>(a.chunk0 + size_t(c) * 16), out.v);
+    st_packed<WTC>(a.flags, reinterpret_cast<uint4 *>(a.chunk0 + size_t(c) * 16), out.v);
   } else { // first / last chunk of the object: only its bytes
     for (int j = 0; j < 16; ++j) {
       const int64_t q = q0 + j;
@@ -751,10 +758,10 @@ __device__ __forceinline__ void pack_dense_tile(const KArgs<ND> &a, uint32_t blk
   }
 }
 
-template <int ND>
+template <int ND, bool WTC>
 __global__ __launch_bounds__(kBlock) void pack_dense_kernel(const KArgs<ND> a, const Sig sg) {
   const uint32_t tile = xcd_tile(blockIdx.x, gridDim.x, a.flags);
-  pack_dense_tile<ND>(a, tile);
+  pack_dense_tile<ND, WTC>(a, tile);
   wg_signal(sg, needs_release(a.flags, tile, gridDim.x));
 }
 
@@ -785,19 +792,19 @@ template <int ND> __device__ __forceinline__ uint32_t find_item(const BatchArgs<
 
 // (sg: a completion ticket folded into the launch, as in the single-object
 // kernels; a workgroup's partial chunks are its item's first / last tile)
-template <int W, int ND>
+template <int W, int ND, bool WTC>
 __global__ __launch_bounds__(kBlock) void pack_batch_kernel(const BatchArgs<ND> b, const Sig sg) {
   const uint32_t i = find_item<ND>(b, blockIdx.x), n = b.first[i + 1] - b.first[i];
   const uint32_t blk = xcd_tile(blockIdx.x - b.first[i], n, b.item[i].flags); // (within the item: balanced)
-  pack_body<W, ND>(b.item[i], blk, n);
+  pack_body<W, ND, WTC>(b.item[i], blk, n);
   wg_signal(sg, needs_release(b.item[i].flags, blk, n));
 }
 
-template <int W, int ND>
+template <int W, int ND, bool WTC>
 __global__ __launch_bounds__(kBlock) void pack_il_batch_kernel(const BatchArgs<ND> b, const Sig sg) {
   const uint32_t i = find_item<ND>(b, blockIdx.x), n = b.first[i + 1] - b.first[i];
   const uint32_t blk = xcd_tile(blockIdx.x - b.first[i], n, b.item[i].flags); // (within the item: balanced)
-  pack_il_tile<W, ND>(b.item[i], blk, n);
+  pack_il_tile<W, ND, WTC>(b.item[i], blk, n);
   wg_signal(sg, needs_release(b.item[i].flags, blk, n));
 }
 template <int W, int ND>
@@ -808,11 +815,11 @@ __global__ __launch_bounds__(kBlock) void unpack_il_batch_kernel(const BatchArgs
   wg_signal(sg, true);
 }
 
-template <int W, int ND>
+template <int W, int ND, bool WTC>
 __global__ __launch_bounds__(kBlock) void unpack_batch_kernel(const BatchArgs<ND> b, const Sig sg) {
   const uint32_t i = find_item<ND>(b, blockIdx.x), n = b.first[i + 1] - b.first[i];
   const uint32_t blk = xcd_tile(blockIdx.x - b.first[i], n, b.item[i].flags); // (within the item: balanced)
-  unpack_body<W, ND>(b.item[i], blk, n);
+  unpack_body<W, ND, WTC>(b.item[i], blk, n);
   wg_signal(sg, needs_release(b.item[i].flags, blk, n));
 }
 
@@ -1033,11 +1040,17 @@ int launch_nd(bool pack, char *packed, char *first, const Norm &n, hipStream_t s
   const bool wt = pack || (W == 16 && scatter_write_through(n));
   const Sig sg = take_fold(blocks, wt);
   if (sg.flag && wt) a.flags |= kWriteThrough;
+  // (a scatter stores write-through only with 16-byte words: no WTC twin below)
+  constexpr bool kScatterWT = W == 16;
+  const bool wtc = (a.flags & kWriteThrough) != 0;
   if (pack) {
-    if (!aql_launch<KArgs<ND>>(pack_kernel<W, ND>, blocks, s, a, sg))
-      hipLaunchKernelGGL((pack_kernel<W, ND>), dim3(blocks), dim3(kBlock), 0, s, a, sg);
-  } else if (!aql_launch<KArgs<ND>>(unpack_kernel<W, ND>, blocks, s, a, sg)) {
-    hipLaunchKernelGGL((unpack_kernel<W, ND>), dim3(blocks), dim3(kBlock), 0, s, a, sg);
+    auto *k = wtc ? pack_kernel<W, ND, true> : pack_kernel<W, ND, false>;
+    if (!aql_launch<KArgs<ND>>(k, blocks, s, a, sg))
+      hipLaunchKernelGGL(k, dim3(blocks), dim3(kBlock), 0, s, a, sg);
+  } else {
+    auto *k = wtc ? unpack_kernel<W, ND, kScatterWT> : unpack_kernel<W, ND, false>;
+    if (!aql_launch<KArgs<ND>>(k, blocks, s, a, sg))
+      hipLaunchKernelGGL(k, dim3(blocks), dim3(kBlock), 0, s, a, sg);
   }
   return int(hipGetLastError());
 }
@@ -1061,24 +1074,32 @@ int launch_batch_nd(bool pack, const std::vector<Job> &jobs, hipStream_t s, temp
     if (!b.nitems) return 0;
     b.first[b.nitems] = total;
     Sig sg{};
+    bool wtc = false; // some item stores write-through: the WTC instantiation
     if (last && fold && total) {
       bool all = true;
       for (uint32_t k = 0; k < b.nitems; ++k) all &= wt[k];
       sg = take_fold_from(fold, total, all);
       if (sg.flag)
         for (uint32_t k = 0; k < b.nitems; ++k)
-          if (wt[k]) b.item[k].flags |= kWriteThrough;
+          if (wt[k]) {
+            b.item[k].flags |= kWriteThrough;
+            wtc = true;
+          }
     }
+    constexpr bool kScatterWT = W == 16;
     if (total) {
       if (il)
         if (pack)
-          hipLaunchKernelGGL((pack_il_batch_kernel<W, ND>), dim3(total), dim3(kBlock), 0, s, b, sg);
+          hipLaunchKernelGGL((wtc ? pack_il_batch_kernel<W, ND, true> : pack_il_batch_kernel<W, ND, false>),
+                             dim3(total), dim3(kBlock), 0, s, b, sg);
         else
           hipLaunchKernelGGL((unpack_il_batch_kernel<W, ND>), dim3(total), dim3(kBlock), 0, s, b, sg);
       else if (pack)
-        hipLaunchKernelGGL((pack_batch_kernel<W, ND>), dim3(total), dim3(kBlock), 0, s, b, sg);
+        hipLaunchKernelGGL((wtc ? pack_batch_kernel<W, ND, true> : pack_batch_kernel<W, ND, false>), dim3(total),
+                           dim3(kBlock), 0, s, b, sg);
       else
-        hipLaunchKernelGGL((unpack_batch_kernel<W, ND>), dim3(total), dim3(kBlock), 0, s, b, sg);
+        hipLaunchKernelGGL((wtc ? unpack_batch_kernel<W, ND, kScatterWT> : unpack_batch_kernel<W, ND, false>),
+                           dim3(total), dim3(kBlock), 0, s, b, sg);
     }
     b.nitems = 0;
     total = 0;
@@ -1156,8 +1177,9 @@ template <int ND> int launch_dense_nd(char *packed, char *first, const Norm &n, 
   if (blocks == 0) return 0;
   const Sig sg = take_fold(blocks, true);
   if (sg.flag) a.flags |= kWriteThrough;
-  if (!aql_launch<KArgs<ND>>(pack_dense_kernel<ND>, blocks, s, a, sg))
-    hipLaunchKernelGGL((pack_dense_kernel<ND>), dim3(blocks), dim3(kBlock), 0, s, a, sg);
+  auto *k = sg.flag ? pack_dense_kernel<ND, true> : pack_dense_kernel<ND, false>;
+  if (!aql_launch<KArgs<ND>>(k, blocks, s, a, sg))
+    hipLaunchKernelGGL(k, dim3(blocks), dim3(kBlock), 0, s, a, sg);
   return int(hipGetLastError());
 }
 
@@ -1182,8 +1204,9 @@ template <int W, int ND> int launch_il_nd(bool pack, char *packed, char *first, 
   const Sig sg = take_fold(blocks, pack);
   if (sg.flag && pack) a.flags |= kWriteThrough;
   if (pack) {
-    if (!aql_launch<KArgs<ND>>(pack_il_kernel<W, ND>, blocks, s, a, sg))
-      hipLaunchKernelGGL((pack_il_kernel<W, ND>), dim3(blocks), dim3(kBlock), 0, s, a, sg);
+    auto *k = sg.flag ? pack_il_kernel<W, ND, true> : pack_il_kernel<W, ND, false>;
+    if (!aql_launch<KArgs<ND>>(k, blocks, s, a, sg))
+      hipLaunchKernelGGL(k, dim3(blocks), dim3(kBlock), 0, s, a, sg);
   } else if (!aql_launch<KArgs<ND>>(unpack_il_kernel<W, ND>, blocks, s, a, sg)) {
     hipLaunchKernelGGL((unpack_il_kernel<W, ND>), dim3(blocks), dim3(kBlock), 0, s, a, sg);
   }
