@@ -30,7 +30,7 @@ build/hip/%.o: tempi_amd/csrc/hip/%.hip include/tempi_hip.h
 
 $(LIB)/libtempi_hip.so: $(HIP_OBJ)
 	@mkdir -p $(LIB)
-	$(HIPCC) --offload-arch=gfx950 -shared -fPIC -o $@ $^ -L$(ROCM)/lib -lhsa-runtime64 -Wl,-rpath,$(ROCM)/lib
+	$(HIPCC) --offload-arch=gfx950 -shared -fPIC -o $@ $^ -Wl,-rpath,$(ROCM)/lib
 
 build/core/%.o: tempi_amd/csrc/core/%.cpp $(CORE_HDR)
 	@mkdir -p build/core

@@ -52,8 +52,6 @@ typedef struct tempi_counters_t {
   uint64_t sync_waits;     /* ... completed by hipStreamSynchronize (kernel wrote application host memory) */
   uint64_t ticket_batches; /* transport batches whose last launch stored a completion ticket (no event) */
   uint64_t persistent_starts; /* MPI_Start / MPI_Startall of persistent requests TEMPI holds */
-  uint64_t direct_pregathers; /* sends to this process gathered before their receive existed (TEMPI_PREGATHER_BYTES) */
-  uint64_t aql_dispatches;    /* synchronous launches dispatched by TEMPI's own AQL packets (TEMPI_AQL=1) */
 } tempi_counters_t;
 void tempi_get_counters(tempi_counters_t *out);
 void tempi_reset_counters(void);

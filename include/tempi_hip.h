@@ -171,18 +171,6 @@ int tempi_hip_stream_ticket(void *stream, const uint32_t **flag, uint32_t *ticke
 int tempi_hip_ticket_wait(void *stream, const uint32_t *flag, uint32_t ticket);
 /* tickets issued so far: stored by the work kernel itself / by a ticket kernel */
 void tempi_hip_ticket_stats(uint64_t *folded, uint64_t *queued);
-/* TEMPI_AQL=1: a synchronous pack / unpack whose one launch stores its own
-   ticket is dispatched by a packet TEMPI writes into an HSA queue of its own
-   instead of hipLaunchKernelGGL. allow(0) turns that off (while HIP events
-   on the stream time the launches), allow(1) back on */
-void tempi_hip_aql_allow(int on);
-/* launches dispatched that way / refused (kernel object not found, argument
-   layout not the expected one) */
-void tempi_hip_aql_stats(uint64_t *dispatched, uint64_t *refused);
-/* bytes of the explicit kernel arguments (descriptor of rank nd + ticket) as
-   the host lays them out in an AQL packet's kernarg slot (tests check it
-   against the code object's metadata); -1 for an unknown rank */
-int64_t tempi_hip_aql_arg_bytes(int nd);
 int tempi_hip_stream_wait_event(void *stream, void *event);
 /* flags: bit 0 = timing enabled, bit 1 = blocking sync, bit 2 = interprocess */
 int tempi_hip_event_create(void **event, int flags);

@@ -22,7 +22,6 @@ struct Counters {
   uint64_t ticket_waits = 0, sync_waits = 0;
   uint64_t ticket_batches = 0; // transport batches completed by a ticket their last launch stored
   uint64_t persistent_starts = 0; // MPI_Start of a TEMPI persistent request
-  uint64_t direct_pregathers = 0; // direct sends gathered before their receive (TEMPI_PREGATHER_BYTES)
   uint64_t sends = 0, recvs = 0, isends = 0, irecvs = 0;
   uint64_t send_device = 0, send_oneshot = 0, send_staged = 0, send_ipc = 0;
   uint64_t lib_sends = 0, lib_recvs = 0;

@@ -77,9 +77,6 @@ TEMPI_EXPORT void tempi_get_counters(tempi_counters_t *o) {
   o->sync_waits = c.sync_waits;
   o->ticket_batches = c.ticket_batches;
   o->persistent_starts = c.persistent_starts;
-  o->direct_pregathers = c.direct_pregathers;
-  uint64_t refused = 0;
-  tempi_hip_aql_stats(&o->aql_dispatches, &refused);
 }
 
 TEMPI_EXPORT void tempi_reset_counters(void) {
@@ -89,7 +86,6 @@ TEMPI_EXPORT void tempi_reset_counters(void) {
 
 TEMPI_EXPORT void tempi_set_kernel_profiling(int on) {
   kernelProfiling = on != 0;
-  tempi_hip_aql_allow(!kernelProfiling); // (events on the stream would not see launches on the AQL queue)
 }
 
 TEMPI_EXPORT void tempi_get_kernel_times(tempi_kernel_times *o) {

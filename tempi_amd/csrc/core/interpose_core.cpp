@@ -145,14 +145,13 @@ void finalize_before_mpi() {
     const Counters &c = counters;
     std::fprintf(stderr,
                  "[tempi r%d] packs=%lu unpacks=%lu isends=%lu irecvs=%lu ipc=%lu (copy %lu/%lu) oneshot=%lu staged=%lu "
-                 "direct=%lu/%lu pregathers=%lu "
+                 "direct=%lu/%lu "
                  "batches=%lu items=%lu passes=%lu | host ms: isend=%.2f irecv=%.2f flush=%.2f events=%.2f "
                  "testsome=%.2f wait=%.2f | nbr=%lu post=%.2f wait=%.2f | slabs MB: device=%.1f pinned=%.1f\n",
                  state.worldRank, (unsigned long)c.packs, (unsigned long)c.unpacks, (unsigned long)c.isends,
                  (unsigned long)c.irecvs, (unsigned long)c.send_ipc, (unsigned long)c.send_ipc_copy,
                  (unsigned long)c.copy_resends, (unsigned long)c.send_oneshot,
                  (unsigned long)c.send_staged, (unsigned long)c.send_direct, (unsigned long)c.direct_fallbacks,
-                 (unsigned long)c.direct_pregathers,
                  (unsigned long)c.batches, (unsigned long)c.batched_items,
                  (unsigned long)c.progress_passes, c.ns_isend * 1e-6, c.ns_irecv * 1e-6, c.ns_flush * 1e-6,
                  c.ns_events * 1e-6, c.ns_testsome * 1e-6, c.ns_wait * 1e-6, (unsigned long)c.neighbor_colls,

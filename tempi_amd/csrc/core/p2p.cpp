@@ -72,11 +72,6 @@ void init() {
   if (const char *s = std::getenv("TEMPI_IPC_COPY_MIN_BYTES")) ipcCopyMinBytes = std::atoll(s);
   if (const char *s = std::getenv("TEMPI_IPC_COPY_MIN_BLOCK")) ipcCopyMinBlock = std::atoll(s);
   scattersInFlight = 0;
-  pregatherBytes = 0;
-  if (const char *s = std::getenv("TEMPI_PREGATHER_BYTES")) pregatherBytes = std::atoll(s);
-  if (const char *s = std::getenv("TEMPI_PREGATHER_MAX_BLOCK")) pregatherMaxBlock = std::atoll(s);
-  if (const char *s = std::getenv("TEMPI_PREGATHER_FLUSH")) pregatherFlush = std::max<int64_t>(1, std::atoll(s));
-  pregatherUsed = pregatherQueued = 0;
   directShared.clear();
   directShared.reserve(512);
   active.reserve(2048);
@@ -173,10 +168,6 @@ int isend(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Co
       rec->flat(count, &flat)) {
     counters.send_direct++;
     *req = add(new_isend_direct(rec, origin, count, dt, dest, tag, comm, p.device, bytes, flat));
-    if (pregatherQueued >= pregatherFlush) { // launch the burst's pre-gathers so far
-      pregatherQueued = 0;
-      flush_list(pendingPack, true);
-    }
     return MPI_SUCCESS;
   }
   if (destWorld == state.worldRank) spill_channel(comm); // a message to this rank the self channel cannot carry

@@ -359,13 +359,6 @@ constexpr size_t kMaxPending = 512;
 constexpr size_t kEarlyFlush = 32;
 constexpr size_t kFirstFlush = 16;
 extern int scattersInFlight;   // scatter / copy batches launched and not yet seen complete
-// Pre-gather (TEMPI_PREGATHER_BYTES, 0 = off): a direct send to this process
-// whose receive is not posted yet, of rows <= pregatherMaxBlock bytes, is
-// gathered into a slab at once while no scatter batch is in flight (the GPU
-// would idle through a send burst), up to pregatherBytes per burst; queued
-// pre-gathers launch every pregatherFlush bytes
-extern int64_t pregatherBytes, pregatherMaxBlock, pregatherFlush;
-extern int64_t pregatherUsed, pregatherQueued;
 void flush_list(PendingList &list, bool pack);
 void flush();
 

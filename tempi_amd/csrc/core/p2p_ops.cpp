@@ -160,8 +160,6 @@ void PendingList::add_items(const Op *op, const Packer &pk, void *packed, const 
 PendingList pendingPack, pendingUnpack;
 int64_t bufferedUnposted = 0;
 int scattersInFlight = 0;
-int64_t pregatherBytes = 0, pregatherMaxBlock = 64, pregatherFlush = int64_t(4) << 20;
-int64_t pregatherUsed = 0, pregatherQueued = 0;
 
 namespace {
 template <typename T> const T *select(const std::vector<T> &v, const std::vector<int> &dev, int d, bool all,
@@ -239,7 +237,6 @@ void flush_list(PendingList &list, bool pack) {
     b->stream = s;
     if (!pack) {
       ++scattersInFlight;
-      pregatherUsed = 0; // the receives have come: the next send burst has its own budget
     }
     if (flag) {
       counters.ticket_batches++;
@@ -414,13 +411,6 @@ struct IsendDirectOp : Op {
   MPI_Comm comm;
   void post() override {
     if (self_send(sh, comm, tag)) {
-      if (sh->state == DirectShared::PENDING && pregatherBytes > 0 && scattersInFlight == 0 &&
-          rec->desc.block <= pregatherMaxBlock && pregatherUsed + bytes <= pregatherBytes) {
-        pregatherUsed += bytes;
-        pregatherQueued += bytes;
-        counters.direct_pregathers++;
-        gather();
-      }
       maybe_done();
       return;
     }

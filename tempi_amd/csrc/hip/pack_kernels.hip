@@ -34,7 +34,6 @@
 #include <hip/hip_runtime.h>
 
 #include "tempi_hip.h"
-#include "aql.hpp"
 #include "ticket.hpp"
 
 #include <cstdint>
@@ -941,31 +940,6 @@ thread_local uint32_t gItemFlags = 0;
 // the completion-ticket fold offered to this thread's next single-object
 // launch (the *_ticket entry points set it around their launch)
 thread_local tempi_ticket::Fold *gFold = nullptr;
-// the AQL queue this thread's next folded single-object launch is dispatched
-// on instead of its stream (with_ticket sets it; aql.hpp)
-thread_local tempi_aql::Queue *gAql = nullptr;
-bool gAqlAllowed = true; // tempi_hip_aql_allow: off while HIP events time the launches
-
-// a kernel's (A a, Sig sg) arguments as the host lays them out for an AQL
-// packet: a at 0, sg behind it at its alignment (the kernel ABI's by-value
-// layout; tests/test_aql_layout_cpu.py checks it against the code object)
-template <typename A> struct KernelArgs {
-  A a;
-  Sig sg;
-  static constexpr size_t bytes() { return offsetof(KernelArgs, sg) + sizeof(Sig); }
-};
-
-// dispatch `kernel` (a, sg) over `blocks` workgroups of kBlock lanes on the
-// AQL queue when one is offered and the launch stores the ticket itself;
-// false: the caller launches it on its stream as usual
-template <typename A>
-bool aql_launch(void (*kernel)(const A, const Sig), uint32_t blocks, hipStream_t s, const A &a, const Sig &sg) {
-  if (!gAql || !sg.flag) return false;
-  const KernelArgs<A> p{a, sg};
-  return tempi_aql::dispatch(gAql, reinterpret_cast<const void *>(kernel), s, blocks, kBlock, &p,
-                             KernelArgs<A>::bytes());
-}
-
 // a 16-byte-word scatter may store write-through (st_scatter): every stride
 // >= 0 and the object's span below 2 GiB
 bool scatter_write_through(const Norm &n) {
@@ -1045,12 +1019,10 @@ int launch_nd(bool pack, char *packed, char *first, const Norm &n, hipStream_t s
   const bool wtc = (a.flags & kWriteThrough) != 0;
   if (pack) {
     auto *k = wtc ? pack_kernel<W, ND, true> : pack_kernel<W, ND, false>;
-    if (!aql_launch<KArgs<ND>>(k, blocks, s, a, sg))
-      hipLaunchKernelGGL(k, dim3(blocks), dim3(kBlock), 0, s, a, sg);
+    hipLaunchKernelGGL(k, dim3(blocks), dim3(kBlock), 0, s, a, sg);
   } else {
     auto *k = wtc ? unpack_kernel<W, ND, kScatterWT> : unpack_kernel<W, ND, false>;
-    if (!aql_launch<KArgs<ND>>(k, blocks, s, a, sg))
-      hipLaunchKernelGGL(k, dim3(blocks), dim3(kBlock), 0, s, a, sg);
+    hipLaunchKernelGGL(k, dim3(blocks), dim3(kBlock), 0, s, a, sg);
   }
   return int(hipGetLastError());
 }
@@ -1178,8 +1150,7 @@ template <int ND> int launch_dense_nd(char *packed, char *first, const Norm &n, 
   const Sig sg = take_fold(blocks, true);
   if (sg.flag) a.flags |= kWriteThrough;
   auto *k = sg.flag ? pack_dense_kernel<ND, true> : pack_dense_kernel<ND, false>;
-  if (!aql_launch<KArgs<ND>>(k, blocks, s, a, sg))
-    hipLaunchKernelGGL(k, dim3(blocks), dim3(kBlock), 0, s, a, sg);
+  hipLaunchKernelGGL(k, dim3(blocks), dim3(kBlock), 0, s, a, sg);
   return int(hipGetLastError());
 }
 
@@ -1205,9 +1176,8 @@ template <int W, int ND> int launch_il_nd(bool pack, char *packed, char *first, 
   if (sg.flag && pack) a.flags |= kWriteThrough;
   if (pack) {
     auto *k = sg.flag ? pack_il_kernel<W, ND, true> : pack_il_kernel<W, ND, false>;
-    if (!aql_launch<KArgs<ND>>(k, blocks, s, a, sg))
-      hipLaunchKernelGGL(k, dim3(blocks), dim3(kBlock), 0, s, a, sg);
-  } else if (!aql_launch<KArgs<ND>>(unpack_il_kernel<W, ND>, blocks, s, a, sg)) {
+    hipLaunchKernelGGL(k, dim3(blocks), dim3(kBlock), 0, s, a, sg);
+  } else {
     hipLaunchKernelGGL((unpack_il_kernel<W, ND>), dim3(blocks), dim3(kBlock), 0, s, a, sg);
   }
   return int(hipGetLastError());
@@ -1693,14 +1663,7 @@ int with_ticket(bool pack, char *packed, char *first, const tempi_hip_desc *d, h
   bool single = norm_bytes(n) < kMaxLaunchBytes; // launch_split makes exactly one launch
   for (int k = 0; k < n.nd; ++k) single &= n.cnt[k] < (int64_t(1) << 32);
   std::lock_guard<std::mutex> lock(tempi_ticket::mutex());
-  // one launch that stores its own ticket may go to the AQL queue (aql.hpp);
-  // the call then completes on that queue's ticket, whichever way it launched
-  tempi_aql::Queue *aq = single && gAqlAllowed ? tempi_aql::for_stream(s) : nullptr;
-  tempi_ticket::Ticket *t = aq ? tempi_ticket::of_aql(aq, s) : nullptr;
-  if (!t) {
-    aq = nullptr;
-    t = tempi_ticket::of(s);
-  }
+  tempi_ticket::Ticket *t = tempi_ticket::of(s);
   if (!t) return int(hipErrorOutOfMemory);
   tempi_ticket::Fold fold;
   fold.t = t;
@@ -1708,10 +1671,8 @@ int with_ticket(bool pack, char *packed, char *first, const tempi_hip_desc *d, h
   fold.max_blocks = single ? tempi_ticket::fold_max_blocks() : 0;
   fold.max_blocks_wt = single ? tempi_ticket::fold_max_blocks_wt() : 0;
   gFold = &fold;
-  gAql = aq;
   const int e = launch_split(pack, packed, first, n, s);
   gFold = nullptr;
-  gAql = nullptr;
   if (e) {
     if (fold.taken) t->broken = true; // the host counted a launch that never ran
     return e;
@@ -1754,29 +1715,6 @@ template <typename F> int batch_with_ticket(hipStream_t s, const uint32_t **flag
 } // namespace
 
 extern "C" {
-
-void tempi_hip_aql_allow(int on) {
-  std::lock_guard<std::mutex> lock(tempi_ticket::mutex());
-  gAqlAllowed = on != 0;
-}
-
-int64_t tempi_hip_aql_arg_bytes(int nd) {
-  switch (nd) {
-  case 0: return int64_t(KernelArgs<KArgs<0>>::bytes());
-  case 1: return int64_t(KernelArgs<KArgs<1>>::bytes());
-  case 2: return int64_t(KernelArgs<KArgs<2>>::bytes());
-  case 3: return int64_t(KernelArgs<KArgs<3>>::bytes());
-  case 4: return int64_t(KernelArgs<KArgs<4>>::bytes());
-  case 5: return int64_t(KernelArgs<KArgs<5>>::bytes());
-  default: return -1;
-  }
-}
-
-void tempi_hip_aql_stats(uint64_t *dispatched, uint64_t *refused) {
-  const tempi_aql::Stats st = tempi_aql::stats();
-  *dispatched = st.dispatched;
-  *refused = st.refused;
-}
 
 int tempi_hip_pack_ticket(void *packed, const void *first, const tempi_hip_desc *d, void *stream,
                           const uint32_t **flag, uint32_t *ticket) {

@@ -11,7 +11,6 @@
 // of MPI_Pack (/root/reference/src/pack.cpp:42-49).
 #include <hip/hip_runtime.h>
 
-#include "aql.hpp"
 #include "tempi_hip.h"
 #include "ticket.hpp"
 
@@ -135,10 +134,6 @@ __global__ void signal_ticket(uint32_t *flag, uint32_t ticket) {
 // one flag per stream: tickets reach a stream in increasing order (issued
 // under the mutex), so a flag >= mine means the work before my ticket is done
 std::unordered_map<void *, tempi_ticket::Ticket> tickets;
-// flags of the AQL queues' tickets (read by waits without the mutex)
-constexpr int kMaxAqlFlags = 64;
-std::atomic<const uint32_t *> aqlFlags[kMaxAqlFlags];
-std::atomic<int> nAqlFlags{0};
 } // namespace
 
 namespace tempi_ticket {
@@ -153,29 +148,8 @@ Stats &stats() {
   return s;
 }
 
-Ticket *of(hipStream_t s) { return of_key(s, s); }
-
-Ticket *of_aql(void *key, hipStream_t s) {
-  Ticket *t = of_key(key, s);
-  if (t && !t->aql) {
-    const int i = nAqlFlags.load();
-    if (i >= kMaxAqlFlags) return nullptr; // (one queue per device: never)
-    t->aql = true;
-    aqlFlags[i].store(t->host);
-    nAqlFlags.store(i + 1);
-  }
-  return t;
-}
-
-bool is_aql_flag(const uint32_t *flag) {
-  const int n = nAqlFlags.load();
-  for (int i = 0; i < n; ++i)
-    if (aqlFlags[i].load() == flag) return true;
-  return false;
-}
-
-Ticket *of_key(void *key, hipStream_t s) {
-  Ticket &t = tickets[key];
+Ticket *of(hipStream_t s) {
+  Ticket &t = tickets[s];
   if (!t.host) {
     void *h = nullptr, *d = nullptr;
     hipError_t e = hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable);
@@ -214,13 +188,11 @@ hipError_t queue_kernel(Ticket &t, hipStream_t s, uint32_t ticket) {
 }
 
 int wait(hipStream_t s, const uint32_t *flag, uint32_t ticket) {
-  const bool aql = is_aql_flag(flag); // (the work may be on the AQL queue: `s` idle says nothing)
   for (uint32_t spins = 1;; ++spins) {
     if (int32_t(__atomic_load_n(flag, __ATOMIC_ACQUIRE) - ticket) >= 0) return 0;
     if ((spins & 1023) == 0) { // ~20 µs of pause loops
-      if (aql && tempi_aql::failed()) return int(hipErrorLaunchFailure);
       const hipError_t e = hipStreamQuery(s);
-      if (e == hipSuccess && !aql) return 0;
+      if (e == hipSuccess) return 0;
       if (e != hipSuccess && e != hipErrorNotReady) return int(e);
     }
     __builtin_ia32_pause();

@@ -58,7 +58,6 @@ struct Ticket {
   uint32_t *counter = nullptr;              // device: kShards shard counters + the top counter
   uint32_t counted[kShards + 1] = {};       // the host's running totals of the same (mod 2^32)
   bool broken = false;                      // a folded launch failed: counters and totals disagree
-  bool aql = false;                         // the ticket of an AQL queue (aql.hpp), not of a stream
 };
 
 // tickets stored by work kernels / by the ticket kernel, all streams
@@ -91,12 +90,6 @@ std::mutex &mutex();
 // the stream's ticket state, flag and counter allocated on first use
 // (caller holds mutex()); nullptr when allocation failed
 Ticket *of(hipStream_t s);
-// the same for an AQL queue (key): its own flag and counters, initialised
-// through stream s (caller holds mutex())
-Ticket *of_aql(void *key, hipStream_t s);
-Ticket *of_key(void *key, hipStream_t s);
-// the flag belongs to an AQL queue's ticket: an idle stream says nothing
-bool is_aql_flag(const uint32_t *flag);
 // queue the one-lane ticket kernel storing `ticket` (caller holds mutex())
 hipError_t queue_kernel(Ticket &t, hipStream_t s, uint32_t ticket);
 // spin until the flag reaches `ticket`; the stream is queried every ~20 us,

@@ -11,7 +11,7 @@ mkdir -p tools/_variants
 rm -f tools/_variants/*.so
 build() { # name dir [flags]
   hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Iinclude $3 \
-    -o tools/_variants/libtempi_hip_$1.so $2/*.hip -Wl,-rpath,/opt/rocm/lib -L/opt/rocm/lib -lhsa-runtime64
+    -o tools/_variants/libtempi_hip_$1.so $2/*.hip -Wl,-rpath,/opt/rocm/lib
 }
 build cur tempi_amd/csrc/hip &
 for ref in "$@"; do
