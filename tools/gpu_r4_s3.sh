@@ -23,6 +23,11 @@ echo "== kab"
 # pitch 4608, 518 rows per plane: plane stride 2386944
 bash tools/kab.sh kab_r4s3.jsonl 2 20 2:23170:417114:23170:18 2:536870912:18 512:2097152:1024 \
   24:512:2386944:512:4608 4096:512:2386944:3:4608 4096:3:2386944:512:4608 || exit 5
+echo "== hbench: the halo's regions as batches (copy GB/s per class, host time per batch)"
+for v in cur ab92370_; do
+  timeout -k 10 200 tools/_variants/hbench tools/_variants/libtempi_hip_$v.so 10 > $O/hbench_$v.jsonl || exit 7
+  cut -c1-400 $O/hbench_$v.jsonl
+done
 echo "== halo 1 rank, counters"
 : > $O/halo1_counters.txt
 for rep in 1 2; do

@@ -9,9 +9,11 @@
 //   unpack packed slab  -> exterior(-d)          (tempi_hip_unpack_batch)
 //   copy   interior(d)  -> exterior(-d) directly (tempi_hip_copy_batch)
 // over QUANTS buffers, and prints one JSON line per class with the kernel time
-// and the algorithmic GB/s (2 x payload per launch set).
+// and the algorithmic GB/s (2 x payload per launch set), plus the host time of
+// one tempi_hip_copy_batch call (planning + launch; copy_host_us).
 #include "tempi_hip.h"
 
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -144,6 +146,7 @@ int main(int argc, char **argv) {
         cp.push_back(cc);
       }
     float ms[3];
+    double hostUs = 0;
     for (int mode = 0; mode < 3; ++mode) {
       auto run = [&]() -> int {
         if (mode == 0) return tempi_hip_pack_batch(pk.data(), int(pk.size()), s);
@@ -153,7 +156,10 @@ int main(int argc, char **argv) {
       CK(run());
       CK(run());
       CK(tempi_hip_event_record(e0, s));
+      const auto h0 = std::chrono::steady_clock::now();
       for (int i = 0; i < reps; ++i) CK(run());
+      if (mode == 2)
+        hostUs = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - h0).count() / reps;
       CK(tempi_hip_event_record(e1, s));
       CK(tempi_hip_event_synchronize(e1));
       CK(tempi_hip_event_elapsed_ms(&ms[mode], e0, e1));
@@ -162,9 +168,9 @@ int main(int argc, char **argv) {
     auto gbs = [&](float m) { return 2.0 * double(payload) / (double(m) * 1e-3) / 1e9; };
     std::printf("{\"lib\": \"%s\", \"class\": \"%s\", \"items\": %zu, \"payload\": %lld, \"pack_us\": %.1f, "
                 "\"unpack_us\": %.1f, \"copy_us\": %.1f, \"pack_gbs\": %.1f, \"unpack_gbs\": %.1f, "
-                "\"copy_gbs\": %.1f}\n",
+                "\"copy_gbs\": %.1f, \"copy_host_us\": %.2f}\n",
                 argv[1], c.name, cp.size(), payload, ms[0] * 1e3, ms[1] * 1e3, ms[2] * 1e3, gbs(ms[0]), gbs(ms[1]),
-                gbs(ms[2]));
+                gbs(ms[2]), hostUs);
     std::fflush(stdout);
   }
   return 0;
