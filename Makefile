@@ -46,30 +46,30 @@ $(LIB)/libtempi.so: $(CORE_OBJ) $(LIB)/libtempi_hip.so
 # applications link -ltempi BEFORE the MPI library, like any TEMPI user
 $(LIB)/libtempi_apps.so: apps/halo_lib.cpp apps/bench_lib.cpp $(LIB)/libtempi.so
 	$(HIPCC) --offload-arch=gfx950 -O2 -std=c++17 -fPIC -shared -Iinclude -I$(MPI_HOME)/include -o $@ apps/halo_lib.cpp apps/bench_lib.cpp \
-	    -L$(LIB) -ltempi -L$(MPI_HOME)/lib -lmpi -static-libstdc++ -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,$(MPI_HOME)/lib
+	    -L$(LIB) -ltempi -ltempi_hip -L$(MPI_HOME)/lib -lmpi -static-libstdc++ -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,$(MPI_HOME)/lib
 
 $(LIB)/halo_exchange: apps/halo_exchange_main.cpp $(LIB)/libtempi_apps.so
 	$(HIPCC) --offload-arch=gfx950 -O2 -std=c++17 -Iinclude -I$(MPI_HOME)/include -o $@ $< -L$(LIB) -ltempi_apps \
-	    -ltempi -L$(MPI_HOME)/lib -lmpi -static-libstdc++ -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,$(MPI_HOME)/lib
+	    -ltempi -ltempi_hip -L$(MPI_HOME)/lib -lmpi -static-libstdc++ -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,$(MPI_HOME)/lib
 
 $(LIB)/pingpong_nd: apps/pingpong_nd.cpp $(LIB)/libtempi_apps.so
 	$(HIPCC) --offload-arch=gfx950 -O2 -std=c++17 -Iinclude -I$(MPI_HOME)/include -o $@ $< -L$(LIB) -ltempi_apps \
-	    -ltempi -L$(MPI_HOME)/lib -lmpi -static-libstdc++ -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,$(MPI_HOME)/lib
+	    -ltempi -ltempi_hip -L$(MPI_HOME)/lib -lmpi -static-libstdc++ -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,$(MPI_HOME)/lib
 
 $(LIB)/pingpong_1d: apps/pingpong_1d.cpp $(LIB)/libtempi_apps.so
 	$(HIPCC) --offload-arch=gfx950 -O2 -std=c++17 -Iinclude -I$(MPI_HOME)/include -o $@ $< -L$(LIB) -ltempi_apps \
-	    -ltempi -L$(MPI_HOME)/lib -lmpi -static-libstdc++ -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,$(MPI_HOME)/lib
+	    -ltempi -ltempi_hip -L$(MPI_HOME)/lib -lmpi -static-libstdc++ -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,$(MPI_HOME)/lib
 
 $(LIB)/alltoallv_sparse: apps/alltoallv_sparse.cpp $(LIB)/libtempi_apps.so
 	$(HIPCC) --offload-arch=gfx950 -O2 -std=c++17 -Iinclude -I$(MPI_HOME)/include -o $@ $< -L$(LIB) -ltempi_apps \
-	    -ltempi -L$(MPI_HOME)/lib -lmpi -static-libstdc++ -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,$(MPI_HOME)/lib
+	    -ltempi -ltempi_hip -L$(MPI_HOME)/lib -lmpi -static-libstdc++ -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,$(MPI_HOME)/lib
 
 # packer level, no MPI: the C-ABI alone
 $(LIB)/pack_bench: apps/pack_bench.cpp $(LIB)/libtempi_hip.so
 	$(HIPCC) --offload-arch=gfx950 -O2 -std=c++17 -Iinclude -o $@ $< -L$(LIB) -ltempi_hip -Wl,-rpath,'$$ORIGIN'
 
 $(LIB)/%: apps/%.cpp $(LIB)/libtempi.so
-	$(HIPCC) --offload-arch=gfx950 -O2 -std=c++17 -Iinclude -I$(MPI_HOME)/include -o $@ $< -L$(LIB) -ltempi -L$(MPI_HOME)/lib -lmpi \
+	$(HIPCC) --offload-arch=gfx950 -O2 -std=c++17 -Iinclude -I$(MPI_HOME)/include -o $@ $< -L$(LIB) -ltempi -ltempi_hip -L$(MPI_HOME)/lib -lmpi \
 	    -static-libstdc++ -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,$(MPI_HOME)/lib
 
 oracle:

@@ -34,10 +34,22 @@
 //   (graph creation) and teardown (MPI_Comm_free) times, min over iterations
 //   of the max over ranks, and the pattern's bytes between and within nodes
 //   (:40-97) under the placement that was made.
+//
+// tempi_bench_sync_phases: where one synchronous MPI_Pack of BASELINE config 1
+//   (MPI_Type_vector(1024, 512, 1024, MPI_BYTE), 512 KiB, device buffers) spends
+//   its time on this box, all in C (no Python): the interposed call end to
+//   end, and its phases at libtempi_hip's C ABI -- pointer classification of
+//   both sides, the launch (host time of tempi_hip_pack_ticket), the wait for
+//   the ticket the kernel stores; the kernel alone between HIP events (200
+//   back-to-back launches); and MPICH's own MPI_Pack of the same type on host
+//   buffers (TEMPI hands host buffers to the library). Medians over `reps`.
 #include <hip/hip_runtime.h>
 #include <mpi.h>
 
+#include "tempi_hip.h"
+
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -536,4 +548,91 @@ EXPORT int tempi_bench_nbr_alltoallv(int iters, int scale, double density, int s
   buf_free(sbuf);
   buf_free(rbuf);
   return errors ? 3 : 0;
+}
+
+namespace {
+double now_us() {
+  return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+double median(std::vector<double> v) {
+  if (v.empty()) return 0;
+  std::sort(v.begin(), v.end());
+  return v[v.size() / 2];
+}
+} // namespace
+
+EXPORT int tempi_bench_sync_phases(int reps, char *json, int jsonCap) {
+  const int rows = 1024, block = 512, stride = 1024;
+  const int extent = (rows - 1) * stride + block, packed = rows * block;
+  MPI_Datatype t;
+  MPI_Type_vector(rows, block, stride, MPI_BYTE, &t);
+  MPI_Type_commit(&t);
+  char *src = nullptr, *dst = nullptr;
+  HIPCHECK(hipMalloc(&src, size_t(extent)));
+  HIPCHECK(hipMalloc(&dst, size_t(packed)));
+  HIPCHECK(hipMemset(src, 7, size_t(extent)));
+  HIPCHECK(hipDeviceSynchronize());
+  std::vector<char> hsrc(size_t(extent), 7);
+  std::vector<char> hdst(size_t(packed), 0);
+  hipStream_t s;
+  HIPCHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  tempi_hip_desc d{};
+  d.block = block;
+  d.ndims = 1;
+  d.counts[0] = rows;
+  d.strides[0] = stride;
+  std::vector<double> api, lib, ptr, launch, wait, total;
+  int errs = 0;
+  for (int r = 0; r < reps + 20; ++r) {
+    const bool keep = r >= 20;
+    int pos = 0;
+    double t0 = now_us();
+    errs += MPI_Pack(src, 1, t, dst, packed, &pos, MPI_COMM_WORLD) != MPI_SUCCESS || pos != packed;
+    double t1 = now_us();
+    pos = 0;
+    errs += MPI_Pack(hsrc.data(), 1, t, hdst.data(), packed, &pos, MPI_COMM_WORLD) != MPI_SUCCESS;
+    double t2 = now_us();
+    tempi_hip_ptrinfo info;
+    tempi_hip_pointer_info(src, &info);
+    tempi_hip_pointer_info(dst, &info);
+    double t3 = now_us();
+    const uint32_t *flag = nullptr;
+    uint32_t ticket = 0;
+    errs += tempi_hip_pack_ticket(dst, src, &d, s, &flag, &ticket) != 0;
+    double t4 = now_us();
+    errs += tempi_hip_ticket_wait(s, flag, ticket) != 0;
+    double t5 = now_us();
+    if (keep) {
+      api.push_back(t1 - t0);
+      lib.push_back(t2 - t1);
+      ptr.push_back(t3 - t2);
+      launch.push_back(t4 - t3);
+      wait.push_back(t5 - t4);
+      total.push_back(t5 - t3);
+    }
+  }
+  hipEvent_t e0, e1;
+  HIPCHECK(hipEventCreate(&e0));
+  HIPCHECK(hipEventCreate(&e1));
+  const int nk = 200;
+  HIPCHECK(hipEventRecord(e0, s));
+  for (int i = 0; i < nk; ++i) errs += tempi_hip_pack(dst, src, &d, s) != 0;
+  HIPCHECK(hipEventRecord(e1, s));
+  HIPCHECK(hipEventSynchronize(e1));
+  float ms = 0;
+  HIPCHECK(hipEventElapsedTime(&ms, e0, e1));
+  HIPCHECK(hipEventDestroy(e0));
+  HIPCHECK(hipEventDestroy(e1));
+  HIPCHECK(hipStreamDestroy(s));
+  HIPCHECK(hipFree(src));
+  HIPCHECK(hipFree(dst));
+  MPI_Type_free(&t);
+  std::snprintf(json, size_t(jsonCap),
+                "{\"workload\": \"config 1: MPI_Pack of vector(1024, 512, 1024), 512 KiB, medians of %d calls in C\", "
+                "\"mpi_pack_device_us\": %.2f, \"mpich_host_us\": %.2f, \"c_speedup\": %.3f, "
+                "\"phases_us\": {\"pointer_info_x2\": %.2f, \"launch\": %.2f, \"ticket_wait\": %.2f, "
+                "\"launch_plus_wait\": %.2f, \"kernel_back_to_back\": %.2f}, \"errors\": %d}",
+                reps, median(api), median(lib), median(api) > 0 ? median(lib) / median(api) : 0.0, median(ptr),
+                median(launch), median(wait), median(total), double(ms) * 1e3 / nk, errs);
+  return errs ? 1 : 0;
 }

@@ -214,6 +214,18 @@ def config1(mpi, torch, dev, iters=300):
                "cpu": "host MPICH 3.3.2 on host buffers, one pinned core of " + _cpu_model(),
                "gpu_us": round(gpu * 1e6, 2), "gpu_payload_GBps": round(512 * 1024 / gpu / 1e9, 2),
                "speedup": round(cpu / gpu, 2), "gpu_matches_cpu": ok}
+        # the same call in C, on this box, with its phases (apps/bench_lib.cpp
+        # tempi_bench_sync_phases): where a synchronous GPU MPI_Pack's time goes
+        try:
+            import ctypes
+
+            buf = ctypes.create_string_buffer(2048)
+            L = apps_lib()
+            L.tempi_bench_sync_phases.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
+            if L.tempi_bench_sync_phases(iters, buf, 2048) == 0 and buf.value:
+                out["c_phases"] = json.loads(buf.value.decode())
+        except Exception as e:  # (reported, never fatal to the line)
+            out["c_phases"] = {"error": str(e)[:200]}
     finally:
         mpi.Type_free(t)
     return out
@@ -1078,6 +1090,10 @@ def _compact_sections(rec, shared_gpu):
     if rec.get("config1"):
         c = rec["config1"]
         out["config1"] = _err(c) or {k: c.get(k) for k in ("cpu_us", "gpu_us", "speedup", "gpu_matches_cpu")}
+        cp = c.get("c_phases") or {}
+        if "phases_us" in cp and isinstance(out["config1"], dict):
+            out["config1"]["c"] = {"gpu_us": cp.get("mpi_pack_device_us"), "mpich_us": cp.get("mpich_host_us"),
+                                   "speedup": cp.get("c_speedup"), "phases_us": cp["phases_us"]}
     if rec.get("type_commit"):
         c = rec["type_commit"]
         out["type_commit"] = _err(c) or {"tempi_us": c["tempi"]["commit_us_median"],
