@@ -214,6 +214,20 @@ check("ibsend then detach", rbuf, 9, 8000 + src)
 mpi.Barrier()
 mpi.Buffer_attach(bsize)
 
+# MPI_Sendrecv_replace whose receive side is MPI_PROC_NULL: the send of the
+# (device) object still goes through TEMPI (it used to reach the
+# library, which cannot read GPU memory), and the object is left as it was
+sbuf, rbuf = buf(10), buf(11)
+refill(sbuf, 9000 + rank)
+r = mpi.Irecv(ptr(rbuf) + origin, count, t, src, 62)
+mpi.Barrier()
+mpi.Sendrecv_replace(ptr(sbuf) + origin, count, t, peer, 62, mpi.PROC_NULL, 62)
+mpi.Wait(r)
+check("sendrecv_replace to a peer from MPI_PROC_NULL", rbuf, 11, 9000 + src)
+if not np.array_equal(host(sbuf), rand(9000 + rank)):
+    fail("sendrecv_replace from MPI_PROC_NULL changed the object")
+mpi.Barrier()
+
 c = mpi.counters()
 starts, sends = c["persistent_starts"], c["sends"]
 if tempi_holds and starts < 4 * 4:
