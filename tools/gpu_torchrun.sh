@@ -14,10 +14,9 @@ for n in ${NS:-2 4}; do
 import json, sys
 d = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][-1])
 h = d["halo"]
+pts = lambda k, c: [p[d[k]["cols"].index(c)] for p in d[k]["points"]]
 print(d["value"], d["n_gpus"], h["us_per_iter"], h["rank0_phase_us"], d["halo_weak"]["us_per_iter"],
-      [p["one_way_us"] if "one_way_us" in p else p.get("us") for p in d["pingpong"]["points"]],
-      [p["oneway_us"] for p in d["pingpong_1d"]["points"]],
-      [p["min_us"] for p in d["alltoallv"]["points"]], [p["min_us"] for p in d["nbr_alltoallv"]["points"]],
-      d.get("incomplete"), d["perf_model"].get("auto_model"))
+      pts("pingpong", "oneway_us"), pts("pingpong_1d", "oneway_us"), pts("alltoallv", "min_us"),
+      pts("nbr_alltoallv", "min_us"), d.get("incomplete"), d["perf_model"].get("auto_model"))
 PY
 done

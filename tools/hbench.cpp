@@ -11,6 +11,9 @@
 // over QUANTS buffers, and prints one JSON line per class with the kernel time
 // and the algorithmic GB/s (2 x payload per launch set), plus the host time of
 // one tempi_hip_copy_batch call (planning + launch; copy_host_us).
+// Then (HBENCH_CONCURRENT=1) the x faces against the y + z faces: one after
+// the other on one stream, and side by side on two streams -- does the
+// x faces' isolated-line pattern overlap with the streaming faces?
 #include "tempi_hip.h"
 
 #include <chrono>
@@ -172,6 +175,51 @@ int main(int argc, char **argv) {
                 argv[1], c.name, cp.size(), payload, ms[0] * 1e3, ms[1] * 1e3, ms[2] * 1e3, gbs(ms[0]), gbs(ms[1]),
                 gbs(ms[2]), hostUs);
     std::fflush(stdout);
+  }
+  if (std::getenv("HBENCH_CONCURRENT")) {
+    std::vector<tempi_hip_copy_item> xs, yz;
+    for (int qi = 0; qi < nq; ++qi)
+      for (const Region &R : regions) {
+        const bool x = R.dx != 0 && !R.dy && !R.dz, y = !R.dx && R.dy != 0 && !R.dz, z = !R.dx && !R.dy && R.dz != 0;
+        if (!x && !y && !z) continue;
+        tempi_hip_copy_item cc{};
+        cc.dst = cc.src = R.desc;
+        cc.src_first = bufs[size_t(qi)] + R.srcOff;
+        cc.dst_first = bufs[size_t(qi)] + R.dstOff;
+        (x ? xs : yz).push_back(cc);
+      }
+    void *s2, *f0, *f1;
+    CK(tempi_hip_stream_create(&s2));
+    CK(tempi_hip_event_create(&f0, 0));
+    CK(tempi_hip_event_create(&f1, 0));
+    SYM(tempi_hip_stream_wait_event)
+    float ms[2];
+    for (int mode = 0; mode < 2; ++mode) {
+      auto run = [&]() -> int {
+        if (mode == 0) {
+          if (int e = tempi_hip_copy_batch(xs.data(), int(xs.size()), s)) return e;
+          return tempi_hip_copy_batch(yz.data(), int(yz.size()), s);
+        }
+        // fork s2 off s, run the two classes side by side, join back into s
+        if (int e = tempi_hip_event_record(f0, s)) return e;
+        if (int e = tempi_hip_stream_wait_event(s2, f0)) return e;
+        if (int e = tempi_hip_copy_batch(xs.data(), int(xs.size()), s)) return e;
+        if (int e = tempi_hip_copy_batch(yz.data(), int(yz.size()), s2)) return e;
+        if (int e = tempi_hip_event_record(f1, s2)) return e;
+        return tempi_hip_stream_wait_event(s, f1);
+      };
+      CK(run());
+      CK(run());
+      CK(tempi_hip_event_record(e0, s));
+      for (int i = 0; i < reps; ++i) CK(run());
+      CK(tempi_hip_event_record(e1, s));
+      CK(tempi_hip_event_synchronize(e1));
+      CK(tempi_hip_event_elapsed_ms(&ms[mode], e0, e1));
+      ms[mode] /= float(reps);
+    }
+    std::printf("{\"lib\": \"%s\", \"class\": \"x_vs_yz\", \"x_items\": %zu, \"yz_items\": %zu, "
+                "\"sequential_us\": %.1f, \"concurrent_us\": %.1f}\n",
+                argv[1], xs.size(), yz.size(), ms[0] * 1e3, ms[1] * 1e3);
   }
   return 0;
 }
