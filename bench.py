@@ -58,7 +58,7 @@ def parse():
                    help="skip the rocprofv3 FETCH_SIZE / WRITE_SIZE passes (child processes) for roofline.traffic")
     p.add_argument("--no-halo", action="store_true")
     p.add_argument("--halo-grid", type=int, default=512)
-    p.add_argument("--halo-iters", type=int, default=10)
+    p.add_argument("--halo-iters", type=int, default=30)  # (trimean of >= 30 iterations)
     p.add_argument("--pp-iters", type=int, default=50)
     p.add_argument("--a2av-iters", type=int, default=20)
     p.add_argument("--no-p2p", action="store_true", help="skip configs 3 and 5 at N > 1")
