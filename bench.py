@@ -602,6 +602,22 @@ def halo(args, mpi, world, grid=None):
                                     "copy (2 x payload bytes algorithmic); the HBM bytes actually moved "
                                     "(traffic_per_iter, when measured) are ~1.9x that, because each 24-byte "
                                     "x-face row costs a whole-line read and 32-byte sector writes")}
+        # the same bytes moved by bare kernels with no packer index math, on
+        # this box: an empirical floor for the GPU's share of an iteration
+        # (apps/bench_lib.cpp tempi_bench_halo_floor)
+        try:
+            L.tempi_bench_halo_floor.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_char_p,
+                                                 ctypes.c_int]
+            fb = ctypes.create_string_buffer(1024)
+            if L.tempi_bench_halo_floor(g, 8, 10, fb, 1024) == 0 and fb.value:
+                f = json.loads(fb.value.decode())
+                floor_us = 3 * f["substep_us"]
+                out["floor"] = {"us_per_iter": round(floor_us, 1), "frac": round(floor_us / r["us_per_iter"], 4),
+                                "x_faces_us_per_substep": f["x_faces_us"], "rest_us_per_substep": f["rest_us"],
+                                "what": ("3 substeps x (x faces, both faces of a row per lane + the other 24 "
+                                         "regions, one 8-byte word per lane), bare kernels timed here")}
+        except Exception as e:  # (evidence beside the metric, never fatal)
+            out["floor"] = {"error": str(e)[:200]}
     else:
         # xGMI: the busiest point-to-point link carries max_peer bytes per iteration
         lb = r["max_peer_bytes_per_iter"] / (XGMI_LINK_GBS * 1e9)
@@ -1081,6 +1097,9 @@ def _compact_sections(rec, shared_gpu):
                       "remote_bytes_per_iter": r.get("remote_bytes_per_iter")})
             x = h.get("xgmi_counters") or {}
             c["xgmi_counter_bytes_per_iter"] = x.get("per_unit_bytes") if x.get("available") else None
+        fl = h.get("floor") or {}
+        if "frac" in fl:
+            c["floor_us_per_iter"], c["frac_floor"] = fl["us_per_iter"], fl["frac"]
         if h.get("rank0_phase_us"):
             c["rank0_phase_us"] = h["rank0_phase_us"]
         cb = h.get("cpu_baseline")
