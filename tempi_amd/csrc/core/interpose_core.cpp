@@ -29,6 +29,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <unistd.h>
 #include <cstring>
 #include <vector>
 
@@ -120,6 +121,7 @@ void init_after_mpi() {
   if (env.noTempi) return;
   MPI_Comm_rank(MPI_COMM_WORLD, &state.worldRank);
   MPI_Comm_size(MPI_COMM_WORLD, &state.worldSize);
+  state.pid = int32_t(getpid());
   logRank = state.worldRank;
   trace::init();
   hostTiming = std::getenv("TEMPI_PRINT_COUNTERS") != nullptr;

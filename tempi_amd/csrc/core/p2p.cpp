@@ -196,7 +196,7 @@ int isend(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Co
     d.magic[1] = kMagic1;
     d.bytes = bytes;
     d.senderWorld = state.worldRank;
-    d.senderPid = int32_t(getpid());
+    d.senderPid = state.pid;
     d.device = p.device;
     d.rawFirst = reinterpret_cast<uint64_t>(origin + rec->desc.start);
     d.desc = flat;

@@ -326,7 +326,7 @@ struct IsendOp : Op {
       desc.offset = 0;
       desc.bytes = bytes;
       desc.senderWorld = state.worldRank;
-      desc.senderPid = int32_t(getpid());
+      desc.senderPid = state.pid;
       desc.rawPtr = reinterpret_cast<uint64_t>(dslab->dev);
       desc.gpu = gpu::identity(device);
       std::memcpy(desc.handle, slab_ipc_handle(dslab), sizeof desc.handle);
@@ -398,7 +398,7 @@ struct IsendDirectOp : Op {
     desc.token = token;
     desc.bytes = b;
     desc.senderWorld = state.worldRank;
-    desc.senderPid = int32_t(getpid());
+    desc.senderPid = state.pid;
     desc.device = dev;
     desc.first = reinterpret_cast<uint64_t>(o + rec->desc.start);
     desc.desc = flat;

@@ -211,7 +211,7 @@ struct IrecvOp : Op {
         return truncate(xd.bytes);
       }
       elems = size ? xd.bytes / size : 0;
-      const bool local = xd.senderPid == int32_t(getpid());
+      const bool local = xd.senderPid == state.pid;
       if (!local) recycle_alloc_maps();
       const char *src = (local && xd.device != device) ? nullptr : peer_object(xd);
       if (src && !local && xd.gpu != gpu::identity(device) &&
@@ -253,7 +253,7 @@ struct IrecvOp : Op {
         return truncate(d.bytes);
       }
       void *base = peer_pointer(d);
-      if (base && d.senderPid != int32_t(getpid()) && d.gpu != gpu::identity(device) &&
+      if (base && d.senderPid != state.pid && d.gpu != gpu::identity(device) &&
           !canary(d.senderWorld, static_cast<const char *>(base) + d.offset, d.bytes, device))
         base = nullptr;
       if (!base) { // cannot map (or trust) the sender's slab: ask for the bytes via the host

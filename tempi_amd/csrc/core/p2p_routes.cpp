@@ -192,7 +192,7 @@ int open_ipc_handle(void **p, const void *handle) {
 
 // the sender's slab mapped into this process, or nullptr when it cannot be
 void *peer_pointer(const IpcDesc &d) {
-  if (d.senderPid == int32_t(getpid())) return reinterpret_cast<void *>(d.rawPtr);
+  if (d.senderPid == state.pid) return reinterpret_cast<void *>(d.rawPtr);
   auto key = std::make_pair(int(d.senderWorld), d.slabId);
   auto it = ipcOpen.find(key);
   if (it != ipcOpen.end()) return it->second;
@@ -307,7 +307,7 @@ void forget_freed_allocs(const IpcCopyDesc &d) {
 // the sender's allocation mapped into this process (its first byte), or
 // nullptr when it cannot be
 const char *peer_object(const IpcCopyDesc &d) {
-  if (d.senderPid == int32_t(getpid())) return reinterpret_cast<const char *>(d.rawFirst);
+  if (d.senderPid == state.pid) return reinterpret_cast<const char *>(d.rawFirst);
   auto key = std::make_pair(int(d.senderWorld), d.bufferId);
   auto it = ipcAllocOpen.find(key);
   if (it == ipcAllocOpen.end()) {
@@ -390,7 +390,7 @@ void direct_finish(std::shared_ptr<DirectShared> &sh) {
 // the matched descriptor's shared state (unmatched until now)
 std::shared_ptr<DirectShared> claim_direct(const DirectDesc &d) {
   auto it = directShared.find(d.token);
-  if (d.senderPid != int32_t(getpid()) || it == directShared.end())
+  if (d.senderPid != state.pid || it == directShared.end())
     LOG_FATAL("direct-send descriptor from another process (rank " << d.senderWorld << ")");
   std::shared_ptr<DirectShared> sh = it->second;
   directShared.erase(it);

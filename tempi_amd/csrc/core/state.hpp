@@ -4,12 +4,15 @@
 
 #include <mpi.h>
 
+#include <cstdint>
+
 namespace tempi {
 
 struct State {
   bool active = false; // MPI initialised through TEMPI and TEMPI not disabled
   int worldRank = 0;
   int worldSize = 1;
+  int32_t pid = 0; // getpid() at MPI_Init (glibc no longer caches it: a syscall per call)
 };
 
 extern State state;
