@@ -637,27 +637,19 @@ EXPORT int tempi_bench_sync_phases(int reps, char *json, int jsonCap) {
   return errs ? 1 : 0;
 }
 
-// tempi_bench_halo_floor: an empirical floor for the 1-rank halo's GPU work,
-// the same bytes moved by bare kernels with no packer index math, timed on
-// this box (tools/xface.hip is the standalone form). One substep of the
+// tempi_bench_halo_floor: the 1-rank halo's x faces as a bare access pattern,
+// timed on this box -- the same bytes as the packer's paired copy, one lane
+// per row (both faces of a row in one lane: each row's two 128-B lines read
+// once and written back once; tools/xface.hip is the standalone form, DESIGN
+// §6) -- and the payload of the other 24 regions (y / z faces, edges,
+// corners), which bench.py prices as streaming bytes. One substep of the
 // `grid`^3 exchange (radius 3, 8-byte cells, pitch rounded to 512 B, as
-// halo_lib.cpp lays it out) for `quants` quantities:
-//   x faces  both faces of a row in one lane (each row's two 128-B lines are
-//            read once and written back once: the pattern the packer's paired
-//            copy uses, and the fastest one measured)
-//   the rest the other 24 regions (y / z faces, edges, corners), one 8-byte
-//            word per lane, consecutive lanes on consecutive words
-// Reported per substep, medians of `reps` timed launches of each.
+// halo_lib.cpp lays it out) for `quants` quantities; median of `reps` timed
+// launches.
 namespace {
 struct FloorGeom {
   int l, r;
   int64_t pitch, plane;
-};
-struct FloorRegion {
-  int64_t src, dst;
-  uint32_t rows, wpr, ey;   // rows = ey * ez, words per row
-  int64_t rowStrideY, rowStrideZ;
-  uint64_t firstWord;       // prefix sum over regions (all quantities)
 };
 constexpr int kFloorMaxQ = 16;
 struct FloorBufs {
@@ -679,22 +671,6 @@ __global__ __launch_bounds__(256) void floor_xface(FloorBufs bufs, FloorGeom g) 
   for (int k = 0; k < 3; ++k) d1[k] = a[k], d2[k] = b[k];
 }
 
-__global__ __launch_bounds__(256) void floor_rest(FloorBufs bufs, const FloorRegion *regs, int nregs,
-                                                  uint64_t wordsPerQ) {
-  const uint64_t w = uint64_t(blockIdx.x) * 256u + threadIdx.x;
-  if (w >= wordsPerQ) return;
-  int lo = 0, hi = nregs; // region holding word w
-  while (hi - lo > 1) {
-    const int mid = (lo + hi) / 2;
-    if (w >= regs[mid].firstWord) lo = mid; else hi = mid;
-  }
-  const FloorRegion &R = regs[lo];
-  const uint64_t k = w - R.firstWord;
-  const uint32_t row = uint32_t(k / R.wpr), x = uint32_t(k % R.wpr);
-  const int64_t off = int64_t(row % R.ey) * R.rowStrideY + int64_t(row / R.ey) * R.rowStrideZ + int64_t(x) * 8;
-  char *b = bufs.b[blockIdx.y];
-  *reinterpret_cast<uint64_t *>(b + R.dst + off) = *reinterpret_cast<const uint64_t *>(b + R.src + off);
-}
 } // namespace
 
 EXPORT int tempi_bench_halo_floor(int grid, int quants, int reps, char *json, int jsonCap) {
@@ -703,73 +679,46 @@ EXPORT int tempi_bench_halo_floor(int grid, int quants, int reps, char *json, in
   const int64_t width = int64_t(l + 2 * r) * q, pitch = (width + 511) / 512 * 512;
   const int64_t ysize = l + 2 * r, plane = pitch * ysize, bufBytes = plane * (l + 2 * r);
   FloorGeom g{l, r, pitch, plane};
-  std::vector<FloorRegion> regs;
-  uint64_t words = 0, restBytes = 0;
+  // payload of the 24 regions that are not x faces (per quantity)
+  uint64_t restBytes = 0;
   for (int dz = -1; dz <= 1; ++dz)
     for (int dy = -1; dy <= 1; ++dy)
       for (int dx = -1; dx <= 1; ++dx) {
-        if ((!dx && !dy && !dz) || (dx && !dy && !dz)) continue; // (the x faces: floor_xface)
+        if ((!dx && !dy && !dz) || (dx && !dy && !dz)) continue;
         const int d[3] = {dx, dy, dz};
-        int64_t pin[3], pex[3], e[3];
-        for (int k = 0; k < 3; ++k) {
-          pin[k] = d[k] == -1 ? r : d[k] == 1 ? l : r;
-          pex[k] = -d[k] == -1 ? 0 : -d[k] == 1 ? l + r : r;
-          e[k] = d[k] == 0 ? l : r;
-        }
-        FloorRegion R{};
-        R.src = pin[2] * plane + pin[1] * pitch + pin[0] * q;
-        R.dst = pex[2] * plane + pex[1] * pitch + pex[0] * q;
-        R.wpr = uint32_t(e[0]);
-        R.ey = uint32_t(e[1]);
-        R.rows = uint32_t(e[1] * e[2]);
-        R.rowStrideY = pitch;
-        R.rowStrideZ = plane;
-        R.firstWord = words;
-        words += uint64_t(R.rows) * R.wpr;
-        restBytes += uint64_t(R.rows) * R.wpr * 8;
-        regs.push_back(R);
+        uint64_t cells = 1;
+        for (int k = 0; k < 3; ++k) cells *= uint64_t(d[k] == 0 ? l : r);
+        restBytes += cells * q;
       }
   FloorBufs bufs{};
   for (int qi = 0; qi < quants; ++qi) {
     HIPCHECK(hipMalloc(&bufs.b[qi], size_t(bufBytes)));
     HIPCHECK(hipMemset(bufs.b[qi], qi + 1, size_t(bufBytes)));
   }
-  FloorRegion *dregs = nullptr;
-  HIPCHECK(hipMalloc(&dregs, regs.size() * sizeof(FloorRegion)));
-  HIPCHECK(hipMemcpy(dregs, regs.data(), regs.size() * sizeof(FloorRegion), hipMemcpyHostToDevice));
   hipStream_t s;
   HIPCHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   hipEvent_t e0, e1;
   HIPCHECK(hipEventCreate(&e0));
   HIPCHECK(hipEventCreate(&e1));
   const uint32_t xrows = uint32_t(l) * uint32_t(l);
-  auto time = [&](int which) {
-    std::vector<double> v;
-    for (int i = 0; i < reps + 2; ++i) {
-      HIPCHECK(hipEventRecord(e0, s));
-      if (which == 0)
-        hipLaunchKernelGGL(floor_xface, dim3((xrows + 255) / 256, quants), dim3(256), 0, s, bufs, g);
-      else
-        hipLaunchKernelGGL(floor_rest, dim3(uint32_t((words + 255) / 256), quants), dim3(256), 0, s, bufs,
-                           dregs, int(regs.size()), words);
-      HIPCHECK(hipEventRecord(e1, s));
-      HIPCHECK(hipEventSynchronize(e1));
-      float ms = 0;
-      HIPCHECK(hipEventElapsedTime(&ms, e0, e1));
-      if (i >= 2) v.push_back(double(ms) * 1e3);
-    }
-    return median(v);
-  };
-  const double xUs = time(0), restUs = time(1);
+  std::vector<double> v;
+  for (int i = 0; i < reps + 2; ++i) {
+    HIPCHECK(hipEventRecord(e0, s));
+    hipLaunchKernelGGL(floor_xface, dim3((xrows + 255) / 256, quants), dim3(256), 0, s, bufs, g);
+    HIPCHECK(hipEventRecord(e1, s));
+    HIPCHECK(hipEventSynchronize(e1));
+    float ms = 0;
+    HIPCHECK(hipEventElapsedTime(&ms, e0, e1));
+    if (i >= 2) v.push_back(double(ms) * 1e3);
+  }
+  const double xUs = median(v);
   HIPCHECK(hipEventDestroy(e0));
   HIPCHECK(hipEventDestroy(e1));
   HIPCHECK(hipStreamDestroy(s));
-  HIPCHECK(hipFree(dregs));
   for (int qi = 0; qi < quants; ++qi) HIPCHECK(hipFree(bufs.b[qi]));
   const double xBytes = 2.0 * xrows * 3 * 8 * quants; // payload of both x faces
   std::snprintf(json, size_t(jsonCap),
-                "{\"x_faces_us\": %.1f, \"rest_us\": %.1f, \"substep_us\": %.1f, \"x_payload_bytes\": %.0f, "
-                "\"rest_payload_bytes\": %.0f, \"reps\": %d}",
-                xUs, restUs, xUs + restUs, xBytes, double(restBytes) * quants, reps);
+                "{\"x_faces_us\": %.1f, \"x_payload_bytes\": %.0f, \"rest_payload_bytes\": %.0f, \"reps\": %d}",
+                xUs, xBytes, double(restBytes) * quants, reps);
   return 0;
 }

@@ -602,20 +602,25 @@ def halo(args, mpi, world, grid=None):
                                     "copy (2 x payload bytes algorithmic); the HBM bytes actually moved "
                                     "(traffic_per_iter, when measured) are ~1.9x that, because each 24-byte "
                                     "x-face row costs a whole-line read and 32-byte sector writes")}
-        # the same bytes moved by bare kernels with no packer index math, on
-        # this box: an empirical floor for the GPU's share of an iteration
-        # (apps/bench_lib.cpp tempi_bench_halo_floor; DESIGN §6)
+        # an empirical floor for the GPU's share of an iteration, per substep:
+        # the x faces as their bare access pattern timed on this box (the
+        # packer's paired copy runs at or below it) + the other 24
+        # regions' read + write at the achievable streaming rate
+        # (apps/bench_lib.cpp tempi_bench_halo_floor)
         try:
             L.tempi_bench_halo_floor.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_char_p,
                                                  ctypes.c_int]
             fb = ctypes.create_string_buffer(1024)
             if L.tempi_bench_halo_floor(g, 8, 10, fb, 1024) == 0 and fb.value:
                 f = json.loads(fb.value.decode())
-                floor_us = 3 * f["substep_us"]
+                rest_us = 2.0 * f["rest_payload_bytes"] / (HBM_ACHIEVABLE_GBS * 1e9) * 1e6
+                floor_us = 3 * (f["x_faces_us"] + rest_us)
                 out["floor"] = {"us_per_iter": round(floor_us, 1), "frac": round(floor_us / r["us_per_iter"], 4),
-                                "x_faces_us_per_substep": f["x_faces_us"], "rest_us_per_substep": f["rest_us"],
-                                "what": ("3 substeps x (x faces, both faces of a row per lane + the other 24 "
-                                         "regions, one 8-byte word per lane), bare kernels timed here")}
+                                "x_faces_bare_us_per_substep": f["x_faces_us"],
+                                "rest_streaming_us_per_substep": round(rest_us, 1),
+                                "what": ("3 substeps x (x faces moved by a bare kernel, both faces of a row per "
+                                         "lane, timed here + the other 24 regions' 2 x payload at "
+                                         f"{HBM_ACHIEVABLE_GBS:.0f} GB/s)")}
         except Exception as e:  # (evidence beside the metric, never fatal)
             out["floor"] = {"error": str(e)[:200]}
     else:
