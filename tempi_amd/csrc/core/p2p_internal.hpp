@@ -293,6 +293,11 @@ struct Op {
   virtual void acked(int) {}                   // that ack arrived with this code
 };
 
+// a library post of the application's message that the library refused
+// (its arguments, under MPI_ERRORS_RETURN): the op completes with that error
+// -- raised by its wait -- instead of waiting on a request that does not exist
+void fail_post(Op *op, int rc, MPI_Comm comm);
+
 void *get_event();
 void put_event(void *e);
 void destroy_events();

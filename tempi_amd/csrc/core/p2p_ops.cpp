@@ -42,6 +42,13 @@ std::pmr::unsynchronized_pool_resource &op_pool() {
 // (the reference's try_progress wakes every operation: async_operation.cpp:
 // 501-513).
 
+void fail_post(Op *op, int rc, MPI_Comm comm) {
+  op->lib = MPI_REQUEST_NULL;
+  op->err = rc;
+  op->errComm = comm;
+  op->done = true;
+}
+
 std::vector<void *> eventPool;
 
 void *get_event() {
@@ -419,7 +426,11 @@ struct IsendDirectOp : Op {
     // receive is posted (MPICH does), so the send's completion cannot wait for
     // it: the request is released now and the descriptor outlives it in `sh`
     MPI_Request sreq;
-    next.MPI_Isend(&sh->desc, int(sizeof sh->desc), MPI_PACKED, dest, tag, comm, &sreq);
+    const int rc = next.MPI_Isend(&sh->desc, int(sizeof sh->desc), MPI_PACKED, dest, tag, comm, &sreq);
+    if (rc != MPI_SUCCESS) {
+      directShared.erase(sh->desc.token);
+      return fail_post(this, rc, comm);
+    }
     next.MPI_Request_free(&sreq);
     maybe_done();
   }
@@ -502,16 +513,22 @@ struct IsendCopyOp : Op {
     if (slot >= 0) {
       desc.ackTag = slot;
       boardSlot = slot;
+      const int rc = next.MPI_Isend(&desc, int(sizeof desc), MPI_PACKED, dest, tag, comm, &lib);
+      if (rc != MPI_SUCCESS) {
+        board_give(slot);
+        boardSlot = -1;
+        return fail_post(this, rc, comm);
+      }
       boardAck = true;
       boardOps.push_back(this);
-      next.MPI_Isend(&desc, int(sizeof desc), MPI_PACKED, dest, tag, comm, &lib);
       watch(this);
       return;
     }
-    next.MPI_Irecv(&ack, 1, MPI_INT, peer, desc.ackTag, ctrlComm, &lib);
-    watch(this);
     MPI_Request r; // the descriptor lives in this op until the ack, which follows its delivery
-    next.MPI_Isend(&desc, int(sizeof desc), MPI_PACKED, dest, tag, comm, &r);
+    const int rc = next.MPI_Isend(&desc, int(sizeof desc), MPI_PACKED, dest, tag, comm, &r);
+    if (rc != MPI_SUCCESS) return fail_post(this, rc, comm);
+    next.MPI_Irecv(&ack, 1, MPI_INT, peer, desc.ackTag, ctrlComm, &lib); // (the ack follows the delivery)
+    watch(this);
     next.MPI_Request_free(&r);
   }
   void lib_done(const MPI_Status &) override {
@@ -610,7 +627,8 @@ struct HostIsendOp : Op {
   }
   ~HostIsendOp() override { drop_type(dt); }
   void post() override {
-    next.MPI_Isend(buf, count, dt, dest, tag, comm, &lib);
+    const int rc = next.MPI_Isend(buf, count, dt, dest, tag, comm, &lib);
+    if (rc != MPI_SUCCESS) return fail_post(this, rc, comm);
     watch(this);
   }
   void lib_done(const MPI_Status &) override { done = true; }

@@ -69,10 +69,14 @@ struct IrecvOp : Op {
       lib_done(pre->st);
       return;
     }
-    if (msg)
-      next.MPI_Imrecv(hslab->host, int(cap), MPI_PACKED, msg, &lib);
-    else
-      next.MPI_Irecv(hslab->host, int(cap), MPI_PACKED, source, tag, comm, &lib);
+    const int rc = msg ? next.MPI_Imrecv(hslab->host, int(cap), MPI_PACKED, msg, &lib)
+                       : next.MPI_Irecv(hslab->host, int(cap), MPI_PACKED, source, tag, comm, &lib);
+    if (rc != MPI_SUCCESS) {
+      pinned_pool().put(hslab);
+      hslab = nullptr;
+      fail_post(this, rc, comm);
+      return;
+    }
     // a message from this same process is matched as the receive is posted:
     // take it now, so its copy can start while the caller posts more
     if (!msg && source >= 0 && topology::world_rank(comm, source) == state.worldRank) {
@@ -394,10 +398,12 @@ struct LibIrecvOp : Op {
       lib_done(pre->st);
       return;
     }
-    if (msg)
-      next.MPI_Imrecv(buf.data(), int(buf.size()), MPI_PACKED, msg, &lib);
-    else
-      next.MPI_Irecv(buf.data(), int(buf.size()), MPI_PACKED, source, tag, comm, &lib);
+    const int rc = msg ? next.MPI_Imrecv(buf.data(), int(buf.size()), MPI_PACKED, msg, &lib)
+                       : next.MPI_Irecv(buf.data(), int(buf.size()), MPI_PACKED, source, tag, comm, &lib);
+    if (rc != MPI_SUCCESS) {
+      fail_post(this, rc, comm);
+      return;
+    }
     watch(this);
   }
   bool cancelled = false;
@@ -527,7 +533,11 @@ struct HostIrecvOp : Op {
     inPlace = !pre && tlb == 0 && text == size && (c == 1 || ext == size) && cap >= int64_t(kDescCap);
     if (inPlace) {
       std::memcpy(saved, b, kDescCap);
-      next.MPI_Irecv(b, c, d, source, tag, cm, &lib);
+      const int rc = next.MPI_Irecv(b, c, d, source, tag, cm, &lib);
+      if (rc != MPI_SUCCESS) {
+        fail_post(this, rc, cm);
+        return;
+      }
       watch(this);
       return;
     }
@@ -539,7 +549,11 @@ struct HostIrecvOp : Op {
     }
     const size_t n = std::max({size_t(std::max<int64_t>(cap, 1)), size_t(pack_size(c, d, cm)), kDescCap});
     stage = stage_pool().get(n);
-    next.MPI_Irecv(stage.p, int(n), MPI_PACKED, source, tag, cm, &lib);
+    const int rc = next.MPI_Irecv(stage.p, int(n), MPI_PACKED, source, tag, cm, &lib);
+    if (rc != MPI_SUCCESS) {
+      fail_post(this, rc, cm);
+      return;
+    }
     watch(this);
   }
   ~HostIrecvOp() override {

@@ -214,6 +214,17 @@ check("ibsend then detach", rbuf, 9, 8000 + src)
 mpi.Barrier()
 mpi.Buffer_attach(bsize)
 
+# a receive the library refuses (a source rank outside the communicator,
+# ERRORS_RETURN): an error at the call or at its wait, not a hang
+rbuf = buf(12)
+try:
+    r = mpi.Irecv(ptr(rbuf) + origin, count, t, size + 3, 63)
+    mpi.Wait(r)
+    fail("a receive from a rank outside the communicator succeeded")
+except tempi_amd.mpi.MPIError:
+    pass
+mpi.Barrier()
+
 # MPI_Sendrecv_replace whose receive side is MPI_PROC_NULL: the send of the
 # (device) object still goes through TEMPI (it used to reach the
 # library, which cannot read GPU memory), and the object is left as it was
