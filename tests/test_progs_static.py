@@ -2,7 +2,8 @@
 programs under tests/mpi_progs/ mostly need a GPU, so the CPU suite cannot run
 all of them; this is a pyflakes-style check (pyflakes is not in the image)
 that every name a script reads is bound somewhere it can be seen -- at module
-level, before the statement that reads it. Round 3's fuzz.py read `modes` two
+level, before the statement that reads it. The other Python files of the
+repository (tools/, tempi_amd/, oracle/, tests/) are held to the same check. Round 3's fuzz.py read `modes` two
 lines before assigning it, and that one NameError hid ~290 GPU tests behind
 pytest -x."""
 import ast
@@ -14,7 +15,9 @@ import pytest
 ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
 PROGS = sorted(os.path.join(ROOT, "tests", "mpi_progs", f)
                for f in os.listdir(os.path.join(ROOT, "tests", "mpi_progs")) if f.endswith(".py"))
-SCRIPTS = PROGS + [os.path.join(ROOT, f) for f in ("bench.py", "__graft_entry__.py")]
+SCRIPTS = PROGS + [os.path.join(ROOT, f) for f in ("bench.py", "__graft_entry__.py")] + sorted(
+    os.path.join(ROOT, d, f) for d in ("tools", "tempi_amd", "oracle", "tests")
+    for f in os.listdir(os.path.join(ROOT, d)) if f.endswith(".py"))
 BUILTINS = set(dir(builtins)) | {"__file__", "__name__", "__doc__", "__spec__", "__builtins__"}
 
 
