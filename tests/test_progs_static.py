@@ -3,9 +3,9 @@ programs under tests/mpi_progs/ mostly need a GPU, so the CPU suite cannot run
 all of them; this is a pyflakes-style check (pyflakes is not in the image)
 that every name a script reads is bound somewhere it can be seen -- at module
 level, before the statement that reads it. The other Python files of the
-repository (tools/, tempi_amd/, oracle/, tests/) are held to the same check. Round 3's fuzz.py read `modes` two
-lines before assigning it, and that one NameError hid ~290 GPU tests behind
-pytest -x."""
+repository (tools/, tempi_amd/, oracle/, tests/) are held to the same check.
+Round 3's fuzz.py read `modes` two lines before assigning it, and that one
+NameError hid ~290 GPU tests behind pytest -x."""
 import ast
 import builtins
 import os
