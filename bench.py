@@ -957,7 +957,7 @@ def sweep(args, mpi, torch, dev, path, sizes=(1 << 20, 16 << 20, 256 << 20, 1 <<
                     src = torch.empty(extent, dtype=torch.uint8, device=dev)
                     pk = torch.empty(payload, dtype=torch.uint8, device=dev)
                     torch.cuda.synchronize()
-                    reps = max(3, min(50, int(2e9 / max(payload, 1))))
+                    reps = max(30, min(50, int(2e9 / max(payload, 1))))  # (>= 30 iterations)
                     mpi.Pack(src.data_ptr(), 1, t, pk.data_ptr(), payload, 0)
                     mpi.Unpack(pk.data_ptr(), payload, 0, src.data_ptr(), 1, t)
                     mpi.reset_counters()
