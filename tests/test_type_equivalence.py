@@ -120,3 +120,35 @@ def test_by_rows_by_cols_library_view(mpi):
     finally:
         typezoo.free(mpi, *rows)
         typezoo.free(mpi, *cols)
+
+
+# /root/reference/test/type_commit.cpp:13-90: the factories committed at the
+# reference's sizes (100 x 13 x 47 out of 256 x 512 x 1024; by rows / by
+# cols 13, 5, 16, 3, 53); here each must also canonicalise to a valid strided
+# descriptor covering exactly the type's bytes
+COMMIT_CASES = {
+    "hv_by_rows": "hvector(3,1,53,vector(5,13,16,byte))",
+    "hv_by_cols": "hvector(5,1,16,vector(3,13,53,byte))",
+    "subarray": "subarray(C,[1024,512,256],[47,13,100],[0,0,0],byte)",
+    "off_subarray": "subarray(C,[1024,512,256],[47,13,100],[4,4,4],byte)",
+    "subarray_v": "vector(47,1,1,subarray(C,[512,256],[13,100],[0,0],byte))",
+    "byte_v_hv": _box_recipes(100, 13, 47, 256, 512, 1024)["byte_v_hv"],
+    "float_v_hv": "hvector(47,1,131072,vector(13,25,64,float))",
+    "byte_v1_hv_hv": _box_recipes(100, 13, 47, 256, 512, 1024)["byte_v1_hv_hv"],
+    "byte_vn_hv_hv": _box_recipes(100, 13, 47, 256, 512, 1024)["byte_vn_hv_hv"],
+    "v1_hv_hv_plane": _box_recipes(100, 100, 1, 100, 100, 100)["byte_v1_hv_hv"],
+}
+
+
+@pytest.mark.parametrize("name", sorted(COMMIT_CASES))
+def test_reference_factories_commit_to_strided_blocks(mpi, name):
+    b = typezoo.build(mpi, COMMIT_CASES[name])
+    try:
+        d = mpi.describe(b[0])
+        assert d is not None and d["valid"], d
+        n = d["block"]
+        for c in d["counts"]:
+            n *= c
+        assert d["size"] == n == mpi.Type_size(b[0])
+    finally:
+        typezoo.free(mpi, *b)
