@@ -4,7 +4,10 @@
 host numpy buffers (TEMPI forwards to the library). Checks every received
 byte against what the sender packed (oracle/typemap.c), for MPI_Send/Recv,
 MPI_Isend/Irecv + MPI_Wait / MPI_Waitall / MPI_Test, several datatypes, and a
-mix of TEMPI and library requests in one MPI_Waitall.
+mix of TEMPI and library requests in one MPI_Waitall. The reference's own
+point-to-point tests only check that such calls complete
+(/root/reference/test/send.cpp, send_vector.cpp:13-60, isend.cu,
+isend_contiguous.cu, sender.cpp); here every byte is compared.
 """
 import os
 import sys
