@@ -74,6 +74,8 @@ def parse():
     p.add_argument("--extras-deadline", type=float, default=400.0,
                    help="seconds after the headline within which the line's other sections must finish; past it "
                         "rank 0 prints the line so far, marked incomplete, and every rank exits")
+    p.add_argument("--detail-name", default=None,
+                   help="file name under gpurun_out/ for the full record (default bench_detail_nN.json)")
     p.add_argument("--inner", action="store_true", help=argparse.SUPPRESS)  # child for --traffic
     return p.parse_args()
 
@@ -1203,11 +1205,14 @@ def compact_line(rec, shared_gpu=False, detail=None, limit=LINE_LIMIT):
     return line
 
 
+DETAIL_NAME = None  # --detail-name
+
+
 def write_detail(rec, world):
     """the full record, next to the line (gpurun_out/ is merged back from
     the GPU box); returns the path relative to the repo, or None"""
     d = os.path.join(ROOT, "gpurun_out")
-    path = os.path.join(d, f"bench_detail_n{world}.json")
+    path = os.path.join(d, os.path.basename(DETAIL_NAME or f"bench_detail_n{world}.json"))
     try:
         os.makedirs(d, exist_ok=True)
         with open(path, "w") as f:
@@ -1265,7 +1270,9 @@ class Sections:
 
 
 def main():
+    global DETAIL_NAME
     args = parse()
+    DETAIL_NAME = args.detail_name
     rank, world, local, pg, keep = dist_setup(args)
     import torch
 
