@@ -15,6 +15,12 @@
 //                NOT allowed for the packer -- they are the application's --
 //                so this is what the partly written sectors cost)
 //   reads        the paired loads only
+//   *_nt / *_sc1 / *_sys  the same with nontemporal loads, agent-scope
+//                (global_load sc1: L1 bypassed) or system-scope (sc0 sc1)
+//                loads: does a load's cache policy change how much of each
+//                isolated row's 128-B line is fetched from memory?
+//   reads8       one 8-B load per face row (how much of the time is lines,
+//                how much bytes)
 // usage: xface [REPS] -> one JSON line per variant (µs per exchange of the 8
 // quantities' x faces, algorithmic GB/s = 2 x payload / time)
 #include <hip/hip_runtime.h>
@@ -47,7 +53,15 @@ __device__ __forceinline__ int64_t row_off(uint32_t r) {
   return (int64_t(r / kL) + kR) * kPlane + (int64_t(r % kL) + kR) * kPitch;
 }
 
-template <int MODE> // 0 paired, 2 full_sector, 3 reads
+// load policy: 0 plain, 1 nontemporal, 2 agent scope (sc1), 3 system scope (sc0 sc1)
+template <int POL> __device__ __forceinline__ uint64_t ldp(const uint64_t *p) {
+  if constexpr (POL == 1) return __builtin_nontemporal_load(p);
+  if constexpr (POL == 2) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if constexpr (POL == 3) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  return *p;
+}
+
+template <int MODE, int POL = 0> // MODE 0 paired, 2 full_sector, 3 reads, 4 reads8
 __global__ __launch_bounds__(256) void xface_paired(Bufs bufs, uint64_t *sink) {
   const uint32_t q = blockIdx.y;
   const uint32_t r = blockIdx.x * 256u + threadIdx.x;
@@ -55,8 +69,12 @@ __global__ __launch_bounds__(256) void xface_paired(Bufs bufs, uint64_t *sink) {
   char *row = bufs.b[q] + row_off(r);
   const uint64_t *s1 = reinterpret_cast<const uint64_t *>(row + 4096); // +x face
   const uint64_t *s2 = reinterpret_cast<const uint64_t *>(row + 24);   // -x face
-  uint64_t a0 = s1[0], a1 = s1[1], a2 = s1[2];
-  uint64_t b0 = s2[0], b1 = s2[1], b2 = s2[2];
+  if constexpr (MODE == 4) {
+    sink[blockIdx.y * gridDim.x * 256u + r] = ldp<POL>(s1) ^ ldp<POL>(s2);
+    return;
+  }
+  uint64_t a0 = ldp<POL>(s1), a1 = ldp<POL>(s1 + 1), a2 = ldp<POL>(s1 + 2);
+  uint64_t b0 = ldp<POL>(s2), b1 = ldp<POL>(s2 + 1), b2 = ldp<POL>(s2 + 2);
   if constexpr (MODE == 3) {
     sink[blockIdx.y * gridDim.x * 256u + r] = a0 ^ a1 ^ a2 ^ b0 ^ b1 ^ b2;
     return;
@@ -101,8 +119,10 @@ int main(int argc, char **argv) {
   CK(hipEventCreate(&e1));
   const dim3 grid((kRows + 255) / 256, kQ);
   const double payload = 2.0 * kQ * kRows * 24; // both faces of every quantity
-  const char *names[] = {"paired", "single", "full_sector", "reads"};
-  for (int v = 0; v < 4; ++v) {
+  const char *names[] = {"paired",    "single",   "full_sector", "reads",     "paired_nt", "reads_nt",
+                         "paired_sc1", "reads_sc1", "paired_sys",  "reads_sys", "reads8",    "reads8_nt"};
+  constexpr int kVariants = 12;
+  for (int v = 0; v < kVariants; ++v) {
     auto run = [&] {
       switch (v) {
       case 0: hipLaunchKernelGGL(xface_paired<0>, grid, dim3(256), 0, s, bufs, sink); break;
@@ -111,7 +131,15 @@ int main(int argc, char **argv) {
         hipLaunchKernelGGL(xface_single, grid, dim3(256), 0, s, bufs, 1);
         break;
       case 2: hipLaunchKernelGGL(xface_paired<2>, grid, dim3(256), 0, s, bufs, sink); break;
-      default: hipLaunchKernelGGL(xface_paired<3>, grid, dim3(256), 0, s, bufs, sink); break;
+      case 3: hipLaunchKernelGGL(xface_paired<3>, grid, dim3(256), 0, s, bufs, sink); break;
+      case 4: hipLaunchKernelGGL((xface_paired<0, 1>), grid, dim3(256), 0, s, bufs, sink); break;
+      case 5: hipLaunchKernelGGL((xface_paired<3, 1>), grid, dim3(256), 0, s, bufs, sink); break;
+      case 6: hipLaunchKernelGGL((xface_paired<0, 2>), grid, dim3(256), 0, s, bufs, sink); break;
+      case 7: hipLaunchKernelGGL((xface_paired<3, 2>), grid, dim3(256), 0, s, bufs, sink); break;
+      case 8: hipLaunchKernelGGL((xface_paired<0, 3>), grid, dim3(256), 0, s, bufs, sink); break;
+      case 9: hipLaunchKernelGGL((xface_paired<3, 3>), grid, dim3(256), 0, s, bufs, sink); break;
+      case 10: hipLaunchKernelGGL((xface_paired<4, 0>), grid, dim3(256), 0, s, bufs, sink); break;
+      default: hipLaunchKernelGGL((xface_paired<4, 1>), grid, dim3(256), 0, s, bufs, sink); break;
       }
     };
     run();
@@ -125,7 +153,8 @@ int main(int argc, char **argv) {
     const double us = double(ms) * 1e3 / reps;
     std::printf("{\"bench\": \"xface\", \"variant\": \"%s\", \"rows\": %u, \"quants\": %d, \"payload\": %.0f, "
                 "\"us\": %.1f, \"alg_GBps\": %.1f}\n",
-                names[v], kRows * 2, kQ, payload, us, (v == 3 ? 1.0 : 2.0) * payload / (us * 1e-6) / 1e9);
+                names[v], kRows * 2, kQ, payload, us,
+                (v == 3 || v == 5 || v == 7 || v == 9 ? 1.0 : v >= 10 ? 1.0 / 3 : 2.0) * payload / (us * 1e-6) / 1e9);
     std::fflush(stdout);
   }
   return 0;
