@@ -62,7 +62,8 @@ def test_completion_family_host():
                                     (2, ("completion.py",)), (1, ("probe_order.py",)), (2, ("probe_order.py",)),
                                     (1, ("persistent.py",)), (2, ("persistent.py",)),
                                     (2, ("fuzz.py", "3", "7", "--host")),
-                                    (3, ("fuzz.py", "3", "11", "--modes", "--host"))])
+                                    (3, ("fuzz.py", "3", "11", "--modes", "--host")),
+                                    (1, ("isend_self.py",)), (2, ("isend_self.py",))])
 def test_tempi_host_paths_without_gpu(n, prog):
     """TEMPI's own host-side paths -- descriptor-aware host receives, the probe
     family and its held messages, send gates, host collectives -- which run

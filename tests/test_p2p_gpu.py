@@ -234,6 +234,15 @@ def test_nbr_alltoallv_sparse_app(gpu, ranks, scale, density, env):
     assert rc == 0 and r["checked"] and r["errors"] == 0 and r["buffers"] == "device", out[-3000:]
 
 
+@pytest.mark.parametrize("n", [1, 2])
+@pytest.mark.parametrize("method", ["AUTO", "ONESHOT", "STAGED"])
+def test_isend_self_reference(gpu, n, method):
+    """the reference's isend.cu / isend_contiguous.cu: send to self, then
+    receive, waiting on the send first; host and device, bytes checked"""
+    rc, out = mpi_launch.run(n, mpi_launch.py("isend_self.py", "--device"), env=METHODS[method], timeout=180)
+    assert rc == 0 and "RESULT errors=0" in out, out[-3000:]
+
+
 @pytest.mark.parametrize("method", ["AUTO", "ONESHOT", "IPC", "STAGED", "XCOPY"])
 def test_completion_family_device(gpu, method):
     """TEMPI device requests mixed with library requests through

@@ -47,6 +47,16 @@ def test_interp_2d_kat(b, x, exp):
     assert t2(A, b, x) == pytest.approx(exp, rel=0, abs=1e-5)
 
 
+@pytest.mark.parametrize("b, lo, hi, frac", [(1, 0, 0, 0.0), (2, 1, 1, 0.0), (3, 1, 2, 0.5), (4, 2, 2, 0.0),
+                                             (5, 2, 3, 0.25)])
+def test_log2_floor_ceil(b, lo, hi, frac):
+    """the reference's numeric test (/root/reference/test/numeric.cpp:13-26:
+    log2_ceil / log2_floor of 1..5), seen through the interpolation that uses
+    them: `b` bytes lie between table entries floor(log2 b) and ceil(log2 b)"""
+    v = [1.0 + 10.0 * i for i in range(6)]
+    assert t1(v, b) == pytest.approx(v[lo] * (1 - frac) + v[hi] * frac, rel=1e-6)
+
+
 def test_unknown_is_inf():
     assert math.isinf(L.tempi_interp_time((ctypes.c_double * 1)(), 0, 100))
 

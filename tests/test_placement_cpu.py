@@ -151,3 +151,12 @@ def test_placement_off_by_default():
     rc, out = mpi_launch.run(4, mpi_launch.py("placement.py", "--expect-none"), env={"TEMPI_FAKE_NODE_SIZE": "2"},
                              timeout=180)
     assert rc == 0 and "RESULT errors=0" in out, out[-3000:]
+
+
+@pytest.mark.parametrize("n, node", [(4, 2), (8, 4), (8, 2)])
+@pytest.mark.parametrize("method", ["TEMPI_PLACEMENT_METIS", "TEMPI_PLACEMENT_RANDOM"])
+def test_reference_pairs_graph(n, node, method):
+    """the reference's dist_graph_create_adjacent test: rank <-> rank + n/2"""
+    rc, out = mpi_launch.run(n, mpi_launch.py("dist_graph_pairs.py"), env={method: "", "TEMPI_FAKE_NODE_SIZE": str(node)},
+                             timeout=180)
+    assert rc == 0 and "RESULT errors=0" in out, out[-3000:]
