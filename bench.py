@@ -217,15 +217,22 @@ def config1(mpi, torch, dev, iters=300):
                "gpu_us": round(gpu * 1e6, 2), "gpu_payload_GBps": round(512 * 1024 / gpu / 1e9, 2),
                "speedup": round(cpu / gpu, 2), "gpu_matches_cpu": ok}
         # the same call in C, on this box, with its phases (apps/bench_lib.cpp
-        # tempi_bench_sync_phases): where a synchronous GPU MPI_Pack's time goes
+        # tempi_bench_sync_phases): where a synchronous GPU MPI_Pack's time goes;
+        # pinned to the core the host MPI_Pack above ran on, both sides
         try:
             import ctypes
 
             buf = ctypes.create_string_buffer(2048)
             L = apps_lib()
             L.tempi_bench_sync_phases.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
-            if L.tempi_bench_sync_phases(iters, buf, 2048) == 0 and buf.value:
+            os.sched_setaffinity(0, {sorted(old)[0]})
+            try:
+                rc = L.tempi_bench_sync_phases(iters, buf, 2048)
+            finally:
+                os.sched_setaffinity(0, old)
+            if rc == 0 and buf.value:
                 out["c_phases"] = json.loads(buf.value.decode())
+                out["c_phases"]["pinned_core"] = sorted(old)[0]
         except Exception as e:  # (reported, never fatal to the line)
             out["c_phases"] = {"error": str(e)[:200]}
     finally:

@@ -8,6 +8,9 @@
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp HYDRA_LAUNCHER=fork
 O=gpurun_out; mkdir -p $O; : > $O/xface_pol.jsonl
+echo "== smoke"
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 2; }
+tail -2 $O/smoke.log
 for r in 1 2; do
   timeout -k 10 120 tools/_variants/xface 20 | sed "s/^{/{\"round\": $r, /" >> $O/xface_pol.jsonl || exit 3
 done
