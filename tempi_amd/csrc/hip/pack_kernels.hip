@@ -212,28 +212,6 @@ template <typename T> __device__ __forceinline__ T ld(const T *p, bool nt) {
   }
   return *p;
 }
-// a relaxed agent-scope load (global_load ... sc1: past L1, served by L2)
-template <typename T> __device__ __forceinline__ T ld_agent(const T *p) {
-  static_assert(sizeof(T) <= 8, "one load of at most 8 bytes");
-  typedef typename std::conditional<
-      sizeof(T) == 8, uint64_t,
-      typename std::conditional<sizeof(T) == 4, uint32_t,
-                                typename std::conditional<sizeof(T) == 2, uint16_t, uint8_t>::type>::type>::type U;
-  const U x = __hip_atomic_load(reinterpret_cast<const U *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  T v;
-  __builtin_memcpy(&v, &x, sizeof(T));
-  return v;
-}
-// cache policy of the strided-side loads of words narrower than 16 bytes
-// (gathers, and the sources of direct copies): 0 plain, 1 nontemporal,
-// 2 agent scope (A/B knob: an isolated narrow row reads a whole 128-byte line)
-#ifndef TEMPI_NARROW_LD
-#define TEMPI_NARROW_LD 0
-#endif
-template <typename T> __device__ __forceinline__ T ld_narrow(const T *p, bool nt) {
-  if constexpr (sizeof(T) < 16 && TEMPI_NARROW_LD == 2) return ld_agent(p);
-  return ld(p, nt || (sizeof(T) < 16 && TEMPI_NARROW_LD == 1));
-}
 template <typename T> __device__ __forceinline__ void st(T *p, const T &v, bool nt) {
   if (nt) {
     typedef typename NativeOf<T>::type N;
@@ -460,13 +438,13 @@ __device__ __forceinline__ void pack_body(const KArgs<ND> &a, uint32_t blk, uint
           // row, one add apart -- no word-in-row bookkeeping at all
 #pragma unroll
           for (int j = 0; j < CW; ++j) {
-            buf[u].w[j] = ld_narrow(reinterpret_cast<const WT *>(a.strided + off), NtStrided<W>::value);
+            buf[u].w[j] = ld(reinterpret_cast<const WT *>(a.strided + off), NtStrided<W>::value);
             if constexpr (ND >= 1) off += a.stride[0];
           }
         } else if (run) {
 #pragma unroll
           for (int j = 0; j < CW; ++j) {
-            buf[u].w[j] = ld_narrow(reinterpret_cast<const WT *>(a.strided + off + int64_t(w) * W), NtStrided<W>::value);
+            buf[u].w[j] = ld(reinterpret_cast<const WT *>(a.strided + off + int64_t(w) * W), NtStrided<W>::value);
             if (j + 1 < CW && ++w == a.wpr) {
               w = 0;
               if constexpr (ND >= 1) off += a.stride[0];
@@ -475,7 +453,7 @@ __device__ __forceinline__ void pack_body(const KArgs<ND> &a, uint32_t blk, uint
         } else {
 #pragma unroll
           for (int j = 0; j < CW; ++j) {
-            buf[u].w[j] = ld_narrow(reinterpret_cast<const WT *>(a.strided + off + int64_t(w) * W), NtStrided<W>::value);
+            buf[u].w[j] = ld(reinterpret_cast<const WT *>(a.strided + off + int64_t(w) * W), NtStrided<W>::value);
             if (j + 1 < CW && ++w == a.wpr) {
               w = 0;
               next_row<ND>(off, dig, a);
@@ -1400,7 +1378,7 @@ template <typename T> __device__ __forceinline__ T ld_sys(const T *p) {
 }
 template <typename T> __device__ __forceinline__ T ld_src(const CArgs &a, const T *p, bool nt) {
   if (a.flags & TEMPI_HIP_ITEM_REMOTE) return ld_sys(p);
-  return ld_narrow(p, nt);
+  return ld(p, nt);
 }
 
 template <int W> __device__ __forceinline__ int64_t side_offset(uint32_t q, const CSide &c) {

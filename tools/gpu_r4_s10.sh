@@ -1,4 +1,5 @@
 #!/bin/bash
+# (The switch was removed after this A/B; rebuild from commit 376322d to repeat.)
 # Halo A/B of the narrow strided-side load policy (tools/build_ab.sh
 # "nt:-DTEMPI_NARROW_LD=1" "sc1:-DTEMPI_NARROW_LD=2", copied to
 # tools/_variants/ld_<v>/libtempi_hip.so): 512^3, 10 iterations, content

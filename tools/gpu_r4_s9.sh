@@ -1,4 +1,5 @@
 #!/bin/bash
+# (The build switch was removed after this A/B; rebuild from commit 376322d to repeat.)
 # Round 4: can a load's cache policy cut the isolated 24-byte rows' fetch?
 # (1) tools/xface.hip bare pattern by load policy, two rounds, then FETCH_SIZE /
 #     WRITE_SIZE passes; (2) hbench (the halo's regions as the transport
