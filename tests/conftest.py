@@ -17,7 +17,7 @@ def pytest_configure(config):
 # exact checks) runs before anything else, so that under `pytest -x` a failure
 # in a transport or tool test can never hide it (round 3: one NameError in a
 # fuzz script stopped the run before test_pack_gpu.py was reached).
-FIRST = ("test_oracle.py", "test_pack_gpu.py", "test_dense_gpu.py", "test_direct_gpu.py")
+FIRST = ("test_oracle.py", "test_pack_gpu.py", "test_fuzz_parity.py", "test_dense_gpu.py", "test_direct_gpu.py")
 
 
 def pytest_collection_modifyitems(session, config, items):
