@@ -19,7 +19,7 @@ import pytest
 from oracle import pyoracle
 from tests import typegen, typezoo
 
-CHUNKS = 12
+CHUNKS = 40
 PER_CHUNK = 50
 
 
