@@ -1,0 +1,76 @@
+// tools/launchcost.hip -- how much of a synchronous MPI_Pack's launch is
+// HIP's and how much is TEMPI's (config 1: vector(1024, 512, 1024), 512 KiB).
+// Host time per call, median of REPS, on one non-blocking stream:
+//   bare_launch    hipLaunchKernelGGL of an empty kernel whose arguments are
+//                  the size of the packer's (KArgs<1> + Sig, 184 B)
+//   bare_roundtrip the same + hipStreamSynchronize
+//   tempi_launch   tempi_hip_pack_ticket (descriptor -> launch, the ticket
+//                  folded in), host time only
+//   tempi_call     tempi_hip_pack_ticket + tempi_hip_ticket_wait
+// usage: launchcost [REPS]  (links libtempi_hip.so)
+//   hipcc --offload-arch=gfx950 -O2 -Iinclude -o tools/_variants/launchcost tools/launchcost.hip
+//         -Ltempi_amd/lib -ltempi_hip -Wl,-rpath,'$ORIGIN/../../tempi_amd/lib'
+#include <hip/hip_runtime.h>
+
+#include "tempi_hip.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+struct Args184 {
+  unsigned char b[184];
+};
+__global__ void empty_kernel(Args184 a) {
+  if (a.b[0] == 0xEE && threadIdx.x == 1000) a.b[1] = 0; // never true; keeps the argument
+}
+
+static double now_us() {
+  return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+static double med(std::vector<double> v) {
+  std::sort(v.begin(), v.end());
+  return v[v.size() / 2];
+}
+
+int main(int argc, char **argv) {
+  const int reps = argc > 1 ? std::atoi(argv[1]) : 2000;
+  const int rows = 1024, block = 512, stride = 1024;
+  char *src = nullptr, *dst = nullptr;
+  if (hipMalloc(&src, size_t(rows) * stride) || hipMalloc(&dst, size_t(rows) * block)) return 3;
+  hipStream_t s;
+  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking)) return 3;
+  tempi_hip_desc d{};
+  d.block = block;
+  d.ndims = 1;
+  d.counts[0] = rows;
+  d.strides[0] = stride;
+  Args184 a{};
+  std::vector<double> bl, br, tl, tc;
+  for (int i = 0; i < reps + 50; ++i) {
+    const bool keep = i >= 50;
+    double t0 = now_us();
+    hipLaunchKernelGGL(empty_kernel, dim3(256), dim3(128), 0, s, a);
+    double t1 = now_us();
+    if (hipStreamSynchronize(s)) return 4;
+    double t2 = now_us();
+    const uint32_t *flag = nullptr;
+    uint32_t ticket = 0;
+    if (tempi_hip_pack_ticket(dst, src, &d, s, &flag, &ticket)) return 5;
+    double t3 = now_us();
+    if (tempi_hip_ticket_wait(s, flag, ticket)) return 6;
+    double t4 = now_us();
+    if (keep) {
+      bl.push_back(t1 - t0);
+      br.push_back(t2 - t0);
+      tl.push_back(t3 - t2);
+      tc.push_back(t4 - t2);
+    }
+  }
+  std::printf("{\"bench\": \"launchcost\", \"reps\": %d, \"bare_launch_us\": %.2f, \"bare_roundtrip_us\": %.2f, "
+              "\"tempi_launch_us\": %.2f, \"tempi_call_us\": %.2f, \"tempi_own_us\": %.2f}\n",
+              reps, med(bl), med(br), med(tl), med(tc), med(tl) - med(bl));
+  return 0;
+}
