@@ -7,10 +7,15 @@
 //   tempi_launch   tempi_hip_pack_ticket (descriptor -> launch, the ticket
 //                  folded in), host time only
 //   tempi_call     tempi_hip_pack_ticket + tempi_hip_ticket_wait
+// and the pointer classification every interposed call makes (a device and
+// a malloc'd host pointer): hipPointerGetAttributes, hsa_amd_pointer_info,
+// and tempi_hip_pointer_info (what the interposer calls).
 // usage: launchcost [REPS]  (links libtempi_hip.so)
 //   hipcc --offload-arch=gfx950 -O2 -Iinclude -o tools/_variants/launchcost tools/launchcost.hip
-//         -Ltempi_amd/lib -ltempi_hip -Wl,-rpath,'$ORIGIN/../../tempi_amd/lib'
+//         -Ltempi_amd/lib -ltempi_hip -lhsa-runtime64 -Wl,-rpath,'$ORIGIN/../../tempi_amd/lib'
 #include <hip/hip_runtime.h>
+
+#include <hsa/hsa_ext_amd.h>
 
 #include "tempi_hip.h"
 
@@ -69,6 +74,41 @@ int main(int argc, char **argv) {
       tc.push_back(t4 - t2);
     }
   }
+  // pointer classification, 1000 calls per timing, median of 50
+  std::vector<char> hostbuf(1 << 20);
+  void *ptrs[2] = {src + 4096, hostbuf.data() + 4096};
+  double cls[2][3];
+  for (int p = 0; p < 2; ++p) {
+    std::vector<double> v[3];
+    for (int r = 0; r < 50; ++r) {
+      double t0 = now_us();
+      for (int i = 0; i < 1000; ++i) {
+        hipPointerAttribute_t at;
+        (void)hipPointerGetAttributes(&at, ptrs[p]);
+      }
+      (void)hipGetLastError();
+      double t1 = now_us();
+      for (int i = 0; i < 1000; ++i) {
+        hsa_amd_pointer_info_t info;
+        info.size = sizeof(info);
+        (void)hsa_amd_pointer_info(ptrs[p], &info, nullptr, nullptr, nullptr);
+      }
+      double t2 = now_us();
+      for (int i = 0; i < 1000; ++i) {
+        tempi_hip_ptrinfo pi;
+        (void)tempi_hip_pointer_info(ptrs[p], &pi);
+      }
+      double t3 = now_us();
+      v[0].push_back((t1 - t0) / 1000);
+      v[1].push_back((t2 - t1) / 1000);
+      v[2].push_back((t3 - t2) / 1000);
+    }
+    for (int k = 0; k < 3; ++k) cls[p][k] = med(v[k]);
+  }
+  std::printf("{\"bench\": \"classify\", \"device_ns\": {\"hipPointerGetAttributes\": %.0f, \"hsa_amd_pointer_info\": %.0f, "
+              "\"tempi_hip_pointer_info\": %.0f}, \"host_ns\": {\"hipPointerGetAttributes\": %.0f, "
+              "\"hsa_amd_pointer_info\": %.0f, \"tempi_hip_pointer_info\": %.0f}}\n",
+              cls[0][0] * 1e3, cls[0][1] * 1e3, cls[0][2] * 1e3, cls[1][0] * 1e3, cls[1][1] * 1e3, cls[1][2] * 1e3);
   std::printf("{\"bench\": \"launchcost\", \"reps\": %d, \"bare_launch_us\": %.2f, \"bare_roundtrip_us\": %.2f, "
               "\"tempi_launch_us\": %.2f, \"tempi_call_us\": %.2f, \"tempi_own_us\": %.2f}\n",
               reps, med(bl), med(br), med(tl), med(tc), med(tl) - med(bl));
