@@ -20,7 +20,7 @@ CXXFLAGS := -std=c++17 -O2 -g -fPIC -fvisibility=hidden -Wall -Wextra -Wno-unuse
 
 APPS := $(LIB)/libtempi_apps.so $(LIB)/halo_exchange $(LIB)/pingpong_nd $(LIB)/pingpong_1d $(LIB)/alltoallv_sparse \
         $(LIB)/measure_system \
-        $(LIB)/type_commit $(LIB)/mpi_pack $(LIB)/pack_bench
+        $(LIB)/type_commit $(LIB)/mpi_pack $(LIB)/mpi_isend $(LIB)/pack_bench
 
 all: $(LIB)/libtempi.so $(APPS) oracle
 
@@ -61,6 +61,10 @@ $(LIB)/pingpong_1d: apps/pingpong_1d.cpp $(LIB)/libtempi_apps.so
 	    -ltempi -ltempi_hip -L$(MPI_HOME)/lib -lmpi -static-libstdc++ -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,$(MPI_HOME)/lib
 
 $(LIB)/alltoallv_sparse: apps/alltoallv_sparse.cpp $(LIB)/libtempi_apps.so
+	$(HIPCC) --offload-arch=gfx950 -O2 -std=c++17 -Iinclude -I$(MPI_HOME)/include -o $@ $< -L$(LIB) -ltempi_apps \
+	    -ltempi -ltempi_hip -L$(MPI_HOME)/lib -lmpi -static-libstdc++ -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,$(MPI_HOME)/lib
+
+$(LIB)/mpi_isend: apps/mpi_isend.cpp $(LIB)/libtempi_apps.so
 	$(HIPCC) --offload-arch=gfx950 -O2 -std=c++17 -Iinclude -I$(MPI_HOME)/include -o $@ $< -L$(LIB) -ltempi_apps \
 	    -ltempi -ltempi_hip -L$(MPI_HOME)/lib -lmpi -static-libstdc++ -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,$(MPI_HOME)/lib
 

@@ -262,6 +262,80 @@ EXPORT int tempi_bench_pingpong_1d(int iters, long total, int check, int setDevi
   return errors ? 3 : 0;
 }
 
+// tempi_bench_isend: the reference's bench_mpi_isend
+// (/root/reference/bin/bench_mpi_isend.cpp:21-83): ranks 0 and 1 ping-pong
+// `tags` overlapping contiguous MPI_BYTE messages of `bytes` each (device
+// buffers) -- rank 0 MPI_Isend's all of them and MPI_Waitall's, then posts
+// the MPI_Irecv's for the replies; rank 1 the other way round. Reported as
+// there: 2 x bytes / trimean(round trip) in MiB/s (:130), plus every received
+// byte checked when `check` (the reference checks none).
+EXPORT int tempi_bench_isend(int iters, long bytes, int tags, int check, char *json, int jsonCap) {
+  int rank, size;
+  MPI_Comm_rank(MPI_COMM_WORLD, &rank);
+  MPI_Comm_size(MPI_COMM_WORLD, &size);
+  if (size < 2 || bytes <= 0 || bytes > (1L << 30) || tags < 1) return 2;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess) ndev = 0; // (host buffers need no GPU)
+  if (ndev > 0) HIPCHECK(hipSetDevice(rank % ndev));
+  const bool active = rank < 2;
+  const int peer = 1 - rank;
+  std::vector<char *> srcs(static_cast<size_t>(tags)), dsts(static_cast<size_t>(tags));
+  std::vector<unsigned char> h(static_cast<size_t>(bytes));
+  for (int t = 0; t < tags; ++t) {
+    srcs[size_t(t)] = static_cast<char *>(buf_alloc(size_t(bytes)));
+    dsts[size_t(t)] = static_cast<char *>(buf_alloc(size_t(bytes)));
+    for (size_t i = 0; i < h.size(); ++i) h[i] = (unsigned char)((i * 13 + size_t(t) * 7 + size_t(rank) * 101) & 0xFF);
+    buf_copy(srcs[size_t(t)], h.data(), h.size());
+  }
+  std::vector<MPI_Request> reqs(static_cast<size_t>(tags));
+  std::vector<double> times;
+  auto sends = [&] {
+    for (int t = 0; t < tags; ++t) MPI_Isend(srcs[size_t(t)], int(bytes), MPI_BYTE, peer, t, MPI_COMM_WORLD, &reqs[size_t(t)]);
+    MPI_Waitall(tags, reqs.data(), MPI_STATUSES_IGNORE);
+  };
+  auto recvs = [&] {
+    for (int t = 0; t < tags; ++t) MPI_Irecv(dsts[size_t(t)], int(bytes), MPI_BYTE, peer, t, MPI_COMM_WORLD, &reqs[size_t(t)]);
+    MPI_Waitall(tags, reqs.data(), MPI_STATUSES_IGNORE);
+  };
+  for (int i = 0; i < iters + 2; ++i) {
+    MPI_Barrier(MPI_COMM_WORLD);
+    const double t0 = MPI_Wtime();
+    if (active && rank == 0) {
+      sends();
+      recvs();
+    } else if (active) {
+      recvs();
+      sends();
+    }
+    double el = MPI_Wtime() - t0;
+    MPI_Allreduce(MPI_IN_PLACE, &el, 1, MPI_DOUBLE, MPI_MAX, MPI_COMM_WORLD);
+    if (i >= 2) times.push_back(el);
+  }
+  long errors = 0;
+  if (check && active) {
+    std::vector<unsigned char> g(static_cast<size_t>(bytes));
+    for (int t = 0; t < tags; ++t) {
+      buf_copy(g.data(), dsts[size_t(t)], g.size());
+      for (size_t i = 0; i < g.size(); ++i)
+        errors += g[i] != (unsigned char)((i * 13 + size_t(t) * 7 + size_t(peer) * 101) & 0xFF);
+    }
+  }
+  MPI_Allreduce(MPI_IN_PLACE, &errors, 1, MPI_LONG, MPI_SUM, MPI_COMM_WORLD);
+  if (rank == 0 && json && jsonCap > 0) {
+    const double rt = trimean(times);
+    std::snprintf(json, size_t(jsonCap),
+                  "{\"bytes\": %ld, \"tags\": %d, \"iters\": %d, \"roundtrip_us\": %.2f, \"MiBps\": %.2f, "
+                  "\"checked\": %s, \"errors\": %ld, \"method\": \"%s\", \"buffers\": \"%s\"}",
+                  bytes, tags, iters, rt * 1e6, 2.0 * double(bytes) / 1024 / 1024 / rt, check ? "true" : "false", errors,
+                  method_name(), host_buffers() ? "host" : "device");
+  }
+  for (int t = 0; t < tags; ++t) {
+    buf_free(srcs[size_t(t)]);
+    buf_free(dsts[size_t(t)]);
+  }
+  return errors ? 3 : 0;
+}
+
 __global__ void a2av_fill(unsigned char *buf, const int64_t *displ, const int64_t *count, const int *dst, int n,
                           int src) {
   for (int d = 0; d < n; ++d)

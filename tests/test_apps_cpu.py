@@ -119,3 +119,16 @@ def test_pingpong_1d_host(mode, ranks):
     recs = [json.loads(l) for l in out.splitlines() if l.startswith("{")]
     assert rc == 0 and len(recs) == 2 and all(r["errors"] == 0 and r["checked"] for r in recs), out[-3000:]
     assert recs[0]["pairs"] == ranks // 2
+
+
+@pytest.mark.parametrize("mode", list(MODES))
+@pytest.mark.parametrize("ranks", [2, 3])
+def test_mpi_isend_host(mode, ranks):
+    """the reference's bench_mpi_isend (10 overlapping MPI_BYTE messages each
+    way between ranks 0 and 1, others idle) on host buffers, every byte checked"""
+    rc, out = mpi_launch.run(ranks, [os.path.join(LIB, "mpi_isend"), "2", "1", "4096", str(1 << 20), "--check"],
+                             env=MODES[mode], timeout=120)
+    recs = [json.loads(l) for l in out.splitlines() if l.startswith("{")]
+    assert rc == 0 and len(recs) == 3 and all(r["errors"] == 0 and r["checked"] for r in recs), out[-3000:]
+    assert all(r["tags"] == 10 and r["buffers"] == "host" for r in recs)
+

@@ -218,6 +218,16 @@ def test_pingpong_1d_app(gpu, ranks, env):
     assert rc == 0 and len(recs) == 4 and all(r["errors"] == 0 and r["buffers"] == "device" for r in recs), out[-3000:]
 
 
+@pytest.mark.parametrize("env", [{}, {"TEMPI_CONTIGUOUS_STAGED": "1"}, METHODS["XCOPY"], {"TEMPI_DATATYPE_ONESHOT": "1"}])
+def test_mpi_isend_app(gpu, env):
+    """the reference's bench_mpi_isend on device buffers: 10 overlapping
+    contiguous messages each way, 1 B to 1 MiB, every byte checked"""
+    rc, out = mpi_launch.run(2, [os.path.join(LIB, "mpi_isend"), "3", "1", "64", "4096", "65536", str(1 << 20),
+                                 "--check"], env=env, timeout=240)
+    recs = [json.loads(l) for l in out.splitlines() if l.startswith("{")]
+    assert rc == 0 and len(recs) == 5 and all(r["errors"] == 0 and r["buffers"] == "device" for r in recs), out[-3000:]
+
+
 @pytest.mark.parametrize("ranks,scale,density,env", [
     (2, 100000, 1.0, {}), (4, 1000, 0.5, {}), (3, 10, 1.0, {"TEMPI_DATATYPE_ONESHOT": "1"}),
     (8, 1, 1.0, {}), (8, 100000, 0.5, {}), (8, 1000000, 0.125, {"TEMPI_STREAMS": "3"}),
