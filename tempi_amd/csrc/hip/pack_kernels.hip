@@ -1059,7 +1059,23 @@ int launch_batch_nd(bool pack, const std::vector<Job> &jobs, hipStream_t s, temp
           }
     }
     constexpr bool kScatterWT = W == 16;
-    if (total) {
+    if (total && b.nitems == 1) {
+      // one item (a lone small message): the single-object kernel, same body,
+      // whose arguments are the item alone instead of the 3.5 KiB batch
+      const KArgs<ND> &a = b.item[0];
+      if (il)
+        if (pack)
+          hipLaunchKernelGGL((wtc ? pack_il_kernel<W, ND, true> : pack_il_kernel<W, ND, false>), dim3(total),
+                             dim3(kBlock), 0, s, a, sg);
+        else
+          hipLaunchKernelGGL((unpack_il_kernel<W, ND>), dim3(total), dim3(kBlock), 0, s, a, sg);
+      else if (pack)
+        hipLaunchKernelGGL((wtc ? pack_kernel<W, ND, true> : pack_kernel<W, ND, false>), dim3(total), dim3(kBlock),
+                           0, s, a, sg);
+      else
+        hipLaunchKernelGGL((wtc ? unpack_kernel<W, ND, kScatterWT> : unpack_kernel<W, ND, false>), dim3(total),
+                           dim3(kBlock), 0, s, a, sg);
+    } else if (total) {
       if (il)
         if (pack)
           hipLaunchKernelGGL((wtc ? pack_il_batch_kernel<W, ND, true> : pack_il_batch_kernel<W, ND, false>),
