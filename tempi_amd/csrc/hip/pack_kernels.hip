@@ -770,18 +770,14 @@ __global__ __launch_bounds__(kBlock) void pack_dense_kernel(const KArgs<ND> a, c
 // uniform binary search over the range starts. This replaces one launch
 // (~7 us of host time on MI355X/ROCm 7.2) per message by one per batch.
 constexpr int kBatchBytes = 3584;
-template <int ND> constexpr int batch_full() { return int((kBatchBytes - 8) / (sizeof(KArgs<ND>) + 4)); }
-// a batch of a few objects carries a small argument block (the host's launch
-// cost grows with the bytes of kernel arguments it copies)
-constexpr int kSmallBatch = 8;
-template <int ND, int CAP = batch_full<ND>()> struct BatchArgs {
-  static constexpr int kMax = CAP;
+template <int ND> struct BatchArgs {
+  static constexpr int kMax = int((kBatchBytes - 8) / (sizeof(KArgs<ND>) + 4));
   uint32_t nitems;
-  uint32_t first[CAP + 1]; // first workgroup of each object; first[nitems] = total
-  KArgs<ND> item[CAP];
+  uint32_t first[kMax + 1]; // first workgroup of each object; first[nitems] = total
+  KArgs<ND> item[kMax];
 };
 
-template <int ND, int CAP> __device__ __forceinline__ uint32_t find_item(const BatchArgs<ND, CAP> &b, uint32_t blk) {
+template <int ND> __device__ __forceinline__ uint32_t find_item(const BatchArgs<ND> &b, uint32_t blk) {
   uint32_t lo = 0, hi = b.nitems;
   while (hi - lo > 1) {
     const uint32_t mid = (lo + hi) >> 1;
@@ -795,32 +791,32 @@ template <int ND, int CAP> __device__ __forceinline__ uint32_t find_item(const B
 
 // (sg: a completion ticket folded into the launch, as in the single-object
 // kernels; a workgroup's partial chunks are its item's first / last tile)
-template <int W, int ND, bool WTC, int CAP>
-__global__ __launch_bounds__(kBlock) void pack_batch_kernel(const BatchArgs<ND, CAP> b, const Sig sg) {
-  const uint32_t i = find_item(b, blockIdx.x), n = b.first[i + 1] - b.first[i];
+template <int W, int ND, bool WTC>
+__global__ __launch_bounds__(kBlock) void pack_batch_kernel(const BatchArgs<ND> b, const Sig sg) {
+  const uint32_t i = find_item<ND>(b, blockIdx.x), n = b.first[i + 1] - b.first[i];
   const uint32_t blk = xcd_tile(blockIdx.x - b.first[i], n, b.item[i].flags); // (within the item: balanced)
   pack_body<W, ND, WTC>(b.item[i], blk, n);
   wg_signal(sg, needs_release(b.item[i].flags, blk, n));
 }
 
-template <int W, int ND, bool WTC, int CAP>
-__global__ __launch_bounds__(kBlock) void pack_il_batch_kernel(const BatchArgs<ND, CAP> b, const Sig sg) {
-  const uint32_t i = find_item(b, blockIdx.x), n = b.first[i + 1] - b.first[i];
+template <int W, int ND, bool WTC>
+__global__ __launch_bounds__(kBlock) void pack_il_batch_kernel(const BatchArgs<ND> b, const Sig sg) {
+  const uint32_t i = find_item<ND>(b, blockIdx.x), n = b.first[i + 1] - b.first[i];
   const uint32_t blk = xcd_tile(blockIdx.x - b.first[i], n, b.item[i].flags); // (within the item: balanced)
   pack_il_tile<W, ND, WTC>(b.item[i], blk, n);
   wg_signal(sg, needs_release(b.item[i].flags, blk, n));
 }
-template <int W, int ND, int CAP>
-__global__ __launch_bounds__(kBlock) void unpack_il_batch_kernel(const BatchArgs<ND, CAP> b, const Sig sg) {
-  const uint32_t i = find_item(b, blockIdx.x), n = b.first[i + 1] - b.first[i];
+template <int W, int ND>
+__global__ __launch_bounds__(kBlock) void unpack_il_batch_kernel(const BatchArgs<ND> b, const Sig sg) {
+  const uint32_t i = find_item<ND>(b, blockIdx.x), n = b.first[i + 1] - b.first[i];
   const uint32_t blk = xcd_tile(blockIdx.x - b.first[i], n, b.item[i].flags); // (within the item: balanced)
   unpack_il_tile<W, ND>(b.item[i], blk, n);
   wg_signal(sg, true);
 }
 
-template <int W, int ND, bool WTC, int CAP>
-__global__ __launch_bounds__(kBlock) void unpack_batch_kernel(const BatchArgs<ND, CAP> b, const Sig sg) {
-  const uint32_t i = find_item(b, blockIdx.x), n = b.first[i + 1] - b.first[i];
+template <int W, int ND, bool WTC>
+__global__ __launch_bounds__(kBlock) void unpack_batch_kernel(const BatchArgs<ND> b, const Sig sg) {
+  const uint32_t i = find_item<ND>(b, blockIdx.x), n = b.first[i + 1] - b.first[i];
   const uint32_t blk = xcd_tile(blockIdx.x - b.first[i], n, b.item[i].flags); // (within the item: balanced)
   unpack_body<W, ND, WTC>(b.item[i], blk, n);
   wg_signal(sg, needs_release(b.item[i].flags, blk, n));
@@ -1037,25 +1033,6 @@ struct Job {
   uint32_t flags;
 };
 
-// one batch launch of capacity CAP (the kernel family of the batch's width)
-template <int W, int ND, int CAP>
-void launch_batch_kernel(bool pack, bool il, bool wtc, uint32_t total, hipStream_t s, const BatchArgs<ND, CAP> &b,
-                         const Sig &sg) {
-  constexpr bool kScatterWT = W == 16;
-  if (il)
-    if (pack)
-      hipLaunchKernelGGL((wtc ? pack_il_batch_kernel<W, ND, true, CAP> : pack_il_batch_kernel<W, ND, false, CAP>),
-                         dim3(total), dim3(kBlock), 0, s, b, sg);
-    else
-      hipLaunchKernelGGL((unpack_il_batch_kernel<W, ND, CAP>), dim3(total), dim3(kBlock), 0, s, b, sg);
-  else if (pack)
-    hipLaunchKernelGGL((wtc ? pack_batch_kernel<W, ND, true, CAP> : pack_batch_kernel<W, ND, false, CAP>), dim3(total),
-                       dim3(kBlock), 0, s, b, sg);
-  else
-    hipLaunchKernelGGL((wtc ? unpack_batch_kernel<W, ND, kScatterWT, CAP> : unpack_batch_kernel<W, ND, false, CAP>),
-                       dim3(total), dim3(kBlock), 0, s, b, sg);
-}
-
 // fold: offered to this group's last launch (the caller passes it to the
 // batch's last group only, so that the ticket follows every launch of it)
 template <int W, int ND>
@@ -1098,14 +1075,19 @@ int launch_batch_nd(bool pack, const std::vector<Job> &jobs, hipStream_t s, temp
       else
         hipLaunchKernelGGL((wtc ? unpack_kernel<W, ND, kScatterWT> : unpack_kernel<W, ND, false>), dim3(total),
                            dim3(kBlock), 0, s, a, sg);
-    } else if (total && b.nitems <= uint32_t(kSmallBatch)) {
-      BatchArgs<ND, kSmallBatch> sb;
-      sb.nitems = b.nitems;
-      for (uint32_t k = 0; k <= b.nitems; ++k) sb.first[k] = b.first[k];
-      for (uint32_t k = 0; k < b.nitems; ++k) sb.item[k] = b.item[k];
-      launch_batch_kernel<W, ND, kSmallBatch>(pack, il, wtc, total, s, sb, sg);
     } else if (total) {
-      launch_batch_kernel<W, ND, BatchArgs<ND>::kMax>(pack, il, wtc, total, s, b, sg);
+      if (il)
+        if (pack)
+          hipLaunchKernelGGL((wtc ? pack_il_batch_kernel<W, ND, true> : pack_il_batch_kernel<W, ND, false>),
+                             dim3(total), dim3(kBlock), 0, s, b, sg);
+        else
+          hipLaunchKernelGGL((unpack_il_batch_kernel<W, ND>), dim3(total), dim3(kBlock), 0, s, b, sg);
+      else if (pack)
+        hipLaunchKernelGGL((wtc ? pack_batch_kernel<W, ND, true> : pack_batch_kernel<W, ND, false>), dim3(total),
+                           dim3(kBlock), 0, s, b, sg);
+      else
+        hipLaunchKernelGGL((wtc ? unpack_batch_kernel<W, ND, kScatterWT> : unpack_batch_kernel<W, ND, false>),
+                           dim3(total), dim3(kBlock), 0, s, b, sg);
     }
     b.nitems = 0;
     total = 0;
