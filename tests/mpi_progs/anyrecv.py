@@ -230,8 +230,10 @@ for label, recipe in SIZES.items():
         mpi.Barrier()
 
 c = mpi.counters()
-print(f"rank {rank} counters ipc={c['send_ipc']} ipc_copy={c['send_ipc_copy']} direct={c['send_direct']} "
-      f"oneshot={c['send_oneshot']} canary_ok={c['canary_ok']} canary_fail={c['canary_fail']}", flush=True)
+# (one write with its newline: the ranks share the launcher's pipe)
+sys.stdout.write(f"rank {rank} counters ipc={c['send_ipc']} ipc_copy={c['send_ipc_copy']} direct={c['send_direct']} "
+                 f"oneshot={c['send_oneshot']} canary_ok={c['canary_ok']} canary_fail={c['canary_fail']}\n")
+sys.stdout.flush()
 mpi.Finalize()
 print(f"RESULT errors={errors}", flush=True)
 sys.exit(1 if errors else 0)

@@ -25,6 +25,20 @@ METHODS = {
 }
 
 
+def _kv_line(out, prefix):
+    """(line, {key: value}) of the key=value line a rank printed after `prefix`;
+    the pairs end at the first token without '=' (another rank's output can
+    land on the same line before its newline)"""
+    line = next(l for l in out.splitlines() if l.startswith(prefix))
+    kv = {}
+    for tok in line[len(prefix):].split():
+        if "=" not in tok:
+            break
+        k, v = tok.split("=", 1)
+        kv[k] = v
+    return line, kv
+
+
 def _json_line(out):
     for line in out.splitlines():
         if line.startswith("{"):
@@ -149,8 +163,7 @@ def test_every_receive_sees_payload(gpu, n, method):
     rc, out = mpi_launch.run(n, mpi_launch.py("anyrecv.py"), env=env, timeout=240)
     assert rc == 0 and "RESULT errors=0" in out, out[-4000:]
     if n == 2 and method == "AUTO":  # the routes the cases are named for were taken
-        line = next(l for l in out.splitlines() if l.startswith("rank 0 counters"))
-        c = dict(kv.split("=") for kv in line.split()[3:])
+        line, c = _kv_line(out, "rank 0 counters")
         assert int(c["ipc"]) > 0 and int(c["ipc_copy"]) > 0 and int(c["oneshot"]) > 0, line
 
 
@@ -176,8 +189,7 @@ def test_cross_gpu_first_contact_canary(gpu, method, fault):
         env["TEMPI_FAULT_CANARY"] = "1"
     rc, out = mpi_launch.run(2, mpi_launch.py("anyrecv.py"), env=env, timeout=240)
     assert rc == 0 and "RESULT errors=0" in out, out[-4000:]
-    line = next(l for l in out.splitlines() if l.startswith("rank 1 counters"))
-    c = dict(kv.split("=") for kv in line.split()[3:])
+    line, c = _kv_line(out, "rank 1 counters")
     assert (int(c["canary_ok"]), int(c["canary_fail"])) == ((0, 1) if fault else (1, 0)), line
 
 
