@@ -14,7 +14,8 @@
  *
  *   symbol           replaces the reference's        TEMPI behaviour
  *   MPI_Init         src/init.cpp:22-65              resolve next MPI, env, GPU
- *   MPI_Init_thread  (not interposed: F8)            same as MPI_Init
+ *   MPI_Init_thread  (not interposed: F8)            as MPI_Init; level capped at SERIALIZED
+ *   MPI_Query_thread (not interposed)                the same capped level
  *   MPI_Finalize     src/finalize.cpp:20-45          drain requests, free pools
  *   MPI_Type_commit  src/type_commit.cpp:16-114      canonicalise + cache
  *   MPI_Type_free    src/type_free.cpp:14-27         drop cache entry first
@@ -102,6 +103,7 @@ extern "C" {
 
 int MPI_Init(int *argc, char ***argv);
 int MPI_Init_thread(int *argc, char ***argv, int required, int *provided);
+int MPI_Query_thread(int *provided);
 int MPI_Finalize(void);
 int MPI_Type_commit(MPI_Datatype *datatype);
 int MPI_Type_free(MPI_Datatype *datatype);

@@ -328,11 +328,40 @@ TEMPI_EXPORT int MPI_Init(int *argc, char ***argv) {
   return rc;
 }
 
+// Thread support. TEMPI's transport keeps unsynchronised process-wide state
+// (the pending launch lists, the board of operations in flight, the library
+// requests it watches: p2p_internal.hpp), so two application threads inside
+// TEMPI at once would race there. TEMPI is safe when the application
+// serialises its MPI calls, and says so: the level the library grants is
+// capped at MPI_THREAD_SERIALIZED, here and in MPI_Query_thread. (The
+// reference only logs the level, /root/reference/src/init.cpp:36-46, and
+// hands back whatever the library granted.) With TEMPI disabled the
+// library's level stands.
+namespace tempi {
+constexpr int kMaxThreadLevel = MPI_THREAD_SERIALIZED;
+int cap_thread_level(int level) { return state.active && level > kMaxThreadLevel ? kMaxThreadLevel : level; }
+} // namespace tempi
+
 TEMPI_EXPORT int MPI_Init_thread(int *argc, char ***argv, int required, int *provided) {
   resolve_next();
   read_environment();
   const int rc = next.MPI_Init_thread(argc, argv, required, provided);
-  if (rc == MPI_SUCCESS) init_after_mpi();
+  if (rc == MPI_SUCCESS) {
+    init_after_mpi();
+    if (provided && *provided != cap_thread_level(*provided)) {
+      if (required > kMaxThreadLevel && state.worldRank == 0)
+        LOG_WARN("MPI_THREAD_MULTIPLE requested: TEMPI provides MPI_THREAD_SERIALIZED (calls into MPI must "
+                 "not overlap; TEMPI_DISABLE=1 keeps the library's level)");
+      *provided = cap_thread_level(*provided);
+    }
+  }
+  return rc;
+}
+
+TEMPI_EXPORT int MPI_Query_thread(int *provided) {
+  resolve_next();
+  const int rc = next.MPI_Query_thread(provided);
+  if (rc == MPI_SUCCESS && provided) *provided = cap_thread_level(*provided);
   return rc;
 }
 

@@ -14,6 +14,7 @@
 #define TEMPI_NEXT_FUNCS(X)                                                    \
   X(MPI_Init)                                                                  \
   X(MPI_Init_thread)                                                           \
+  X(MPI_Query_thread)                                                          \
   X(MPI_Finalize)                                                              \
   X(MPI_Type_commit)                                                           \
   X(MPI_Type_free)                                                             \

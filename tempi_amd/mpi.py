@@ -114,6 +114,19 @@ class MPI:
             self._call("MPI_Init", None, None)
             self.initialized = True
 
+    def Init_thread(self, required):
+        """MPI_Init_thread; returns the level provided"""
+        p = ctypes.c_int(-1)
+        if not self.initialized:
+            self._call("MPI_Init_thread", None, None, int(required), ctypes.byref(p))
+            self.initialized = True
+        return p.value
+
+    def Query_thread(self):
+        p = ctypes.c_int(-1)
+        self._call("MPI_Query_thread", ctypes.byref(p))
+        return p.value
+
     def Finalize(self):
         if self.initialized:
             self._call("MPI_Finalize")

@@ -344,3 +344,14 @@ def test_placement_device(gpu, method):
     rc, out = mpi_launch.run(8, mpi_launch.py("placement.py", "--device"),
                              env={method: "", "TEMPI_FAKE_NODE_SIZE": "4"}, timeout=240)
     assert rc == 0 and "RESULT errors=0" in out, out[-3000:]
+
+
+@pytest.mark.parametrize("n,method", [(1, "AUTO"), (2, "AUTO"), (2, "ONESHOT")])
+def test_serialized_threads_device(gpu, n, method):
+    """MPI_Init_thread(MULTIPLE) under TEMPI provides MPI_THREAD_SERIALIZED;
+    two application threads then take turns with strided device-object
+    Isend / Irecv / Test (each thread's requests in flight while the other
+    thread calls in), 300 rounds each, every byte checked"""
+    rc, out = mpi_launch.run(n, mpi_launch.py("threads.py", "MULTIPLE", "SERIALIZED", "2", "300", "--device"),
+                             env=METHODS[method], timeout=240)
+    assert rc == 0 and out.count("RESULT errors=0") == n, out[-3000:]

@@ -1,0 +1,73 @@
+#!/bin/bash
+# One parameterised GPU session (replaces the per-session gpu_r4_s*.sh
+# scripts of round 4). Usage, on the GPU box:
+#   bash tools/gpu_session.sh STEP [STEP ...]
+# Steps (run in the order given; the session stops at the first failure, so a
+# GPU fault, abort or time limit never has a second GPU step behind it):
+#   tests        the whole -m gpu suite in the driver's form (-x, one process)
+#   focus        only the tests FOCUS="-k expr" selects
+#   bench        the driver's N=1 bench line (tools/gpu_bench_n1.sh)
+#   prof         rocprofv3 kernel-trace stats + FETCH_SIZE / WRITE_SIZE passes
+#                of the headline (tools/gpu_prof.sh)
+#   halo         halo_exchange 10 512 at RANKS (default "1 2") ranks, both forms
+#   halo-trace   kernel + HIP API trace of the 1-rank halo (tools/halo_trace_summary.py)
+#   sweep-pmc    FETCH_SIZE / WRITE_SIZE passes over SHAPES (tools/sweep_pmc.sh)
+#   measure      measure_system --quick at 2 ranks into gpurun_out/perf_quick.json
+#   torchrun     the driver's torchrun command at NS (default "2") ranks
+#   n8           the driver's torchrun command at 8 ranks (tools/gpu_n8.sh)
+#   kab          kernel A/B: tools/kab.sh $KAB_OUT $KAB_ROUNDS $KAB_ITERS $KAB_SHAPES
+set -o pipefail
+cd "$(dirname "$0")/.."
+O=gpurun_out
+mkdir -p $O
+export TMPDIR=/tmp HYDRA_LAUNCHER=fork
+MPIEXEC=/opt/conda/bin/mpiexec
+for step in "$@"; do
+  echo "== $step $(date +%T)"
+  case $step in
+  tests)
+    timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 250 --timeout-method thread \
+      > $O/gpu_tests.log 2>&1
+    rc=$?; tail -n 3 $O/gpu_tests.log; [ $rc -eq 0 ] || exit $rc ;;
+  focus)
+    timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread $FOCUS \
+      > $O/gpu_focus.log 2>&1
+    rc=$?; tail -n 15 $O/gpu_focus.log; [ $rc -eq 0 ] || exit $rc ;;
+  bench)
+    bash tools/gpu_bench_n1.sh || exit 5 ;;
+  prof)
+    bash tools/gpu_prof.sh || exit 7 ;;
+  halo)
+    rm -f $O/halo.jsonl
+    for n in ${RANKS:-1 2}; do
+      for mode in "" "--neighbor"; do
+        timeout -k 10 300 $MPIEXEC -n $n tempi_amd/lib/halo_exchange 10 512 $mode >> $O/halo.jsonl 2>> $O/halo.err || exit 9
+      done
+    done
+    cat $O/halo.jsonl ;;
+  halo-trace)
+    rm -rf $O/halo_trace
+    timeout -k 10 200 rocprofv3 --kernel-trace --hip-trace --marker-trace --output-format csv -d $O/halo_trace -o run \
+      -- tempi_amd/lib/halo_exchange 10 512 $HALO_ARGS > $O/halo_trace.log 2>&1 || exit 10
+    grep '^{' $O/halo_trace.log
+    python3 tools/halo_trace_summary.py $O/halo_trace > $O/halo_trace_summary.txt 2>&1 || exit 11
+    cat $O/halo_trace_summary.txt ;;
+  sweep-pmc)
+    bash tools/sweep_pmc.sh || exit 12 ;;
+  measure)
+    rm -f $O/perf_quick.json
+    timeout -k 10 400 $MPIEXEC -n 2 tempi_amd/lib/measure_system --quick --out $O/perf_quick.json \
+      > $O/measure.log 2>&1 || exit 13
+    tail -n 2 $O/measure.log ;;
+  torchrun)
+    bash tools/gpu_torchrun.sh || exit 14 ;;
+  n8)
+    bash tools/gpu_n8.sh || exit 15 ;;
+  kab)
+    bash tools/kab.sh $KAB_OUT ${KAB_ROUNDS:-3} ${KAB_ITERS:-20} $KAB_SHAPES || exit 16
+    python3 tools/kab_summary.py $O/$KAB_OUT 2>&1 | tail -40 ;;
+  *)
+    echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "== done $(date +%T)"
