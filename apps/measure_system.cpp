@@ -18,6 +18,10 @@
 // samples pass the SP 800-90B permutation test (tempi_sp800_90b_iid) or 3
 // trials elapse; the stored time is the trimean.
 //
+// With no GPU visible only the host curves (intraNodeCpuCpuPingpong or
+// interNodeCpuCpuPingpong) are measured; the GPU curves stay empty, which the
+// model reads as "unknown" (+inf), so AUTO then prices only what was measured.
+//
 // usage: mpiexec -n 2 measure_system [--out FILE] [--quick]
 #include <hip/hip_runtime.h>
 #include <mpi.h>
@@ -118,8 +122,9 @@ int main(int argc, char **argv) {
     if (!std::strcmp(argv[i], "--quick")) quick = true;
   }
   int ndev = 0;
-  HIPCHECK(hipGetDeviceCount(&ndev));
-  HIPCHECK(hipSetDevice(rank % ndev));
+  if (hipGetDeviceCount(&ndev) != hipSuccess) ndev = 0;
+  const bool gpu = ndev > 0;
+  if (gpu) HIPCHECK(hipSetDevice(rank % ndev));
   const int maxLog = quick ? 20 : 23;
 
   // node placement of ranks 0 and 1
@@ -144,14 +149,16 @@ int main(int argc, char **argv) {
   const int maxTableLog = quick ? 18 : 22;
   const size_t tableExtent = ((size_t(1) << maxTableLog) - 1) * 512 + 1;
   const size_t devBytes = std::max(4 * maxBytes, tableExtent);
-  char *dev, *dev2, *host;
-  HIPCHECK(hipMalloc(&dev, devBytes));
-  HIPCHECK(hipMalloc(&dev2, 4 * maxBytes));
-  HIPCHECK(hipMemset(dev, 0, devBytes));
-  HIPCHECK(hipHostMalloc(reinterpret_cast<void **>(&host), 4 * maxBytes, hipHostMallocMapped));
+  char *dev = nullptr, *dev2 = nullptr, *host = nullptr;
+  if (gpu) {
+    HIPCHECK(hipMalloc(&dev, devBytes));
+    HIPCHECK(hipMalloc(&dev2, 4 * maxBytes));
+    HIPCHECK(hipMemset(dev, 0, devBytes));
+    HIPCHECK(hipHostMalloc(reinterpret_cast<void **>(&host), 4 * maxBytes, hipHostMallocMapped));
+  }
   std::vector<char> pageable(maxBytes);
 
-  if (rank == 0) {
+  if (rank == 0 && gpu) {
     launch = measure([&] {
       const double t0 = MPI_Wtime();
       hipLaunchKernelGGL(empty_kernel, dim3(1), dim3(1), 0, 0);
@@ -220,11 +227,11 @@ int main(int argc, char **argv) {
     MPI_Comm pair;
     MPI_Comm_split(MPI_COMM_WORLD, rank < 2 ? 0 : MPI_UNDEFINED, rank, &pair);
     if (rank < 2) {
-      for (int gpu = 0; gpu < 2; ++gpu) {
-        if (gpu) tempi_set_datatype_method(4); // IPC: this build's DEVICE path
+      for (int onGpu = 0; onGpu < (gpu ? 2 : 1); ++onGpu) {
+        if (onGpu) tempi_set_datatype_method(4); // IPC: this build's DEVICE path
         for (int i = 0; i <= maxLog; ++i) {
           const int n = 1 << i;
-          char *buf = gpu ? dev : pageable.data();
+          char *buf = onGpu ? dev : pageable.data();
           Point p = measure(
               [&] {
                 MPI_Barrier(pair);
@@ -239,7 +246,7 @@ int main(int argc, char **argv) {
                 return (MPI_Wtime() - t0) / 2;
               },
               pair);
-          (gpu ? gpuPP : cpuPP).push_back(p);
+          (onGpu ? gpuPP : cpuPP).push_back(p);
         }
         tempi_set_datatype_method(0);
       }
@@ -248,7 +255,9 @@ int main(int argc, char **argv) {
   }
 
   if (rank == 0) {
-    std::string doc = "{\n  \"cudaKernelLaunch\": " + std::to_string(launch);
+    char launchText[32]; // %.9g: std::to_string keeps 6 decimals, 0.00001 for a 10.4 us launch
+    std::snprintf(launchText, sizeof launchText, "%.9g", launch);
+    std::string doc = "{\n  \"cudaKernelLaunch\": " + std::string(launchText);
     doc += ",\n  \"d2h\": " + curve_json(d2h) + ",\n  \"h2d\": " + curve_json(h2d);
     doc += ",\n  \"intraNodeCpuCpuPingpong\": " + curve_json(colocated ? cpuPP : std::vector<Point>());
     doc += ",\n  \"intraNodeGpuGpuPingpong\": " + curve_json(colocated ? gpuPP : std::vector<Point>());
@@ -276,12 +285,14 @@ int main(int argc, char **argv) {
     }
     std::fputs(doc.c_str(), f);
     std::fclose(f);
-    std::printf("{\"perf_json\": \"%s\", \"colocated\": %s, \"launch_us\": %.2f}\n", out.c_str(),
-                colocated ? "true" : "false", launch * 1e6);
+    std::printf("{\"perf_json\": \"%s\", \"colocated\": %s, \"gpu\": %s, \"launch_us\": %.3f}\n", out.c_str(),
+                colocated ? "true" : "false", gpu ? "true" : "false", launch * 1e6);
   }
-  HIPCHECK(hipFree(dev));
-  HIPCHECK(hipFree(dev2));
-  HIPCHECK(hipHostFree(host));
+  if (gpu) {
+    HIPCHECK(hipFree(dev));
+    HIPCHECK(hipFree(dev2));
+    HIPCHECK(hipHostFree(host));
+  }
   MPI_Finalize();
   return 0;
 }

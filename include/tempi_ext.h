@@ -99,6 +99,14 @@ int tempi_perf_roundtrip(const char *json_in, char *json_out, int cap);
    3 STAGED, 4 IPC (used by tools/measure_system) */
 void tempi_set_datatype_method(int method);
 
+/* the route TEMPI takes for a strided message of `bytes` packed bytes in
+   `block`-byte blocks to a co-located (1) or off-node (0) peer, blocking (1)
+   or non-blocking (0), under the current TEMPI_DATATYPE_* choice: 1 ONESHOT,
+   2 DEVICE, 3 STAGED, 4 IPC (0 before MPI_Init); *from_model = 1 when AUTO
+   priced it with the loaded perf.json (/root/reference/src/internal/
+   sender.cpp:251-290), 0 when the built-in policy decided */
+int tempi_choose_method(int64_t bytes, int64_t block, int colocated, int blocking, int *from_model);
+
 /* NIST SP 800-90B sec. 5.1 permutation test: 1 when `samples` look IID
    (tools/measure_system repeats a measurement until they do) */
 int tempi_sp800_90b_iid(const double *samples, int n, int perms, uint64_t seed);

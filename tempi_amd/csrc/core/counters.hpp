@@ -18,7 +18,7 @@ struct Counters {
   uint64_t staged_packs = 0, staged_unpacks = 0;
   // synchronous MPI_Pack / MPI_Unpack completed by a ticket (device memory or
   // TEMPI's coherent slab written) or by hipStreamSynchronize (the
-  // application's pinned host memory written, or TEMPI_STREAM_SYNC)
+  // application's pinned host memory written)
   uint64_t ticket_waits = 0, sync_waits = 0;
   uint64_t ticket_batches = 0; // transport batches completed by a ticket their last launch stored
   uint64_t persistent_starts = 0; // MPI_Start of a TEMPI persistent request

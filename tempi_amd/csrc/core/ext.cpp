@@ -118,7 +118,7 @@ TEMPI_EXPORT int64_t tempi_mpi_constant(const char *name, int *found) {
       H(MPI_REQUEST_NULL), H(MPI_ORDER_C), H(MPI_ORDER_FORTRAN), H(MPI_ANY_SOURCE), H(MPI_ANY_TAG),
       H(MPI_PROC_NULL), H(MPI_SUM), H(MPI_MAX), H(MPI_MIN), H(MPI_THREAD_SINGLE),
       H(MPI_THREAD_FUNNELED), H(MPI_THREAD_SERIALIZED), H(MPI_THREAD_MULTIPLE),
-      H(MPI_MAX_PROCESSOR_NAME), H(MPI_UNDEFINED), H(MPI_BSEND_OVERHEAD), H(MPI_ERR_REQUEST),
+      H(MPI_MAX_PROCESSOR_NAME), H(MPI_UNDEFINED), H(MPI_BSEND_OVERHEAD), H(MPI_ERR_REQUEST), H(MPI_ERR_IN_STATUS),
       P(MPI_STATUS_IGNORE), P(MPI_STATUSES_IGNORE), P(MPI_IN_PLACE), P(MPI_UNWEIGHTED), P(MPI_WEIGHTS_EMPTY), H(MPI_INFO_NULL),
       H(MPI_ERRORS_RETURN), H(MPI_ERRORS_ARE_FATAL), H(MPI_MESSAGE_NULL), H(MPI_MESSAGE_NO_PROC),
       {"sizeof(MPI_Message)", int64_t(sizeof(MPI_Message))},
@@ -188,6 +188,13 @@ TEMPI_EXPORT void tempi_set_datatype_method(int m) {
   static const DatatypeMethod map[] = {DatatypeMethod::AUTO, DatatypeMethod::ONESHOT, DatatypeMethod::DEVICE,
                                        DatatypeMethod::STAGED, DatatypeMethod::IPC};
   if (m >= 0 && m < 5) env.datatype = map[m];
+}
+
+TEMPI_EXPORT int tempi_choose_method(int64_t bytes, int64_t block, int colocated, int blocking, int *from_model) {
+  bool fm = false;
+  const int m = state.active ? p2p::query_method(bytes, block, colocated != 0, blocking != 0, &fm) : 0;
+  if (from_model) *from_model = fm ? 1 : 0;
+  return m;
 }
 
 // ---- rank placement (core/placement.hpp)

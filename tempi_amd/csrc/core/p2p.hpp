@@ -27,7 +27,8 @@
 //            strided with one kernel (no packed intermediate); a send waited
 //            on before its receive is posted falls back to a gathered slab.
 //            TEMPI_NO_DIRECT disables it
-//   AUTO     IPC for co-located peers at >= TEMPI_IPC_MIN_BYTES (4 KiB),
+//   AUTO     blocking sends: the cheapest method the perf model prices
+//            (perf.json); otherwise IPC for co-located peers at >= 4 KiB,
 //            ONESHOT otherwise (with no perf.json the reference would stop
 //            here with LOG_FATAL: SURVEY F10)
 // Receives are adaptive: a TEMPI device receive lands in pinned host memory
@@ -52,6 +53,9 @@ void init();
 void finalize();
 // re-read the perf model (after measure_system wrote this node's perf.json)
 void reload_perf_model();
+// the route a strided message would take (tempi_choose_method): 1 ONESHOT,
+// 2 DEVICE, 3 STAGED, 4 IPC; *fromModel set when the perf model decided
+int query_method(int64_t bytes, int64_t block, bool colocated, bool blocking, bool *fromModel);
 
 // what handles() found out, handed on to isend / irecv
 struct Route {

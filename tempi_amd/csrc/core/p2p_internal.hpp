@@ -267,7 +267,7 @@ extern std::deque<std::shared_ptr<GpuBatch>> batches; // launch order
 struct PersistentOp; // p2p_persistent.cpp
 
 struct Op {
-  virtual ~Op() {}
+  virtual ~Op() { settle_buffered(); }
   virtual PersistentOp *persistent() { return nullptr; }
   static void *operator new(size_t n) { return op_pool().allocate(n, alignof(std::max_align_t)); }
   // (virtual destructor: `n` is the size of the object's dynamic type)
@@ -291,6 +291,12 @@ struct Op {
   MPI_Comm errComm = MPI_COMM_NULL;            // whose error handler the wait raises it on
   int boardSlot = -1;                          // waiting for an ack in this board slot (boardOps)
   virtual void acked(int) {}                   // that ack arrived with this code
+  // a buffered-mode send counts in bufferedUnposted (MPI_Buffer_detach waits
+  // for it) from construction until its post() -- or its destruction, should
+  // it never be posted, so that the detach cannot wait forever
+  bool unpostedBuffered = false;
+  void count_buffered();
+  void settle_buffered();
 };
 
 // a library post of the application's message that the library refused

@@ -166,6 +166,16 @@ void PendingList::add_items(const Op *op, const Packer &pk, void *packed, const 
 
 PendingList pendingPack, pendingUnpack;
 int64_t bufferedUnposted = 0;
+
+void Op::count_buffered() {
+  if (!unpostedBuffered) ++bufferedUnposted;
+  unpostedBuffered = true;
+}
+
+void Op::settle_buffered() {
+  if (unpostedBuffered) --bufferedUnposted;
+  unpostedBuffered = false;
+}
 int scattersInFlight = 0;
 
 namespace {
@@ -291,7 +301,7 @@ struct IsendOp : Op {
       : rec(r->ref()), origin(o), count(c), dest(de), tag(t), dt(d), comm(cm), method(m), bytes(b),
         key(gate_key(cm, de)), mode(md) {
     device = dev;
-    if (mode == SendMode::BUFFERED) ++bufferedUnposted;
+    if (mode == SendMode::BUFFERED) count_buffered();
     gate_enter(key, this);
     if (method == Method::ONESHOT) {
       hslab = pinned_pool().get(size_t(bytes), device);
@@ -320,7 +330,7 @@ struct IsendOp : Op {
     lib_done(MPI_Status{});
   }
   void post() override {
-    if (mode == SendMode::BUFFERED) --bufferedUnposted;
+    settle_buffered();
     int rc = MPI_SUCCESS;
     switch (method) {
     case Method::ONESHOT:
@@ -463,7 +473,7 @@ struct IsendDirectOp : Op {
     if (s != MPI_STATUS_IGNORE) {
       s->MPI_SOURCE = MPI_ANY_SOURCE;
       s->MPI_TAG = MPI_ANY_TAG;
-      s->MPI_ERROR = MPI_SUCCESS;
+      s->MPI_ERROR = err; // set by fail_post when the library refused the post
       MPI_Status_set_elements(s, MPI_BYTE, 0);
     }
   }
@@ -572,7 +582,7 @@ struct IsendCopyOp : Op {
     if (s != MPI_STATUS_IGNORE) {
       s->MPI_SOURCE = MPI_ANY_SOURCE;
       s->MPI_TAG = MPI_ANY_TAG;
-      s->MPI_ERROR = MPI_SUCCESS;
+      s->MPI_ERROR = err; // set by fail_post when the library refused the post
       MPI_Status_set_elements(s, MPI_BYTE, 0);
     }
   }
@@ -590,11 +600,11 @@ struct LibIsendOp : Op {
       : dt(d), dest(de), tag(t), comm(cm), mode(md) {
     buf.resize(size_t(std::max<int64_t>(pack_size(c, d, comm), 1)));
     tempi::pack(b, c, d, buf.data(), int(buf.size()), &n, comm);
-    if (mode == SendMode::BUFFERED) ++bufferedUnposted;
+    if (mode == SendMode::BUFFERED) count_buffered();
     post_or_queue(gate_key(comm, dest), this);
   }
   void post() override {
-    if (mode == SendMode::BUFFERED) --bufferedUnposted;
+    settle_buffered();
     const int rc = lib_isend(mode, buf.data(), n, MPI_PACKED, dest, tag, comm, &lib);
     if (rc == MPI_SUCCESS) {
       watch(this);
@@ -634,7 +644,7 @@ struct HostIsendOp : Op {
   void lib_done(const MPI_Status &) override { done = true; }
   void status(MPI_Status *s) const override {
     if (s != MPI_STATUS_IGNORE) {
-      s->MPI_ERROR = MPI_SUCCESS;
+      s->MPI_ERROR = err; // set by fail_post when the library refused the post
       MPI_Status_set_elements(s, MPI_BYTE, 0);
     }
   }
@@ -655,7 +665,7 @@ struct LocalCopyOp : Op {
     if (s != MPI_STATUS_IGNORE) {
       s->MPI_SOURCE = state.worldRank;
       s->MPI_TAG = MPI_ANY_TAG;
-      s->MPI_ERROR = MPI_SUCCESS;
+      s->MPI_ERROR = err; // set by fail_post when the library refused the post
       set_received(s, bytes);
     }
   }

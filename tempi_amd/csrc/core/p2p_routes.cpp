@@ -53,7 +53,7 @@ std::unordered_map<uintptr_t, Export> ipcExports;
 bool ipcCopyEnabled = true;             // TEMPI_NO_IPC_COPY
 // Inside MPI_Alltoallv every receive is posted before any send is waited on,
 // so a rendezvous send cannot deadlock there: IPC COPY takes messages of any
-// size (TEMPI_NO_COLL_COPY keeps the point-to-point threshold)
+// size there. Point-to-point, it takes messages
 // above MPICH's own eager limit (MPIR_CVAR_CH3_EAGER_MAX_MSG_SIZE, 128 KiB):
 // a program that works with the library's rendezvous works with this one
 int64_t ipcCopyMinBytes = 128 * 1024 + 1; // TEMPI_IPC_COPY_MIN_BYTES
@@ -168,6 +168,27 @@ Method choose(int64_t bytes, bool colocated, bool blocking) {
 }
 
 void clear_model_cache() { modelCache.clear(); }
+
+} // namespace detail
+
+int query_method(int64_t bytes, int64_t block, bool colocated, bool blocking, bool *fromModel) {
+  using namespace detail;
+  Method m;
+  const int64_t keep = modelBlock;
+  modelBlock = block;
+  *fromModel = env.datatype == DatatypeMethod::AUTO && blocking && model_choice(bytes, colocated, block, &m);
+  m = choose(bytes, colocated, blocking);
+  modelBlock = keep;
+  switch (m) {
+  case Method::ONESHOT: return 1;
+  case Method::DEVICE: return 2;
+  case Method::STAGED: return 3;
+  case Method::IPC: return 4;
+  default: return 0;
+  }
+}
+
+namespace detail {
 
 namespace {
 // peers whose memory could not be mapped: no more IPC to or from them

@@ -423,6 +423,17 @@ class MPI:
         self._call("MPI_Waitall", n, arr, self.STATUSES_IGNORE)
         return list(arr)[:n]
 
+    def Waitall_errors(self, reqs):
+        """MPI_Waitall with statuses, not raising: (return code, [MPI_ERROR
+        of each status])"""
+        n = len(reqs)
+        arr = (self.Request * max(n, 1))(*reqs)
+        sts = (ctypes.c_char * (self.status_size * max(n, 1)))()
+        rc = self.L.MPI_Waitall(n, arr, sts)
+        off = self.const("offsetof(MPI_Status,MPI_ERROR)")
+        errs = [ctypes.c_int.from_buffer(sts, k * self.status_size + off).value for k in range(n)]
+        return rc, errs
+
     def _reqs(self, reqs):
         return (self.Request * max(len(reqs), 1))(*reqs)
 
@@ -623,6 +634,10 @@ class MPI:
         c = Counters()
         self.L.tempi_get_counters(ctypes.byref(c))
         return {n: getattr(c, n) for n in _COUNTER_FIELDS}
+
+    def set_datatype_method(self, m):
+        """tempi_set_datatype_method: 0 AUTO, 1 ONESHOT, 2 DEVICE, 3 STAGED, 4 IPC"""
+        self.L.tempi_set_datatype_method(int(m))
 
     def reset_counters(self):
         self.L.tempi_reset_counters()

@@ -225,6 +225,48 @@ except tempi_amd.mpi.MPIError:
     pass
 mpi.Barrier()
 
+# a host send queued behind a device send that is still
+# gathering to the same peer (TEMPI's HostIsendOp) whose post the library
+# refuses (a negative tag): MPI_Waitall returns MPI_ERR_IN_STATUS, the
+# refused request's status carries the library's error, the device send's
+# MPI_SUCCESS, and the device message still arrives. ONESHOT gathers 16 MiB
+# into pinned host memory (milliseconds), so the gate is still closed when
+# the host send is posted. (Two ranks or more: a send to itself may be
+# matched by the self channel instead of gathering.)
+if device and size >= 2:
+    big_recipe = "vector(65536,256,512,byte)"
+    bt, btemps, bbasic = typezoo.build(mpi, big_recipe)
+    btm = pyoracle.TypeMap(big_recipe)
+    borigin, blen = btm.geometry(1)
+    bsrc = torch.from_numpy(np.random.default_rng(4000 + rank).integers(0, 256, blen, dtype=np.uint8)).cuda()
+    bdst = torch.zeros(blen, dtype=torch.uint8, device="cuda")
+    hb = np.zeros(64, dtype=np.uint8)
+    torch.cuda.synchronize()
+    mpi.set_datatype_method(1)  # ONESHOT
+    r = mpi.Irecv(bdst.data_ptr() + borigin, 1, bt, src, 64)
+    mpi.Barrier()
+    c0 = mpi.counters()["lib_sends"]
+    s_dev = mpi.Isend(bsrc.data_ptr() + borigin, 1, bt, peer, 64)
+    try:
+        s_host = mpi.Isend(hb.ctypes.data, 64, mpi.BYTE, peer, -5)
+    except tempi_amd.mpi.MPIError:
+        s_host = None
+        fail("the host send behind a gathering send was refused at the call, not queued")
+    if s_host is not None:
+        rc, errs = mpi.Waitall_errors([s_dev, s_host])
+        if rc != mpi.const("MPI_ERR_IN_STATUS") or errs[0] != mpi.SUCCESS or errs[1] == mpi.SUCCESS:
+            fail(f"queued host send refused by the library: Waitall rc {rc}, status errors {errs}")
+    mpi.Wait(r)
+    exp = btm.pack(np.random.default_rng(4000 + src).integers(0, 256, blen, dtype=np.uint8), borigin, 1)
+    got = btm.pack(bdst.cpu().numpy(), borigin, 1)
+    if not np.array_equal(got, exp):
+        fail("the device send beside a refused host send did not arrive intact")
+    forced = [k for k, v in (("ONESHOT", 1), ("DEVICE", 2), ("STAGED", 3), ("IPC", 4))
+              if "TEMPI_DATATYPE_" + k in os.environ]
+    mpi.set_datatype_method({"ONESHOT": 1, "DEVICE": 2, "STAGED": 3, "IPC": 4}[forced[0]] if forced else 0)
+    typezoo.free(mpi, bt, btemps, bbasic)
+    mpi.Barrier()
+
 # MPI_Sendrecv_replace whose receive side is MPI_PROC_NULL: the send of the
 # (device) object still goes through TEMPI (it used to reach the
 # library, which cannot read GPU memory), and the object is left as it was

@@ -132,3 +132,23 @@ def test_mpi_isend_host(mode, ranks):
     assert rc == 0 and len(recs) == 3 and all(r["errors"] == 0 and r["checked"] for r in recs), out[-3000:]
     assert all(r["tags"] == 10 and r["buffers"] == "host" for r in recs)
 
+
+
+def test_measure_system_host_curves(tmp_path):
+    """apps/measure_system (the perf.json writer, /root/reference/src/internal/
+    measure_system.cu:377-606) at 2 ranks without a GPU: the host ping-pong
+    curve over 2^0 .. 2^20 bytes with IID flags, the GPU curves empty; the
+    file round-trips through TEMPI's parser, and TEMPI then loads it from
+    TEMPI_CACHE_DIR -- with no GPU curves AUTO keeps its built-in policy"""
+    from tests import perf_json_check
+
+    out = tmp_path / "perf.json"
+    rc, log = mpi_launch.run(2, [os.path.join(LIB, "measure_system"), "--quick", "--out", str(out)], timeout=200)
+    assert rc == 0 and '"gpu": false' in log, log[-3000:]
+    doc, bad = perf_json_check.check(str(out), gpu=False)
+    assert not bad, bad[:10]
+    rc, log = mpi_launch.run(1, mpi_launch.py("perf_pick.py"), env={"TEMPI_CACHE_DIR": str(tmp_path)}, timeout=120)
+    assert rc == 0, log[-3000:]
+    pick = json.loads(next(l for l in log.splitlines() if l.startswith("{")))
+    assert pick["loaded"] == 1 and pick["source"] == str(out), pick
+    assert all(fm == 0 for _, _, _, fm in pick["picks"]), pick  # no GPU curve priced

@@ -355,3 +355,27 @@ def test_serialized_threads_device(gpu, n, method):
     rc, out = mpi_launch.run(n, mpi_launch.py("threads.py", "MULTIPLE", "SERIALIZED", "2", "300", "--device"),
                              env=METHODS[method], timeout=240)
     assert rc == 0 and out.count("RESULT errors=0") == n, out[-3000:]
+
+
+def test_measure_system_writes_a_model_auto_uses(gpu, tmp_path):
+    """VERDICT r04 next 2 (row a12): apps/measure_system --quick at 2 ranks
+    (the perf.json writer, /root/reference/src/internal/measure_system.cu:
+    377-606) writes the reference's schema with finite, positive, IID-flagged
+    times -- d2h / h2d / both intra-node ping-pongs over 2^0 .. 2^20 bytes,
+    packDevice / unpackDevice / packHost / unpackHost rows of 2^(2i+6) bytes x
+    2^j-byte blocks, the launch time with sub-microsecond digits -- and a
+    fresh process given that TEMPI_CACHE_DIR loads it and has AUTO price
+    blocking sends with it"""
+    from tests import perf_json_check
+
+    out = tmp_path / "perf.json"
+    rc, log = mpi_launch.run(2, [os.path.join(LIB, "measure_system"), "--quick", "--out", str(out)], timeout=240)
+    assert rc == 0 and '"gpu": true' in log, log[-3000:]
+    doc, bad = perf_json_check.check(str(out), gpu=True)
+    assert not bad, bad[:10]
+    rc, log = mpi_launch.run(1, mpi_launch.py("perf_pick.py"), env={"TEMPI_CACHE_DIR": str(tmp_path)}, timeout=120)
+    assert rc == 0, log[-3000:]
+    pick = json.loads(next(l for l in log.splitlines() if l.startswith("{")))
+    assert pick["loaded"] == 1 and pick["source"] == str(out), pick
+    colocated = [p for p in pick["picks"] if p[1] == 1]
+    assert all(fm == 1 and m in (1, 3, 4) for _, _, m, fm in colocated), pick  # ONESHOT / STAGED / IPC, priced

@@ -5,7 +5,7 @@
 # Steps (run in the order given; the session stops at the first failure, so a
 # GPU fault, abort or time limit never has a second GPU step behind it):
 #   tests        the whole -m gpu suite in the driver's form (-x, one process)
-#   focus        only the tests FOCUS="-k expr" selects
+#   focus        only the tests FOCUS (a pytest -k expression) selects
 #   bench        the driver's N=1 bench line (tools/gpu_bench_n1.sh)
 #   prof         rocprofv3 kernel-trace stats + FETCH_SIZE / WRITE_SIZE passes
 #                of the headline (tools/gpu_prof.sh)
@@ -30,7 +30,7 @@ for step in "$@"; do
       > $O/gpu_tests.log 2>&1
     rc=$?; tail -n 3 $O/gpu_tests.log; [ $rc -eq 0 ] || exit $rc ;;
   focus)
-    timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread $FOCUS \
+    timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread -k "$FOCUS" \
       > $O/gpu_focus.log 2>&1
     rc=$?; tail -n 15 $O/gpu_focus.log; [ $rc -eq 0 ] || exit $rc ;;
   bench)
