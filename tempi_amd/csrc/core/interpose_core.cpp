@@ -169,6 +169,7 @@ void finalize_before_mpi() {
                                << counters.lib_packs << " sends=" << counters.sends);
   types_finalize();
   gpu::finalize();
+  trace::finalize(state.worldRank);
   state.active = false;
 }
 

@@ -25,23 +25,74 @@ namespace tempi {
 namespace p2p {
 namespace detail {
 namespace {
-uint32_t nextHandle = 1;
-std::pmr::unordered_map<uint32_t, std::unique_ptr<Op>> active{&op_pool()};
-std::vector<uint32_t> detachedOps; // freed by the application, still running
+// The operations in flight, by request handle. Handles are handed out in
+// sequence (mod kHandleSpace, never 0) and the table is direct-mapped: handle
+// h lives in slot h & mask, so finding a request is one index and one compare
+// (a halo substep waits on 416 requests, most of them already complete: three
+// hash lookups each were a third of its tail, profiles/r05/halo_tl*). A
+// handle whose slot is still taken by an older operation is skipped; the
+// table doubles when half full (entries never collide after doubling: equal
+// low bits under the new mask would mean equal slots under the old one).
+class OpTable {
+  struct Slot {
+    uint32_t h = 0;
+    std::unique_ptr<Op> op;
+  };
+  std::vector<Slot> slots_ = std::vector<Slot>(4096);
+  size_t mask_ = 4095, n_ = 0;
 
-bool handlesWrapped = false; // once the counter has wrapped, skip handles still in use
+  void grow() {
+    std::vector<Slot> old(slots_.size() * 2);
+    old.swap(slots_);
+    mask_ = slots_.size() - 1;
+    for (Slot &s : old)
+      if (s.op) slots_[s.h & mask_] = std::move(s);
+  }
+
+public:
+  Op *get(uint32_t h) const {
+    const Slot &s = slots_[h & mask_];
+    return h && s.h == h ? s.op.get() : nullptr;
+  }
+  bool slot_free(uint32_t h) const { return !slots_[h & mask_].op; }
+  void put(uint32_t h, std::unique_ptr<Op> op) {
+    if (2 * (n_ + 1) > slots_.size()) grow();
+    Slot &s = slots_[h & mask_];
+    s.h = h;
+    s.op = std::move(op);
+    ++n_;
+  }
+  // the slot is cleared before the operation is destroyed (a destructor may
+  // free or add other requests)
+  void erase(uint32_t h) {
+    Slot &s = slots_[h & mask_];
+    if (!h || s.h != h || !s.op) return;
+    std::unique_ptr<Op> dead = std::move(s.op);
+    s.h = 0;
+    --n_;
+  }
+  size_t size() const { return n_; }
+  bool all_done() const {
+    for (const Slot &s : slots_)
+      if (s.op && !s.op->done) return false;
+    return true;
+  }
+  void clear() {
+    std::vector<Slot> old(slots_.size());
+    old.swap(slots_);
+    n_ = 0;
+  }
+};
+OpTable active;
+uint32_t nextHandle = 1;
+std::vector<uint32_t> detachedOps; // freed by the application, still running
 } // namespace
 
 MPI_Request add(std::unique_ptr<Op> op) {
-  if (handlesWrapped)
-    while (active.count(nextHandle) || nextHandle == 0) nextHandle = (nextHandle + 1) % kHandleSpace;
-  const uint32_t h = nextHandle;
-  nextHandle = (nextHandle + 1) % kHandleSpace;
-  if (nextHandle == 0) {
-    nextHandle = 1;
-    handlesWrapped = true;
-  }
-  active.emplace(h, std::move(op));
+  uint32_t h = nextHandle;
+  while (h == 0 || !active.slot_free(h)) h = (h + 1) % kHandleSpace; // (a free slot holds no live handle)
+  nextHandle = (h + 1) % kHandleSpace;
+  active.put(h, std::move(op));
   return MPI_Request(h);
 }
 
@@ -74,7 +125,6 @@ void init() {
   scattersInFlight = 0;
   directShared.clear();
   directShared.reserve(512);
-  active.reserve(2048);
   systemPerformanceLoaded = import_system_performance(&systemPerformance);
   clear_model_cache();
   MPI_Comm_dup(MPI_COMM_WORLD, &ctrlComm);
@@ -95,11 +145,7 @@ void finalize() {
   // complete everything the application left behind, then wait (bounded) for
   // the acks that let us release IPC slabs
   const auto t0 = std::chrono::steady_clock::now();
-  auto all_done = [] {
-    for (auto &kv : active)
-      if (!kv.second->done) return false;
-    return true;
-  };
+  auto all_done = [] { return active.all_done(); };
   while (!all_done()) {
     progress();
     if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(30)) {
@@ -313,56 +359,54 @@ void drain_buffered() {
 
 bool is_tempi_request(MPI_Request r) {
   const uint32_t h = uint32_t(r);
-  return h != 0 && h < kHandleSpace && active.count(h);
+  return h < kHandleSpace && active.get(h) != nullptr;
 }
 
 namespace detail {
 Op *find_op(MPI_Request r) {
   const uint32_t h = uint32_t(r);
-  if (h == 0 || h >= kHandleSpace) return nullptr;
-  auto it = active.find(h);
-  return it == active.end() ? nullptr : it->second.get();
+  return h < kHandleSpace ? active.get(h) : nullptr;
 }
 } // namespace detail
 
 bool peek(MPI_Request r) {
-  auto it = active.find(uint32_t(r));
-  if (it == active.end()) return false;
-  if (PersistentOp *p = it->second->persistent()) return persistent_peek(p);
-  return it->second->done;
+  Op *op = find_op(r);
+  if (!op) return false;
+  if (PersistentOp *p = op->persistent()) return persistent_peek(p);
+  return op->done;
 }
 
 void release(MPI_Request *req) {
-  auto it = active.find(uint32_t(*req));
-  if (it != active.end()) {
-    if (PersistentOp *p = it->second->persistent()) {
+  const uint32_t h = uint32_t(*req);
+  if (Op *op = find_op(*req)) {
+    if (PersistentOp *p = op->persistent()) {
       persistent_free(p);
-      active.erase(uint32_t(*req)); // (the iterator may have moved: freeing the inner request touched the table)
-    } else if (it->second->done) {
-      active.erase(it);
+      active.erase(h);
+    } else if (op->done) {
+      active.erase(h);
     } else {
-      it->second->detached = true;
-      detachedOps.push_back(uint32_t(*req));
+      op->detached = true;
+      detachedOps.push_back(h);
     }
   }
   *req = MPI_REQUEST_NULL;
 }
 
 int get_status(MPI_Request r, int *flag, MPI_Status *status) {
-  auto it = active.find(uint32_t(r));
-  if (it == active.end()) return next.MPI_Request_get_status(r, flag, status);
-  if (PersistentOp *p = it->second->persistent()) return persistent_get_status(p, flag, status);
+  Op *op = find_op(r);
+  if (!op) return next.MPI_Request_get_status(r, flag, status);
+  if (PersistentOp *p = op->persistent()) return persistent_get_status(p, flag, status);
   progress();
-  *flag = it->second->done ? 1 : 0;
-  if (*flag) it->second->status(status);
+  *flag = op->done ? 1 : 0; // (progress never frees an application-visible request)
+  if (*flag) op->status(status);
   return MPI_SUCCESS;
 }
 
 int cancel(MPI_Request r) {
-  auto it = active.find(uint32_t(r));
-  if (it == active.end()) return MPI_SUCCESS;
-  if (PersistentOp *p = it->second->persistent()) return persistent_cancel(p);
-  it->second->cancel();
+  Op *op = find_op(r);
+  if (!op) return MPI_SUCCESS;
+  if (PersistentOp *p = op->persistent()) return persistent_cancel(p);
+  op->cancel();
   return MPI_SUCCESS;
 }
 
@@ -431,6 +475,7 @@ bool progress(bool full) {
       b->event = nullptr;
     }
     b->complete = true;
+    if (trace::timelineOn) trace::mark(b->scatter ? "batch done (scatter)" : "batch done (gather)", 2);
     if (b->scatter) --scattersInFlight;
     std::vector<Op *> ops;
     ops.swap(b->ops);
@@ -543,10 +588,10 @@ bool progress(bool full) {
   if (!detachedOps.empty() && progressDepth == 1) {
     size_t w = 0;
     for (uint32_t h : detachedOps) {
-      auto it = active.find(h);
-      if (it == active.end()) continue;
-      if (it->second->done)
-        active.erase(it);
+      Op *op = active.get(h);
+      if (!op) continue;
+      if (op->done)
+        active.erase(h);
       else
         detachedOps[w++] = h;
     }
@@ -569,36 +614,37 @@ int finish_error(int err, MPI_Comm comm) {
 
 int wait(MPI_Request *req, MPI_Status *status) {
   const uint32_t h = uint32_t(*req);
-  auto it = active.find(h);
-  if (it == active.end()) return next.MPI_Wait(req, status);
-  if (PersistentOp *p = it->second->persistent()) return persistent_wait(p, status);
-  ScopedNs timer(counters.ns_wait);
-  Op *op = it->second.get();
-  while (!op->done) {
-    progress();
-    if (!op->done) op->stalled();
+  Op *op = find_op(*req);
+  if (!op) return next.MPI_Wait(req, status);
+  if (PersistentOp *p = op->persistent()) return persistent_wait(p, status);
+  if (!op->done) {
+    ScopedNs timer(counters.ns_wait);
+    while (!op->done) {
+      progress();
+      if (!op->done) op->stalled();
+    }
   }
-  it->second->status(status);
+  op->status(status);
   const int err = op->err;
   const MPI_Comm ec = op->errComm;
-  active.erase(it);
+  active.erase(h);
   *req = MPI_REQUEST_NULL;
   return finish_error(err, ec);
 }
 
 int test(MPI_Request *req, int *flag, MPI_Status *status) {
   const uint32_t h = uint32_t(*req);
-  auto it = active.find(h);
-  if (it == active.end()) return next.MPI_Test(req, flag, status);
-  if (PersistentOp *p = it->second->persistent()) return persistent_test(p, flag, status);
+  Op *op = find_op(*req);
+  if (!op) return next.MPI_Test(req, flag, status);
+  if (PersistentOp *p = op->persistent()) return persistent_test(p, flag, status);
   progress();
-  if (!it->second->done) it->second->stalled();
-  *flag = it->second->done ? 1 : 0;
+  if (!op->done) op->stalled();
+  *flag = op->done ? 1 : 0;
   if (*flag) {
-    it->second->status(status);
-    const int err = it->second->err;
-    const MPI_Comm ec = it->second->errComm;
-    active.erase(it);
+    op->status(status);
+    const int err = op->err;
+    const MPI_Comm ec = op->errComm;
+    active.erase(h);
     *req = MPI_REQUEST_NULL;
     return finish_error(err, ec);
   }

@@ -11,6 +11,8 @@
 #                of the headline (tools/gpu_prof.sh)
 #   halo         halo_exchange 10 512 at RANKS (default "1 2") ranks, both forms
 #   halo-trace   kernel + HIP API trace of the 1-rank halo (tools/halo_trace_summary.py)
+#   halo-timeline  TEMPI's host timeline (TEMPI_TIMELINE) beside a kernel-only
+#                trace of the 1-rank halo: idle attribution (tools/halo_timeline.py)
 #   sweep-pmc    FETCH_SIZE / WRITE_SIZE passes over SHAPES (tools/sweep_pmc.sh)
 #   measure      measure_system --quick at 2 ranks into gpurun_out/perf_quick.json
 #   torchrun     the driver's torchrun command at NS (default "2") ranks
@@ -52,6 +54,13 @@ for step in "$@"; do
     grep '^{' $O/halo_trace.log
     python3 tools/halo_trace_summary.py $O/halo_trace > $O/halo_trace_summary.txt 2>&1 || exit 11
     cat $O/halo_trace_summary.txt ;;
+  halo-timeline)
+    rm -rf $O/halo_tl $O/halo_tl.r0.csv
+    TEMPI_TIMELINE=$O/halo_tl timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d $O/halo_tl -o run \
+      -- tempi_amd/lib/halo_exchange 10 512 $HALO_ARGS > $O/halo_tl.log 2>&1 || exit 17
+    grep '^{' $O/halo_tl.log
+    python3 tools/halo_timeline.py $O/halo_tl.r0.csv $O/halo_tl > $O/halo_timeline.txt 2>&1 || exit 18
+    cat $O/halo_timeline.txt ;;
   sweep-pmc)
     bash tools/sweep_pmc.sh || exit 12 ;;
   measure)
