@@ -32,6 +32,8 @@
 #include <hip/hip_runtime.h>
 #include <mpi.h>
 
+#include "tempi_ext.h"
+
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
@@ -130,6 +132,7 @@ static bool host_buffers() {
 // TEMPI's own entry points, when the interposer is linked (weak: the app runs
 // unchanged on a plain MPI)
 extern "C" __attribute__((weak)) void tempi_reset_counters(void);
+extern "C" __attribute__((weak)) void tempi_get_counters(tempi_counters_t *out);
 
 static double trimean(std::vector<double> v) {
   if (v.empty()) return 0;
@@ -408,6 +411,14 @@ tempi_bench_halo(int nIters, int gx, int gy, int gz, int nQuants, int radius, in
     }
   MPI_Allreduce(MPI_IN_PLACE, remote, 2, MPI_DOUBLE, MPI_SUM, MPI_COMM_WORLD);
   const double tIter = trimean(times);
+  // the GPU's busy time by TEMPI's own account (a transport batch in flight),
+  // so that the line splits an iteration into GPU work and host-only time
+  double inflightUs = -1;
+  if (tempi_get_counters) {
+    tempi_counters_t c{};
+    tempi_get_counters(&c);
+    inflightUs = double(c.gpu_inflight_ns) * 1e-3 / nIters;
+  }
   if (worldRank == 0 && json && jsonCap > 0) {
     std::snprintf(json, size_t(jsonCap), "{\"ranks\": %d, \"global\": [%d, %d, %d], \"dims\": [%d, %d, %d], \"lcr\": [%d, %d, %d], "
                 "\"quants\": %d, \"radius\": %d, \"iters\": %d, \"us_per_iter\": %.2f, \"us_min\": %.2f, "
@@ -416,14 +427,14 @@ tempi_bench_halo(int nIters, int gx, int gy, int gz, int nQuants, int radius, in
                 "\"remote_bytes_per_iter\": %.0f, \"links_used\": %.0f, "
                 "\"checked\": %s, \"errors\": %lld, \"api\": \"%s\", \"reorder\": %s, \"buffers\": \"%s\", "
                 "\"rank0_us_per_iter\": {\"isend\": %.1f, "
-                "\"irecv\": %.1f, \"wait\": %.1f}}\n",
+                "\"irecv\": %.1f, \"wait\": %.1f, \"gpu_inflight\": %.1f}}\n",
                 size, global.x, global.y, global.z, dims.x, dims.y, dims.z, lcr.x, lcr.y, lcr.z, nQuants, radius,
                 nIters, tIter * 1e6, *std::min_element(times.begin(), times.end()) * 1e6, bytesPerIter, totalBytes,
                 maxLinkAll, totalBytes / tIter / 1e9, maxLinkAll / tIter / 1e9, remote[0], remote[1],
                 check ? "true" : "false", errors,
                 (neighbor & 1) ? "MPI_Neighbor_alltoallw" : "MPI_Isend/MPI_Irecv/MPI_Wait", reorder ? "true" : "false",
                 onHost ? "host" : "device",
-                tIsend / nIters * 1e6, tIrecv / nIters * 1e6, tWait / nIters * 1e6);
+                tIsend / nIters * 1e6, tIrecv / nIters * 1e6, tWait / nIters * 1e6, inflightUs);
   }
   if (graph != MPI_COMM_NULL) MPI_Comm_free(&graph);
   for (Dir &D : dirs) {

@@ -636,6 +636,20 @@ def halo(args, mpi, world, grid=None):
                                          f"{HBM_ACHIEVABLE_GBS:.0f} GB/s)")}
         except Exception as e:  # (evidence beside the metric, never fatal)
             out["floor"] = {"error": str(e)[:200]}
+        # the iteration split by TEMPI's own account (counters.ns_gpu_inflight:
+        # a transport batch launched and not yet seen complete): GPU work, and
+        # host-only time -- the send burst (every MPI_Isend of a substep is
+        # posted before any receive exists, so nothing can run) and the rest
+        # (first receives and launch, the waits' tail); DESIGN §6
+        ph = r.get("rank0_us_per_iter") or {}
+        if ph.get("gpu_inflight", -1) > 0:
+            busy = ph["gpu_inflight"]
+            out["split_us_per_iter"] = {"gpu_inflight": round(busy, 1),
+                                        "host_only": round(r["us_per_iter"] - busy, 1),
+                                        "send_burst": round(ph.get("isend", 0.0), 1)}
+            fl = out.get("floor") or {}
+            if "us_per_iter" in fl:
+                fl["frac_of_gpu_inflight"] = round(fl["us_per_iter"] / busy, 4)
     else:
         # xGMI: the busiest point-to-point link carries max_peer bytes per iteration
         lb = r["max_peer_bytes_per_iter"] / (XGMI_LINK_GBS * 1e9)
@@ -1118,6 +1132,10 @@ def _compact_sections(rec, shared_gpu):
         fl = h.get("floor") or {}
         if "frac" in fl:
             c["floor_us_per_iter"], c["frac_floor"] = fl["us_per_iter"], fl["frac"]
+            if "frac_of_gpu_inflight" in fl:
+                c["frac_floor_of_gpu_inflight"] = fl["frac_of_gpu_inflight"]
+        if h.get("split_us_per_iter"):
+            c["split_us_per_iter"] = h["split_us_per_iter"]
         if h.get("rank0_phase_us"):
             c["rank0_phase_us"] = h["rank0_phase_us"]
         cb = h.get("cpu_baseline")

@@ -52,6 +52,9 @@ typedef struct tempi_counters_t {
   uint64_t sync_waits;     /* ... completed by hipStreamSynchronize (kernel wrote application host memory) */
   uint64_t ticket_batches; /* transport batches whose last launch stored a completion ticket (no event) */
   uint64_t persistent_starts; /* MPI_Start / MPI_Startall of persistent requests TEMPI holds */
+  uint64_t batches;        /* transport batches launched (gathers, scatters, copies) */
+  uint64_t gpu_inflight_ns; /* time with a transport batch in flight: from its launch's return to its
+                               completion observed by the host (the GPU's busy time, by TEMPI's account) */
 } tempi_counters_t;
 void tempi_get_counters(tempi_counters_t *out);
 void tempi_reset_counters(void);

@@ -44,6 +44,10 @@ struct Counters {
   // and the MPI_Waitall that completes them (the call is blocking)
   uint64_t ns_nbr_post = 0, ns_nbr_wait = 0;
   uint64_t progress_passes = 0, batches = 0, batched_items = 0;
+  // time (ns) with at least one transport batch in flight by the host's own
+  // account: from a batched launch's return to that batch observed complete
+  // (always on: two clock reads per batch)
+  uint64_t ns_gpu_inflight = 0;
 };
 
 extern Counters counters;

@@ -77,6 +77,8 @@ TEMPI_EXPORT void tempi_get_counters(tempi_counters_t *o) {
   o->sync_waits = c.sync_waits;
   o->ticket_batches = c.ticket_batches;
   o->persistent_starts = c.persistent_starts;
+  o->batches = c.batches;
+  o->gpu_inflight_ns = c.ns_gpu_inflight;
 }
 
 TEMPI_EXPORT void tempi_reset_counters(void) {

@@ -123,6 +123,7 @@ void init() {
   if (const char *s = std::getenv("TEMPI_IPC_COPY_MIN_BYTES")) ipcCopyMinBytes = std::atoll(s);
   if (const char *s = std::getenv("TEMPI_IPC_COPY_MIN_BLOCK")) ipcCopyMinBlock = std::atoll(s);
   scattersInFlight = 0;
+  batchesInFlight = 0;
   directShared.clear();
   directShared.reserve(512);
   systemPerformanceLoaded = import_system_performance(&systemPerformance);
@@ -163,6 +164,7 @@ void finalize() {
     if (b->event) tempi_hip_event_destroy(b->event);
   batches.clear();
   scattersInFlight = 0;
+  batchesInFlight = 0;
   while (!pendingAcks.empty()) {
     progress();
     if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(30)) {
@@ -475,6 +477,7 @@ bool progress(bool full) {
       b->event = nullptr;
     }
     b->complete = true;
+    batch_observed_done();
     if (trace::timelineOn) trace::mark(b->scatter ? "batch done (scatter)" : "batch done (gather)", 2);
     if (b->scatter) --scattersInFlight;
     std::vector<Op *> ops;

@@ -369,8 +369,12 @@ constexpr size_t kMaxPending = 512;
 // (kFirstFlush while no scatter batch is in flight: the GPU is idle then)
 constexpr size_t kEarlyFlush = 32;
 constexpr size_t kFirstFlush = 16;
+extern int batchesInFlight;    // batches launched and not yet seen complete (any kind)
 extern int scattersInFlight;   // scatter / copy batches launched and not yet seen complete
 void flush_list(PendingList &list, bool pack);
+// counters.ns_gpu_inflight bookkeeping: a batch launched / observed complete
+void batch_launched();
+void batch_observed_done();
 void flush();
 
 // the send state machines (p2p_ops.cpp)

@@ -177,6 +177,16 @@ void Op::settle_buffered() {
   unpostedBuffered = false;
 }
 int scattersInFlight = 0;
+int batchesInFlight = 0;
+uint64_t inflightSince = 0; // (ns) the first of the batches now in flight was launched
+
+void batch_launched() {
+  if (batchesInFlight++ == 0) inflightSince = now_ns();
+}
+
+void batch_observed_done() {
+  if (batchesInFlight > 0 && --batchesInFlight == 0) counters.ns_gpu_inflight += now_ns() - inflightSince;
+}
 
 namespace {
 template <typename T> const T *select(const std::vector<T> &v, const std::vector<int> &dev, int d, bool all,
@@ -270,6 +280,7 @@ void flush_list(PendingList &list, bool pack) {
         b->ops.push_back(op);
       }
     batches.push_back(b);
+    batch_launched();
   }
   list.clear();
 }

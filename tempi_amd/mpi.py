@@ -42,7 +42,7 @@ _COUNTER_FIELDS = [
     "send_ipc", "lib_sends", "lib_recvs", "send_direct", "direct_fallbacks",
     "neighbor_colls", "send_ipc_copy", "copy_resends", "ipc_maps_replaced", "canary_ok", "canary_fail",
     "self_matched", "staged_packs", "staged_unpacks", "ticket_waits", "sync_waits",
-    "ticket_batches", "persistent_starts",
+    "ticket_batches", "persistent_starts", "batches", "gpu_inflight_ns",
 ]
 
 
