@@ -951,6 +951,28 @@ def nbr_alltoallv(args, world):
             "points": out}
 
 
+def sweep_shape(mpi, bl, st, dims, packed_target):
+    """One config-2 sweep shape: (uncommitted type, extent, label, planes,
+    payload). planes = (planes, rows per plane, plane stride, first byte) for
+    touched_model."""
+    rows = packed_target // bl
+    if dims == 2:
+        t = mpi.Type_create_subarray([rows, st], [rows, bl], [0, 0], mpi.ORDER_C, mpi.BYTE)
+        extent = rows * st
+        shape = f"2d rows={rows} stride={st}"
+        planes = (1, rows, 0, 0)
+    else:
+        y = max(1, int(rows ** 0.5))
+        z = max(1, rows // y)
+        rows = y * z
+        Y = y + 3
+        t = mpi.Type_create_subarray([z + 2, Y, st], [z, y, bl], [1, 2, 0], mpi.ORDER_C, mpi.BYTE)
+        extent = (z + 2) * Y * st
+        shape = f"3d {z}x{y} rows pitch={st} ypad=3"
+        planes = (z, y, Y * st, Y * st + 2 * st)
+    return t, extent, shape, planes, rows * bl
+
+
 def sweep(args, mpi, torch, dev, path, sizes=(1 << 20, 16 << 20, 256 << 20, 1 << 30), quiet=False):
     """Config-2 sweep: 2D subarray and 3D subarray, block 1 B - 4 KiB.
     Returns the records (also written to `path` when given)."""
@@ -961,26 +983,11 @@ def sweep(args, mpi, torch, dev, path, sizes=(1 << 20, 16 << 20, 256 << 20, 1 <<
             strides = sorted({2 * bl, bl + 16} | ({512} if bl <= 256 else set()))
             for st in strides:
                 for dims in (2, 3):
-                    rows = packed_target // bl
-                    if dims == 2:
-                        t = mpi.Type_create_subarray([rows, st], [rows, bl], [0, 0], mpi.ORDER_C, mpi.BYTE)
-                        extent = rows * st
-                        shape = f"2d rows={rows} stride={st}"
-                        planes = (1, rows, 0, 0)  # (planes, rows per plane, plane stride, first byte)
-                    else:
-                        y = max(1, int(rows ** 0.5))
-                        z = max(1, rows // y)
-                        rows = y * z
-                        Y = y + 3
-                        t = mpi.Type_create_subarray([z + 2, Y, st], [z, y, bl], [1, 2, 0], mpi.ORDER_C, mpi.BYTE)
-                        extent = (z + 2) * Y * st
-                        shape = f"3d {z}x{y} rows pitch={st} ypad=3"
-                        planes = (z, y, Y * st, Y * st + 2 * st)
+                    t, extent, shape, planes, payload = sweep_shape(mpi, bl, st, dims, packed_target)
                     if extent > (12 << 30):
                         mpi.Type_free(t)
                         continue
                     t = mpi.Type_commit(t)
-                    payload = rows * bl
                     src = torch.empty(extent, dtype=torch.uint8, device=dev)
                     pk = torch.empty(payload, dtype=torch.uint8, device=dev)
                     torch.cuda.synchronize()

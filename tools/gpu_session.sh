@@ -13,7 +13,8 @@
 #   halo-trace   kernel + HIP API trace of the 1-rank halo (tools/halo_trace_summary.py)
 #   halo-timeline  TEMPI's host timeline (TEMPI_TIMELINE) beside a kernel-only
 #                trace of the 1-rank halo: idle attribution (tools/halo_timeline.py)
-#   sweep-pmc    FETCH_SIZE / WRITE_SIZE passes over SHAPES (tools/sweep_pmc.sh)
+#   sweep-pmc    FETCH_SIZE / WRITE_SIZE passes over the sweep shapes SHAPES
+#                (DIMS:BLOCK:STRIDE ...; tools/sweep_pmc.py)
 #   measure      measure_system --quick at 2 ranks into gpurun_out/perf_quick.json
 #   torchrun     the driver's torchrun command at NS (default "2") ranks
 #   n8           the driver's torchrun command at 8 ranks (tools/gpu_n8.sh)
@@ -62,7 +63,9 @@ for step in "$@"; do
     python3 tools/halo_timeline.py $O/halo_tl.r0.csv $O/halo_tl > $O/halo_timeline.txt 2>&1 || exit 18
     cat $O/halo_timeline.txt ;;
   sweep-pmc)
-    bash tools/sweep_pmc.sh || exit 12 ;;
+    timeout -k 10 900 python3 tools/sweep_pmc.py $O/sweep_pmc.json ${SHAPES:-2:2:18 3:2:18 3:1:2 3:2:4 3:3:19 2:24:40 3:64:128 2:8:512} \
+      > $O/sweep_pmc.log 2>&1 || exit 12
+    cat $O/sweep_pmc.log ;;
   measure)
     rm -f $O/perf_quick.json
     timeout -k 10 400 $MPIEXEC -n 2 tempi_amd/lib/measure_system --quick --out $O/perf_quick.json \
