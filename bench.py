@@ -65,6 +65,9 @@ def parse():
     p.add_argument("--sweep", default=None, help="run the config-2 sweep and write JSON records here")
     p.add_argument("--sweep-sizes", default=None,
                    help="comma-separated packed sizes for --sweep (default 1 MiB, 16 MiB, 256 MiB, 1 GiB)")
+    p.add_argument("--sweep-traffic", default=None, metavar="SHAPES",
+                   help="comma-separated DIMS:BLOCK:STRIDE sweep shapes whose FETCH / WRITE traffic is counted "
+                        "against the touched model (tools/sweep_pmc.py; sweep_geomean.traffic_checked in the detail)")
     p.add_argument("--no-sweep-geomean", action="store_true",
                    help="skip the 1 GiB points of the config-2 sweep in the default line (sweep_geomean)")
     p.add_argument("--no-measure-system", action="store_true",
@@ -1027,6 +1030,21 @@ def sweep(args, mpi, torch, dev, path, sizes=(1 << 20, 16 << 20, 256 << 20, 1 <<
     return recs
 
 
+def sweep_traffic(specs):
+    """FETCH_SIZE / WRITE_SIZE counted per sweep shape against the touched
+    model's raw bytes (tools/sweep_pmc.py): model / counted ratios, and the
+    shapes re-scored where the model over-predicts by more than 10 %"""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import sweep_pmc
+
+    outdir = os.path.join(ROOT, "gpurun_out") if os.path.isdir(os.path.join(ROOT, "gpurun_out")) else None
+    recs = sweep_pmc.run(specs, outdir)
+    keep = ("spec", "shape", "pack_model_over_counted", "unpack_model32_over_counted", "pack_frac_touched",
+            "unpack_frac_touched", "pack_frac_counted", "unpack_frac_counted", "pack_rescored_frac_touched",
+            "unpack_rescored_frac_touched", "counted", "model")
+    return [{k: r[k] for k in keep if k in r} for r in recs]
+
+
 def sweep_geomean(args, mpi, torch, dev):
     """The config-2 sweep's 1 GiB points (2D and 3D subarrays, block 1 B -
     4 KiB, strides 2*bl / bl+16 / 512): geometric mean of algorithmic GB/s
@@ -1387,6 +1405,9 @@ def main():
                     rec["roofline"]["traffic_source"] = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, "
                                                          "per launch of pack_kernel/unpack_kernel, FETCH_SIZE x2 "
                                                          "(gfx950)")
+                if args.sweep_traffic and isinstance(rec.get("sweep_geomean"), dict):
+                    tc = sec.run("sweep_traffic", sweep_traffic, args.sweep_traffic.split(","))
+                    rec["sweep_geomean"]["traffic_checked"] = tc
                 if rec.get("halo") and "error" not in rec["halo"]:
                     ht = sec.run("halo_traffic", halo_traffic, args)
                     if isinstance(ht, dict):

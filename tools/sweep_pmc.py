@@ -100,7 +100,10 @@ def one(spec):
 
 
 def family(name):
-    n = name.split("(")[0]
+    import re
+
+    m = re.search(r"::(\w+)[<(]", name)
+    n = m.group(1) if m else ""
     if "ticket" in n:
         return None
     if "unpack" in n:
