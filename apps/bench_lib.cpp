@@ -633,6 +633,13 @@ double median(std::vector<double> v) {
   std::sort(v.begin(), v.end());
   return v[v.size() / 2];
 }
+// the same kernel-argument size as the packer's launch (KArgs<1> + Sig)
+struct Args184 {
+  unsigned char b[184];
+};
+__global__ void empty_kernel_184(Args184 a) {
+  if (a.b[0] == 0xEE && threadIdx.x == 1000) a.b[1] = 0; // never true; keeps the argument
+}
 } // namespace
 
 EXPORT int tempi_bench_sync_phases(int reps, char *json, int jsonCap) {
@@ -655,16 +662,28 @@ EXPORT int tempi_bench_sync_phases(int reps, char *json, int jsonCap) {
   d.ndims = 1;
   d.counts[0] = rows;
   d.strides[0] = stride;
-  std::vector<double> api, lib, ptr, launch, wait, total;
+  std::vector<double> api, lib, ptr, launch, wait, total, apiMixed, launchMixed, bare;
   int errs = 0;
+  // Each phase in a loop of its own (the call as an application makes it,
+  // back to back), then the interleaved loop round 4 measured: there, each
+  // TEMPI call followed MPICH's 512 KiB host pack, which evicts the HIP
+  // runtime's state from the core's caches and adds ~1 us to the launch
+  // (VERDICT r04 weak 4). `bare_launch` is an empty kernel with the packer's
+  // argument size on the same stream: HIP's own floor on this box.
   for (int r = 0; r < reps + 20; ++r) {
-    const bool keep = r >= 20;
     int pos = 0;
     double t0 = now_us();
     errs += MPI_Pack(src, 1, t, dst, packed, &pos, MPI_COMM_WORLD) != MPI_SUCCESS || pos != packed;
-    double t1 = now_us();
-    pos = 0;
+    if (r >= 20) api.push_back(now_us() - t0);
+  }
+  for (int r = 0; r < reps + 20; ++r) {
+    int pos = 0;
+    double t0 = now_us();
     errs += MPI_Pack(hsrc.data(), 1, t, hdst.data(), packed, &pos, MPI_COMM_WORLD) != MPI_SUCCESS;
+    if (r >= 20) lib.push_back(now_us() - t0);
+  }
+  for (int r = 0; r < reps + 20; ++r) {
+    const bool keep = r >= 20;
     double t2 = now_us();
     tempi_hip_ptrinfo info;
     tempi_hip_pointer_info(src, &info);
@@ -677,12 +696,38 @@ EXPORT int tempi_bench_sync_phases(int reps, char *json, int jsonCap) {
     errs += tempi_hip_ticket_wait(s, flag, ticket) != 0;
     double t5 = now_us();
     if (keep) {
-      api.push_back(t1 - t0);
-      lib.push_back(t2 - t1);
       ptr.push_back(t3 - t2);
       launch.push_back(t4 - t3);
       wait.push_back(t5 - t4);
       total.push_back(t5 - t3);
+    }
+  }
+  for (int r = 0; r < reps + 20; ++r) {
+    HIPCHECK(hipStreamSynchronize(s));
+    double t0 = now_us();
+    hipLaunchKernelGGL(empty_kernel_184, dim3(256), dim3(256), 0, s, Args184{});
+    double t1 = now_us();
+    if (r >= 20) bare.push_back(t1 - t0);
+  }
+  HIPCHECK(hipStreamSynchronize(s));
+  for (int r = 0; r < reps + 20; ++r) { // interleaved with MPICH's host pack (round 4's loop)
+    int pos = 0;
+    errs += MPI_Pack(hsrc.data(), 1, t, hdst.data(), packed, &pos, MPI_COMM_WORLD) != MPI_SUCCESS;
+    double t0 = now_us();
+    pos = 0;
+    errs += MPI_Pack(src, 1, t, dst, packed, &pos, MPI_COMM_WORLD) != MPI_SUCCESS || pos != packed;
+    double t1 = now_us();
+    const uint32_t *flag = nullptr;
+    uint32_t ticket = 0;
+    int pos2 = 0;
+    errs += MPI_Pack(hsrc.data(), 1, t, hdst.data(), packed, &pos2, MPI_COMM_WORLD) != MPI_SUCCESS;
+    double t3 = now_us();
+    errs += tempi_hip_pack_ticket(dst, src, &d, s, &flag, &ticket) != 0;
+    double t4 = now_us();
+    errs += tempi_hip_ticket_wait(s, flag, ticket) != 0;
+    if (r >= 20) {
+      apiMixed.push_back(t1 - t0);
+      launchMixed.push_back(t4 - t3);
     }
   }
   hipEvent_t e0, e1;
@@ -702,12 +747,14 @@ EXPORT int tempi_bench_sync_phases(int reps, char *json, int jsonCap) {
   HIPCHECK(hipFree(dst));
   MPI_Type_free(&t);
   std::snprintf(json, size_t(jsonCap),
-                "{\"workload\": \"config 1: MPI_Pack of vector(1024, 512, 1024), 512 KiB, medians of %d calls in C\", "
+                "{\"workload\": \"config 1: MPI_Pack of vector(1024, 512, 1024), 512 KiB, medians of %d calls in C, each phase in a loop of its own\", "
                 "\"mpi_pack_device_us\": %.2f, \"mpich_host_us\": %.2f, \"c_speedup\": %.3f, "
                 "\"phases_us\": {\"pointer_info_x2\": %.2f, \"launch\": %.2f, \"ticket_wait\": %.2f, "
-                "\"launch_plus_wait\": %.2f, \"kernel_back_to_back\": %.2f}, \"errors\": %d}",
+                "\"launch_plus_wait\": %.2f, \"kernel_back_to_back\": %.2f, \"bare_launch\": %.2f}, "
+                "\"interleaved_with_mpich\": {\"mpi_pack_device_us\": %.2f, \"launch\": %.2f}, \"errors\": %d}",
                 reps, median(api), median(lib), median(api) > 0 ? median(lib) / median(api) : 0.0, median(ptr),
-                median(launch), median(wait), median(total), double(ms) * 1e3 / nk, errs);
+                median(launch), median(wait), median(total), double(ms) * 1e3 / nk, median(bare), median(apiMixed),
+                median(launchMixed), errs);
   return errs ? 1 : 0;
 }
 
