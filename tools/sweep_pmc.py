@@ -15,7 +15,8 @@ MI355X_MICROARCH.md) are set beside the model's raw-byte prediction:
 The ratio model / counter > 1.10 means the model over-predicts the traffic:
 that shape's frac_touched is then re-scored with the counted bytes
 (`rescored_frac_touched`, the counted bytes at 6.3 TB/s over the kernel
-time measured in the same process).
+time of a third run of the same child without a profiler: counter
+collection serialises and slows the dispatches it counts).
 
 usage (GPU box): python3 tools/sweep_pmc.py OUT.json DIMS:BLOCK:STRIDE ...
        python3 tools/sweep_pmc.py --one DIMS:BLOCK:STRIDE   (the profiled child)"""
@@ -131,13 +132,24 @@ def profile(spec, counter, outdir):
     return info, {k: (sum(v[1:]) / len(v[1:]) if len(v) > 1 else None) for k, v in vals.items()}
 
 
+def timed(spec):
+    """the same child without a profiler: its kernel times (counter
+    collection serialises and slows the dispatches it counts)"""
+    r = subprocess.run(["timeout", "-s", "KILL", "120", sys.executable, os.path.abspath(__file__), "--one", spec],
+                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"{spec} timing run: rc {r.returncode}\n{r.stdout[-2000:]}")
+    return json.loads(next(l for l in r.stdout.splitlines() if l.startswith("{")))
+
+
 def run(specs, outdir):
     import bench
 
     recs = []
     for spec in specs:
-        info, fetch = profile(spec, "FETCH_SIZE", outdir)
+        _, fetch = profile(spec, "FETCH_SIZE", outdir)
         _, write = profile(spec, "WRITE_SIZE", outdir)
+        info = timed(spec)
         dims, bl, st = (int(x) for x in spec.split(":"))
         m = model(bl, st, tuple(info["planes"]))
         got = {"pack_read": 2.0 * fetch["pack"], "pack_write": write["pack"],
