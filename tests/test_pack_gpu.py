@@ -699,12 +699,13 @@ def _hip():
     return hip
 
 
-# host arrays the registered case hipHostRegister'ed: kept for the whole
-# session, so that their addresses are never handed out again by malloc. (GPU
-# box, round 4: right after the registered case unregistered and freed its
-# arrays, the next case's first pageable torch copy -- a fresh 18 MiB numpy
-# array, likely at the freed address -- failed with an illegal address.)
-_REGISTERED_KEEP = []
+# (Round 4 kept the registered arrays alive for the whole session after one
+# illegal address in the next case's first pageable copy. Round 5 replayed
+# the sequence step by step -- tools/diag_registered.py, profiles/r05/
+# diag_registered_s8.jsonl: hipHostUnregister returns 0, both HIP runtimes
+# then see the range as plain host memory, a fresh array lands on the freed
+# address and both a pageable torch copy and TEMPI's staged MPI_Pack into it
+# are correct -- so the arrays are freed here again, as an application would.)
 
 
 @pytest.mark.parametrize("kind", ["noncoherent", "registered", "coherent"])
@@ -720,14 +721,14 @@ def test_application_pinned_memory_waits_with_stream_sync(mpi, gpu, kind):
     n = rows * block
     ext = (rows - 1) * stride + block
     t = mpi.Type_commit(mpi.Type_vector(rows, block, stride, mpi.BYTE))
-    ptrs = []
+    ptrs, arrays = [], []
 
     def host_buf(nbytes):
         if kind == "registered":
             a = np.zeros(nbytes + 4096, dtype=np.uint8)
             p = (a.ctypes.data + 4095) & ~4095
             assert hip.hipHostRegister(ctypes.c_void_p(p), nbytes, 0x2 | 0x1) == 0  # mapped, portable
-            _REGISTERED_KEEP.append(a)
+            arrays.append(a)
             ptrs.append(("unreg", p))
         else:
             v = ctypes.c_void_p()
@@ -765,3 +766,4 @@ def test_application_pinned_memory_waits_with_stream_sync(mpi, gpu, kind):
         for how, p in ptrs:
             rc = (hip.hipHostUnregister if how == "unreg" else hip.hipHostFree)(ctypes.c_void_p(p))
             assert rc == 0, f"{how} of {p:#x}: hip error {rc}"
+        arrays.clear()  # (the registered arrays go back to malloc once unregistered)
