@@ -65,9 +65,10 @@ def parse():
     p.add_argument("--sweep", default=None, help="run the config-2 sweep and write JSON records here")
     p.add_argument("--sweep-sizes", default=None,
                    help="comma-separated packed sizes for --sweep (default 1 MiB, 16 MiB, 256 MiB, 1 GiB)")
-    p.add_argument("--sweep-traffic", default=None, metavar="SHAPES",
+    p.add_argument("--sweep-traffic", default="2:2:18,3:1:2,2:24:40,2:8:512", metavar="SHAPES",
                    help="comma-separated DIMS:BLOCK:STRIDE sweep shapes whose FETCH / WRITE traffic is counted "
-                        "against the touched model (tools/sweep_pmc.py; sweep_geomean.traffic_checked in the detail)")
+                        "against the touched model (tools/sweep_pmc.py; sweep_geomean.traffic_checked in the "
+                        "detail); 'none' skips it")
     p.add_argument("--no-sweep-geomean", action="store_true",
                    help="skip the 1 GiB points of the config-2 sweep in the default line (sweep_geomean)")
     p.add_argument("--no-measure-system", action="store_true",
@@ -1034,6 +1035,11 @@ def sweep_traffic(specs):
     """FETCH_SIZE / WRITE_SIZE counted per sweep shape against the touched
     model's raw bytes (tools/sweep_pmc.py): model / counted ratios, and the
     shapes re-scored where the model over-predicts by more than 10 %"""
+    import shutil
+
+    if not shutil.which("rocprofv3") or any(k.startswith("ROCPROF") for k in os.environ) or \
+            "rocprof" in os.environ.get("LD_PRELOAD", ""):
+        return None  # (no profiler, or already under one: see run_traffic_passes)
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import sweep_pmc
 
@@ -1405,7 +1411,7 @@ def main():
                     rec["roofline"]["traffic_source"] = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, "
                                                          "per launch of pack_kernel/unpack_kernel, FETCH_SIZE x2 "
                                                          "(gfx950)")
-                if args.sweep_traffic and isinstance(rec.get("sweep_geomean"), dict):
+                if args.sweep_traffic not in (None, "", "none") and isinstance(rec.get("sweep_geomean"), dict):
                     tc = sec.run("sweep_traffic", sweep_traffic, args.sweep_traffic.split(","))
                     rec["sweep_geomean"]["traffic_checked"] = tc
                 if rec.get("halo") and "error" not in rec["halo"]:
