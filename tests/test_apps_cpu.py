@@ -152,3 +152,31 @@ def test_measure_system_host_curves(tmp_path):
     pick = json.loads(next(l for l in log.splitlines() if l.startswith("{")))
     assert pick["loaded"] == 1 and pick["source"] == str(out), pick
     assert all(fm == 0 for _, _, _, fm in pick["picks"]), pick  # no GPU curve priced
+
+
+def test_timeline_records_entry_points(tmp_path):
+    """TEMPI_TIMELINE=PREFIX (core/trace.cpp) writes PREFIX.r<rank>.csv at
+    MPI_Finalize: every interposed MPI_Isend / MPI_Irecv / MPI_Wait as a
+    begin / end pair on CLOCK_BOOTTIME, in order, one file per rank, which
+    tools/halo_timeline.py then splits into substeps"""
+    import csv
+    import subprocess
+    import sys
+
+    pre = str(tmp_path / "tl")
+    rc, out = mpi_launch.run(2, [os.path.join(LIB, "halo_exchange"), "2", "16", "--quants", "1"],
+                             env={"TEMPI_TIMELINE": pre, "TEMPI_BENCH_HOST": "1"}, timeout=120)
+    assert rc == 0, out[-3000:]
+    for r in (0, 1):
+        rows = list(csv.DictReader(open(f"{pre}.r{r}.csv")))
+        ns = [int(x["ns"]) for x in rows]
+        assert ns == sorted(ns) and len(rows) > 100
+        for name in ("MPI_Isend", "MPI_Irecv", "MPI_Wait", "MPI_Barrier"):
+            b = sum(1 for x in rows if x["name"] == name and x["phase"] == "0")
+            e = sum(1 for x in rows if x["name"] == name and x["phase"] == "1")
+            assert b == e > 0, (r, name, b, e)
+    # 3 iterations x 3 substeps of 26 sends each; the analysis finds them
+    # (no batches on host buffers: all idle is host time)
+    p = subprocess.run([sys.executable, os.path.join(mpi_launch.ROOT, "tools", "halo_timeline.py"), f"{pre}.r0.csv",
+                        "-", "3"], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=60)
+    assert p.returncode == 0 and "substeps" in p.stdout, p.stdout

@@ -118,6 +118,10 @@ def test_halo_exchange_512_full_check(gpu, ranks, env):
                              timeout=240)
     r = _json_line(out)
     assert rc == 0 and r["checked"] and r["errors"] == 0 and r["global"] == [512, 512, 512], out[-3000:]
+    # the GPU's busy time by TEMPI's account (counters.ns_gpu_inflight): some
+    # of every iteration, never more than the iteration
+    busy = r["rank0_us_per_iter"]["gpu_inflight"]
+    assert 0 < busy <= r["us_per_iter"] * 1.05, r
 
 
 def test_halo_check_finds_a_planted_error(gpu):
