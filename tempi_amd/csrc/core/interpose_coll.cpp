@@ -24,6 +24,7 @@
 #include "env.hpp"
 #include "gpu.hpp"
 #include "log.hpp"
+#include "mt.hpp"
 #include "next_mpi.hpp"
 #include "p2p.hpp"
 #include "state.hpp"
@@ -74,7 +75,7 @@ int staged(const void *sendbuf, const int *scounts, const int *sdispls, MPI_Data
   if (r) gpu::check(tempi_hip_memcpy(hr->host, static_cast<char *>(recvbuf) + rlo, size_t(rhi - rlo)), "a2av D2H");
   const char *hsend = s ? static_cast<const char *>(hs->host) - slo : nullptr;
   char *hrecv = r ? static_cast<char *>(hr->host) - rlo : nullptr;
-  const int rc = next.MPI_Alltoallv(hsend, scounts, sdispls, stype, hrecv, rcounts, rdispls, rtype, comm);
+  const int rc = TEMPI_UNLOCKED(next.MPI_Alltoallv(hsend, scounts, sdispls, stype, hrecv, rcounts, rdispls, rtype, comm));
   if (r) gpu::check(tempi_hip_memcpy(static_cast<char *>(recvbuf) + rlo, hr->host, size_t(rhi - rlo)), "a2av H2D");
   if (hs) pinned_pool().put(hs);
   if (hr) pinned_pool().put(hr);
@@ -147,6 +148,7 @@ int isir(const void *sendbuf, const int *scounts, const int *sdispls, MPI_Dataty
         const int e = next.MPI_Test(&r, &flag, MPI_STATUS_IGNORE);
         if (e != MPI_SUCCESS || flag) return e;
         p2p::progress();
+        mt::yield();
       }
     }();
     if (rc != MPI_SUCCESS) err = rc;
@@ -200,11 +202,12 @@ using namespace tempi;
 TEMPI_EXPORT int MPI_Alltoallv(const void *sendbuf, const int sendcounts[], const int sdispls[],
                                MPI_Datatype sendtype, void *recvbuf, const int recvcounts[], const int rdispls[],
                                MPI_Datatype recvtype, MPI_Comm comm) {
+  TEMPI_MT_ENTRY;
   resolve_next();
   TEMPI_RANGE("MPI_Alltoallv");
   auto lib = [&] {
-    return next.MPI_Alltoallv(sendbuf, sendcounts, sdispls, sendtype, recvbuf, recvcounts, rdispls, recvtype,
-                              comm);
+    return TEMPI_UNLOCKED(next.MPI_Alltoallv(sendbuf, sendcounts, sdispls, sendtype, recvbuf, recvcounts, rdispls, recvtype,
+                              comm));
   };
   if (!state.active || env.alltoallv == AlltoallvMethod::NONE || !gpu::available() || sendbuf == MPI_IN_PLACE)
     return lib();
@@ -249,9 +252,10 @@ TEMPI_EXPORT int MPI_Alltoallv(const void *sendbuf, const int sendcounts[], cons
 // whenever TEMPI is active, since a blocking and a non-blocking barrier do
 // not match each other (whether a rank is busy is its own business).
 TEMPI_EXPORT int MPI_Barrier(MPI_Comm comm) {
+  TEMPI_MT_ENTRY;
   resolve_next();
   TEMPI_RANGE("MPI_Barrier");
-  if (!state.active) return next.MPI_Barrier(comm);
+  if (!state.active) return TEMPI_UNLOCKED(next.MPI_Barrier(comm));
   MPI_Request r = MPI_REQUEST_NULL;
   int rc = MPI_Ibarrier(comm, &r);
   if (rc != MPI_SUCCESS) return rc;
@@ -260,5 +264,6 @@ TEMPI_EXPORT int MPI_Barrier(MPI_Comm comm) {
     rc = next.MPI_Test(&r, &flag, MPI_STATUS_IGNORE);
     if (rc != MPI_SUCCESS || flag) return rc;
     if (p2p::busy()) p2p::progress();
+    mt::yield();
   }
 }

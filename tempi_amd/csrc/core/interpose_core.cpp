@@ -17,6 +17,7 @@
 #include "env.hpp"
 #include "gpu.hpp"
 #include "log.hpp"
+#include "mt.hpp"
 #include "next_mpi.hpp"
 #include "state.hpp"
 #include "p2p.hpp"
@@ -330,17 +331,22 @@ TEMPI_EXPORT int MPI_Init(int *argc, char ***argv) {
 }
 
 // Thread support. TEMPI's transport keeps unsynchronised process-wide state
-// (the pending launch lists, the board of operations in flight, the library
-// requests it watches: p2p_internal.hpp), so two application threads inside
-// TEMPI at once would race there. TEMPI is safe when the application
-// serialises its MPI calls, and says so: the level the library grants is
-// capped at MPI_THREAD_SERIALIZED, here and in MPI_Query_thread. (The
+// (p2p_internal.hpp). An application that asks for MPI_THREAD_MULTIPLE, and
+// gets it from the library, gets it from TEMPI too: every interposed call then
+// runs under TEMPI's lock, which wait loops and blocking library calls give
+// up (mt.hpp). Any other request is answered with at most
+// MPI_THREAD_SERIALIZED -- the level the unlocked state is safe at -- so that
+// applications that never asked for MULTIPLE pay nothing for the lock. (The
 // reference only logs the level, /root/reference/src/init.cpp:36-46, and
-// hands back whatever the library granted.) With TEMPI disabled the
-// library's level stands.
+// hands back whatever the library granted.) With TEMPI disabled the library's
+// level stands.
 namespace tempi {
-constexpr int kMaxThreadLevel = MPI_THREAD_SERIALIZED;
-int cap_thread_level(int level) { return state.active && level > kMaxThreadLevel ? kMaxThreadLevel : level; }
+constexpr int kMaxUnlockedLevel = MPI_THREAD_SERIALIZED;
+int cap_thread_level(int level) {
+  if (!state.active) return level;
+  if (mt::on) return MPI_THREAD_MULTIPLE;
+  return level > kMaxUnlockedLevel ? kMaxUnlockedLevel : level;
+}
 } // namespace tempi
 
 TEMPI_EXPORT int MPI_Init_thread(int *argc, char ***argv, int required, int *provided) {
@@ -349,10 +355,10 @@ TEMPI_EXPORT int MPI_Init_thread(int *argc, char ***argv, int required, int *pro
   const int rc = next.MPI_Init_thread(argc, argv, required, provided);
   if (rc == MPI_SUCCESS) {
     init_after_mpi();
-    if (provided && *provided != cap_thread_level(*provided)) {
-      if (required > kMaxThreadLevel && state.worldRank == 0)
-        LOG_WARN("MPI_THREAD_MULTIPLE requested: TEMPI provides MPI_THREAD_SERIALIZED (calls into MPI must "
-                 "not overlap; TEMPI_DISABLE=1 keeps the library's level)");
+    if (provided && state.active) {
+      mt::on = required == MPI_THREAD_MULTIPLE && *provided == MPI_THREAD_MULTIPLE;
+      if (mt::on && state.worldRank == 0)
+        LOG_DEBUG("MPI_THREAD_MULTIPLE: TEMPI's calls run under one process-wide lock");
       *provided = cap_thread_level(*provided);
     }
   }
@@ -367,12 +373,15 @@ TEMPI_EXPORT int MPI_Query_thread(int *provided) {
 }
 
 TEMPI_EXPORT int MPI_Finalize(void) {
+  TEMPI_MT_ENTRY;
   resolve_next();
   finalize_before_mpi();
+  mt::on = false; // (this call's own Entry still unlocks: it captured `on`)
   return next.MPI_Finalize();
 }
 
 TEMPI_EXPORT int MPI_Type_commit(MPI_Datatype *datatype) {
+  TEMPI_MT_ENTRY;
   resolve_next();
   const int rc = next.MPI_Type_commit(datatype);
   if (rc != MPI_SUCCESS || !state.active || env.noTypeCommit) return rc;
@@ -381,6 +390,7 @@ TEMPI_EXPORT int MPI_Type_commit(MPI_Datatype *datatype) {
 }
 
 TEMPI_EXPORT int MPI_Type_free(MPI_Datatype *datatype) {
+  TEMPI_MT_ENTRY;
   resolve_next();
   // the library may hand the handle out again: forget it first
   if (state.active && !env.noTypeCommit) type_release(*datatype);
@@ -477,6 +487,7 @@ int unpack(const void *inbuf, int insize, int *position, void *outbuf, int outco
 
 TEMPI_EXPORT int MPI_Pack(const void *inbuf, int incount, MPI_Datatype datatype, void *outbuf,
                           int outsize, int *position, MPI_Comm comm) {
+  TEMPI_MT_ENTRY;
   resolve_next();
   TEMPI_RANGE("MPI_Pack");
   return tempi::pack(inbuf, incount, datatype, outbuf, outsize, position, comm);
@@ -484,6 +495,7 @@ TEMPI_EXPORT int MPI_Pack(const void *inbuf, int incount, MPI_Datatype datatype,
 
 TEMPI_EXPORT int MPI_Unpack(const void *inbuf, int insize, int *position, void *outbuf, int outcount,
                             MPI_Datatype datatype, MPI_Comm comm) {
+  TEMPI_MT_ENTRY;
   resolve_next();
   TEMPI_RANGE("MPI_Unpack");
   return tempi::unpack(inbuf, insize, position, outbuf, outcount, datatype, comm);

@@ -36,6 +36,7 @@
 #include "trace.hpp"
 #include "counters.hpp"
 #include "gpu.hpp"
+#include "mt.hpp"
 #include "next_mpi.hpp"
 #include "p2p.hpp"
 #include "placement.hpp"
@@ -268,11 +269,12 @@ using namespace tempi;
 TEMPI_EXPORT int MPI_Neighbor_alltoallw(const void *sendbuf, const int sendcounts[], const MPI_Aint sdispls[],
                                         const MPI_Datatype sendtypes[], void *recvbuf, const int recvcounts[],
                                         const MPI_Aint rdispls[], const MPI_Datatype recvtypes[], MPI_Comm comm) {
+  TEMPI_MT_ENTRY;
   resolve_next();
   TEMPI_RANGE("MPI_Neighbor_alltoallw");
   auto lib = [&] {
-    return next.MPI_Neighbor_alltoallw(sendbuf, sendcounts, sdispls, sendtypes, recvbuf, recvcounts, rdispls,
-                                       recvtypes, comm);
+    return TEMPI_UNLOCKED(next.MPI_Neighbor_alltoallw(sendbuf, sendcounts, sdispls, sendtypes, recvbuf, recvcounts, rdispls,
+                                       recvtypes, comm));
   };
   // every rank takes the per-edge route, whatever memory its own blocks are
   // in: its neighbours' device blocks travel on the private duplicate, which
@@ -286,11 +288,12 @@ TEMPI_EXPORT int MPI_Neighbor_alltoallw(const void *sendbuf, const int sendcount
 TEMPI_EXPORT int MPI_Neighbor_alltoallv(const void *sendbuf, const int sendcounts[], const int sdispls[],
                                         MPI_Datatype sendtype, void *recvbuf, const int recvcounts[],
                                         const int rdispls[], MPI_Datatype recvtype, MPI_Comm comm) {
+  TEMPI_MT_ENTRY;
   resolve_next();
   TEMPI_RANGE("MPI_Neighbor_alltoallv");
   auto lib = [&] {
-    return next.MPI_Neighbor_alltoallv(sendbuf, sendcounts, sdispls, sendtype, recvbuf, recvcounts, rdispls,
-                                       recvtype, comm);
+    return TEMPI_UNLOCKED(next.MPI_Neighbor_alltoallv(sendbuf, sendcounts, sdispls, sendtype, recvbuf, recvcounts, rdispls,
+                                       recvtype, comm));
   };
   const Neighbours *nb = state.active && gpu::available() ? neighbours(comm) : nullptr;
   if (!nb) return lib();
@@ -311,29 +314,33 @@ TEMPI_EXPORT int MPI_Dist_graph_create_adjacent(MPI_Comm comm_old, int indegree,
                                                 const int sourceweights[], int outdegree, const int destinations[],
                                                 const int destweights[], MPI_Info info, int reorder,
                                                 MPI_Comm *comm_dist_graph) {
+  TEMPI_MT_ENTRY;
   resolve_next();
   TEMPI_RANGE("MPI_Dist_graph_create_adjacent");
   int rc = MPI_SUCCESS;
   if (state.active && placement::create(comm_old, indegree, sources, sourceweights, outdegree, destinations,
                                         destweights, info, reorder, comm_dist_graph, &rc))
     return rc;
-  return next.MPI_Dist_graph_create_adjacent(comm_old, indegree, sources, sourceweights, outdegree, destinations,
-                                             destweights, info, reorder, comm_dist_graph);
+  return TEMPI_UNLOCKED(next.MPI_Dist_graph_create_adjacent(comm_old, indegree, sources, sourceweights, outdegree, destinations,
+                                             destweights, info, reorder, comm_dist_graph));
 }
 
 TEMPI_EXPORT int MPI_Dist_graph_neighbors(MPI_Comm comm, int maxindegree, int sources[], int sourceweights[],
                                           int maxoutdegree, int destinations[], int destweights[]) {
+  TEMPI_MT_ENTRY;
   resolve_next();
   return next.MPI_Dist_graph_neighbors(comm, maxindegree, sources, sourceweights, maxoutdegree, destinations,
                                        destweights);
 }
 
 TEMPI_EXPORT int MPI_Comm_rank(MPI_Comm comm, int *rank) {
+  TEMPI_MT_ENTRY;
   resolve_next();
   return next.MPI_Comm_rank(comm, rank);
 }
 
 TEMPI_EXPORT int MPI_Comm_free(MPI_Comm *comm) {
+  TEMPI_MT_ENTRY;
   resolve_next();
   if (state.active && comm && *comm != MPI_COMM_NULL) comm_release(*comm);
   return next.MPI_Comm_free(comm);

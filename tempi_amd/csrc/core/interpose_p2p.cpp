@@ -10,6 +10,7 @@
 #include "trace.hpp"
 #include "counters.hpp"
 #include "log.hpp"
+#include "mt.hpp"
 #include "next_mpi.hpp"
 #include "p2p.hpp"
 #include "gpu.hpp"
@@ -25,6 +26,7 @@ using namespace tempi;
 
 TEMPI_EXPORT int MPI_Send(const void *buf, int count, MPI_Datatype datatype, int dest, int tag,
                           MPI_Comm comm) {
+  TEMPI_MT_ENTRY;
   resolve_next();
   TEMPI_RANGE("MPI_Send");
   p2p::Route route;
@@ -32,7 +34,7 @@ TEMPI_EXPORT int MPI_Send(const void *buf, int count, MPI_Datatype datatype, int
     counters.lib_sends++;
     p2p::self_spill(comm, dest);
     if (state.active && p2p::send_gated(comm, dest)) p2p::drain_sends(comm, dest); // keep send order
-    return next.MPI_Send(buf, count, datatype, dest, tag, comm);
+    return TEMPI_UNLOCKED(next.MPI_Send(buf, count, datatype, dest, tag, comm));
   }
   counters.sends++;
   MPI_Request r;
@@ -43,6 +45,7 @@ TEMPI_EXPORT int MPI_Send(const void *buf, int count, MPI_Datatype datatype, int
 
 TEMPI_EXPORT int MPI_Recv(void *buf, int count, MPI_Datatype datatype, int source, int tag, MPI_Comm comm,
                           MPI_Status *status) {
+  TEMPI_MT_ENTRY;
   resolve_next();
   TEMPI_RANGE("MPI_Recv");
   p2p::Route route;
@@ -57,11 +60,12 @@ TEMPI_EXPORT int MPI_Recv(void *buf, int count, MPI_Datatype datatype, int sourc
   const int rc = p2p::recv_host_ipc_aware(buf, count, datatype, source, tag, comm, status, &handled);
   if (handled) return rc;
   counters.lib_recvs++;
-  return next.MPI_Recv(buf, count, datatype, source, tag, comm, status);
+  return TEMPI_UNLOCKED(next.MPI_Recv(buf, count, datatype, source, tag, comm, status));
 }
 
 TEMPI_EXPORT int MPI_Isend(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm,
                            MPI_Request *request) {
+  TEMPI_MT_ENTRY;
   resolve_next();
   TEMPI_RANGE("MPI_Isend");
   p2p::Route route;
@@ -79,6 +83,7 @@ TEMPI_EXPORT int MPI_Isend(const void *buf, int count, MPI_Datatype datatype, in
 
 TEMPI_EXPORT int MPI_Irecv(void *buf, int count, MPI_Datatype datatype, int source, int tag, MPI_Comm comm,
                            MPI_Request *request) {
+  TEMPI_MT_ENTRY;
   resolve_next();
   TEMPI_RANGE("MPI_Irecv");
   p2p::Route route;
@@ -93,20 +98,23 @@ TEMPI_EXPORT int MPI_Irecv(void *buf, int count, MPI_Datatype datatype, int sour
 }
 
 TEMPI_EXPORT int MPI_Wait(MPI_Request *request, MPI_Status *status) {
+  TEMPI_MT_ENTRY;
   resolve_next();
   TEMPI_RANGE("MPI_Wait");
-  if (!state.active) return next.MPI_Wait(request, status);
+  if (!state.active) return TEMPI_UNLOCKED(next.MPI_Wait(request, status));
   if (p2p::is_tempi_request(*request)) return p2p::wait(request, status);
-  if (!p2p::busy()) return next.MPI_Wait(request, status);
+  if (!p2p::busy()) return TEMPI_UNLOCKED(next.MPI_Wait(request, status));
   for (;;) { // a library request, while TEMPI operations are in flight
     int flag = 0;
     const int rc = next.MPI_Test(request, &flag, status);
     if (rc != MPI_SUCCESS || flag) return rc;
     p2p::progress();
+    mt::yield();
   }
 }
 
 TEMPI_EXPORT int MPI_Test(MPI_Request *request, int *flag, MPI_Status *status) {
+  TEMPI_MT_ENTRY;
   resolve_next();
   if (!state.active) return next.MPI_Test(request, flag, status);
   if (p2p::is_tempi_request(*request)) return p2p::test(request, flag, status);
@@ -115,12 +123,13 @@ TEMPI_EXPORT int MPI_Test(MPI_Request *request, int *flag, MPI_Status *status) {
 }
 
 TEMPI_EXPORT int MPI_Waitall(int count, MPI_Request requests[], MPI_Status statuses[]) {
+  TEMPI_MT_ENTRY;
   resolve_next();
   TEMPI_RANGE("MPI_Waitall");
-  if (!state.active) return next.MPI_Waitall(count, requests, statuses);
+  if (!state.active) return TEMPI_UNLOCKED(next.MPI_Waitall(count, requests, statuses));
   bool any = false;
   for (int i = 0; i < count && !any; ++i) any = p2p::is_tempi_request(requests[i]);
-  if (!any && !p2p::busy()) return next.MPI_Waitall(count, requests, statuses);
+  if (!any && !p2p::busy()) return TEMPI_UNLOCKED(next.MPI_Waitall(count, requests, statuses));
   std::vector<char> done(size_t(count), 0);
   int remaining = count;
   int err = MPI_SUCCESS;
@@ -141,6 +150,7 @@ TEMPI_EXPORT int MPI_Waitall(int count, MPI_Request requests[], MPI_Status statu
         --remaining;
       }
     }
+    if (remaining) mt::yield();
   }
   return err;
 }
@@ -176,6 +186,7 @@ MPI_Status *at(MPI_Status *statuses, int i) {
 } // namespace
 
 TEMPI_EXPORT int MPI_Testall(int count, MPI_Request requests[], int *flag, MPI_Status statuses[]) {
+  TEMPI_MT_ENTRY;
   resolve_next();
   if (!state.active || (!any_tempi(count, requests) && !p2p::busy()))
     return next.MPI_Testall(count, requests, flag, statuses);
@@ -205,6 +216,7 @@ TEMPI_EXPORT int MPI_Testall(int count, MPI_Request requests[], int *flag, MPI_S
 }
 
 TEMPI_EXPORT int MPI_Testany(int count, MPI_Request requests[], int *index, int *flag, MPI_Status *status) {
+  TEMPI_MT_ENTRY;
   resolve_next();
   if (!state.active || (!any_tempi(count, requests) && !p2p::busy()))
     return next.MPI_Testany(count, requests, index, flag, status);
@@ -233,18 +245,21 @@ TEMPI_EXPORT int MPI_Testany(int count, MPI_Request requests[], int *index, int 
 }
 
 TEMPI_EXPORT int MPI_Waitany(int count, MPI_Request requests[], int *index, MPI_Status *status) {
+  TEMPI_MT_ENTRY;
   resolve_next();
   if (!state.active || (!any_tempi(count, requests) && !p2p::busy()))
-    return next.MPI_Waitany(count, requests, index, status);
+    return TEMPI_UNLOCKED(next.MPI_Waitany(count, requests, index, status));
   for (;;) {
     int flag = 0;
     const int rc = MPI_Testany(count, requests, index, &flag, status);
     if (rc != MPI_SUCCESS || flag) return rc;
+    mt::yield();
   }
 }
 
 TEMPI_EXPORT int MPI_Testsome(int incount, MPI_Request requests[], int *outcount, int indices[],
                               MPI_Status statuses[]) {
+  TEMPI_MT_ENTRY;
   resolve_next();
   if (!state.active || (!any_tempi(incount, requests) && !p2p::busy()))
     return next.MPI_Testsome(incount, requests, outcount, indices, statuses);
@@ -266,16 +281,19 @@ TEMPI_EXPORT int MPI_Testsome(int incount, MPI_Request requests[], int *outcount
 
 TEMPI_EXPORT int MPI_Waitsome(int incount, MPI_Request requests[], int *outcount, int indices[],
                               MPI_Status statuses[]) {
+  TEMPI_MT_ENTRY;
   resolve_next();
   if (!state.active || (!any_tempi(incount, requests) && !p2p::busy()))
-    return next.MPI_Waitsome(incount, requests, outcount, indices, statuses);
+    return TEMPI_UNLOCKED(next.MPI_Waitsome(incount, requests, outcount, indices, statuses));
   for (;;) {
     const int rc = MPI_Testsome(incount, requests, outcount, indices, statuses);
     if (rc != MPI_SUCCESS || *outcount != 0) return rc;
+    mt::yield();
   }
 }
 
 TEMPI_EXPORT int MPI_Request_free(MPI_Request *request) {
+  TEMPI_MT_ENTRY;
   resolve_next();
   if (state.active && p2p::is_tempi_request(*request)) {
     p2p::release(request);
@@ -286,6 +304,7 @@ TEMPI_EXPORT int MPI_Request_free(MPI_Request *request) {
 
 // MPI_Request_get_status and MPI_Cancel: not interposed by the reference (F8)
 TEMPI_EXPORT int MPI_Request_get_status(MPI_Request request, int *flag, MPI_Status *status) {
+  TEMPI_MT_ENTRY;
   resolve_next();
   if (state.active && p2p::is_tempi_request(request)) return p2p::get_status(request, flag, status);
   if (state.active && p2p::busy()) p2p::progress();
@@ -293,6 +312,7 @@ TEMPI_EXPORT int MPI_Request_get_status(MPI_Request request, int *flag, MPI_Stat
 }
 
 TEMPI_EXPORT int MPI_Cancel(MPI_Request *request) {
+  TEMPI_MT_ENTRY;
   resolve_next();
   if (state.active && p2p::is_tempi_request(*request)) return p2p::cancel(*request);
   return next.MPI_Cancel(request);
@@ -306,6 +326,7 @@ TEMPI_EXPORT int MPI_Cancel(MPI_Request *request) {
 TEMPI_EXPORT int MPI_Sendrecv(const void *sendbuf, int sendcount, MPI_Datatype sendtype, int dest, int sendtag,
                               void *recvbuf, int recvcount, MPI_Datatype recvtype, int source, int recvtag,
                               MPI_Comm comm, MPI_Status *status) {
+  TEMPI_MT_ENTRY;
   resolve_next();
   TEMPI_RANGE("MPI_Sendrecv");
   p2p::Route sr, rr;
@@ -318,8 +339,8 @@ TEMPI_EXPORT int MPI_Sendrecv(const void *sendbuf, int sendcount, MPI_Datatype s
     p2p::self_spill(comm, dest);
     p2p::self_spill(comm, source);
     if (state.active && p2p::send_gated(comm, dest)) p2p::drain_sends(comm, dest); // keep send order
-    return next.MPI_Sendrecv(sendbuf, sendcount, sendtype, dest, sendtag, recvbuf, recvcount, recvtype, source,
-                             recvtag, comm, status);
+    return TEMPI_UNLOCKED(next.MPI_Sendrecv(sendbuf, sendcount, sendtype, dest, sendtag, recvbuf, recvcount, recvtype, source,
+                             recvtag, comm, status));
   }
   MPI_Request r = MPI_REQUEST_NULL, s = MPI_REQUEST_NULL;
   int rc = MPI_Irecv(recvbuf, recvcount, recvtype, source, recvtag, comm, &r);
@@ -336,17 +357,20 @@ TEMPI_EXPORT int MPI_Sendrecv(const void *sendbuf, int sendcount, MPI_Datatype s
 // may travel as a descriptor, so a probe reports the payload's size and a
 // matched receive lands the payload (p2p.hpp).
 TEMPI_EXPORT int MPI_Probe(int source, int tag, MPI_Comm comm, MPI_Status *status) {
+  TEMPI_MT_ENTRY;
   resolve_next();
   TEMPI_RANGE("MPI_Probe");
   return p2p::probe(source, tag, comm, nullptr, status);
 }
 
 TEMPI_EXPORT int MPI_Iprobe(int source, int tag, MPI_Comm comm, int *flag, MPI_Status *status) {
+  TEMPI_MT_ENTRY;
   resolve_next();
   return p2p::probe(source, tag, comm, flag, status);
 }
 
 TEMPI_EXPORT int MPI_Mprobe(int source, int tag, MPI_Comm comm, MPI_Message *message, MPI_Status *status) {
+  TEMPI_MT_ENTRY;
   resolve_next();
   TEMPI_RANGE("MPI_Mprobe");
   return p2p::mprobe(source, tag, comm, nullptr, message, status);
@@ -354,19 +378,22 @@ TEMPI_EXPORT int MPI_Mprobe(int source, int tag, MPI_Comm comm, MPI_Message *mes
 
 TEMPI_EXPORT int MPI_Improbe(int source, int tag, MPI_Comm comm, int *flag, MPI_Message *message,
                              MPI_Status *status) {
+  TEMPI_MT_ENTRY;
   resolve_next();
   return p2p::mprobe(source, tag, comm, flag, message, status);
 }
 
 TEMPI_EXPORT int MPI_Mrecv(void *buf, int count, MPI_Datatype datatype, MPI_Message *message, MPI_Status *status) {
+  TEMPI_MT_ENTRY;
   resolve_next();
   TEMPI_RANGE("MPI_Mrecv");
-  if (!state.active) return next.MPI_Mrecv(buf, count, datatype, message, status);
+  if (!state.active) return TEMPI_UNLOCKED(next.MPI_Mrecv(buf, count, datatype, message, status));
   return p2p::mrecv(buf, count, datatype, message, status);
 }
 
 TEMPI_EXPORT int MPI_Imrecv(void *buf, int count, MPI_Datatype datatype, MPI_Message *message,
                             MPI_Request *request) {
+  TEMPI_MT_ENTRY;
   resolve_next();
   if (!state.active) return next.MPI_Imrecv(buf, count, datatype, message, request);
   return p2p::imrecv(buf, count, datatype, message, request);
@@ -404,34 +431,40 @@ int mode_send(const void *buf, int count, MPI_Datatype datatype, int dest, int t
     if (mode == M::BUFFERED) return next.MPI_Ibsend(buf, count, datatype, dest, tag, comm, request);
     return next.MPI_Irsend(buf, count, datatype, dest, tag, comm, request);
   }
-  if (mode == M::SYNC) return next.MPI_Ssend(buf, count, datatype, dest, tag, comm);
-  if (mode == M::BUFFERED) return next.MPI_Bsend(buf, count, datatype, dest, tag, comm);
-  return next.MPI_Rsend(buf, count, datatype, dest, tag, comm);
+  if (mode == M::SYNC) return TEMPI_UNLOCKED(next.MPI_Ssend(buf, count, datatype, dest, tag, comm));
+  if (mode == M::BUFFERED) return TEMPI_UNLOCKED(next.MPI_Bsend(buf, count, datatype, dest, tag, comm));
+  return TEMPI_UNLOCKED(next.MPI_Rsend(buf, count, datatype, dest, tag, comm));
 }
 } // namespace
 
 TEMPI_EXPORT int MPI_Ssend(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm) {
+  TEMPI_MT_ENTRY;
   TEMPI_RANGE("MPI_Ssend");
   return mode_send(buf, count, datatype, dest, tag, comm, nullptr, p2p::SendMode::SYNC);
 }
 TEMPI_EXPORT int MPI_Bsend(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm) {
+  TEMPI_MT_ENTRY;
   TEMPI_RANGE("MPI_Bsend");
   return mode_send(buf, count, datatype, dest, tag, comm, nullptr, p2p::SendMode::BUFFERED);
 }
 TEMPI_EXPORT int MPI_Rsend(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm) {
+  TEMPI_MT_ENTRY;
   TEMPI_RANGE("MPI_Rsend");
   return mode_send(buf, count, datatype, dest, tag, comm, nullptr, p2p::SendMode::READY);
 }
 TEMPI_EXPORT int MPI_Issend(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm,
                             MPI_Request *request) {
+  TEMPI_MT_ENTRY;
   return mode_send(buf, count, datatype, dest, tag, comm, request, p2p::SendMode::SYNC);
 }
 TEMPI_EXPORT int MPI_Ibsend(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm,
                             MPI_Request *request) {
+  TEMPI_MT_ENTRY;
   return mode_send(buf, count, datatype, dest, tag, comm, request, p2p::SendMode::BUFFERED);
 }
 TEMPI_EXPORT int MPI_Irsend(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm,
                             MPI_Request *request) {
+  TEMPI_MT_ENTRY;
   return mode_send(buf, count, datatype, dest, tag, comm, request, p2p::SendMode::READY);
 }
 
@@ -440,9 +473,10 @@ TEMPI_EXPORT int MPI_Irsend(const void *buf, int count, MPI_Datatype datatype, i
 // gather has run, and the attached buffer must still be there then (the
 // library's own detach then waits for the library's copies to drain).
 TEMPI_EXPORT int MPI_Buffer_detach(void *buffer_addr, int *size) {
+  TEMPI_MT_ENTRY;
   resolve_next();
   if (state.active) p2p::drain_buffered();
-  return next.MPI_Buffer_detach(buffer_addr, size);
+  return TEMPI_UNLOCKED(next.MPI_Buffer_detach(buffer_addr, size));
 }
 
 // Persistent requests: TEMPI's while it is active beside a GPU (p2p.hpp:
@@ -466,26 +500,31 @@ int persistent_init(bool send, const void *buf, int count, MPI_Datatype datatype
 
 TEMPI_EXPORT int MPI_Send_init(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm,
                                MPI_Request *request) {
+  TEMPI_MT_ENTRY;
   resolve_next();
   return persistent_init(true, buf, count, datatype, dest, tag, comm, request, p2p::SendMode::STANDARD);
 }
 TEMPI_EXPORT int MPI_Ssend_init(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm,
                                 MPI_Request *request) {
+  TEMPI_MT_ENTRY;
   resolve_next();
   return persistent_init(true, buf, count, datatype, dest, tag, comm, request, p2p::SendMode::SYNC);
 }
 TEMPI_EXPORT int MPI_Bsend_init(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm,
                                 MPI_Request *request) {
+  TEMPI_MT_ENTRY;
   resolve_next();
   return persistent_init(true, buf, count, datatype, dest, tag, comm, request, p2p::SendMode::BUFFERED);
 }
 TEMPI_EXPORT int MPI_Rsend_init(const void *buf, int count, MPI_Datatype datatype, int dest, int tag, MPI_Comm comm,
                                 MPI_Request *request) {
+  TEMPI_MT_ENTRY;
   resolve_next();
   return persistent_init(true, buf, count, datatype, dest, tag, comm, request, p2p::SendMode::READY);
 }
 TEMPI_EXPORT int MPI_Recv_init(void *buf, int count, MPI_Datatype datatype, int source, int tag, MPI_Comm comm,
                                MPI_Request *request) {
+  TEMPI_MT_ENTRY;
   resolve_next();
   if (state.active && !gpu::available() && p2p::holds(source, tag, comm))
     LOG_WARN("MPI_Recv_init: a message it matches is held by an earlier MPI_Probe; the library's persistent "
@@ -494,12 +533,14 @@ TEMPI_EXPORT int MPI_Recv_init(void *buf, int count, MPI_Datatype datatype, int 
 }
 
 TEMPI_EXPORT int MPI_Start(MPI_Request *request) {
+  TEMPI_MT_ENTRY;
   resolve_next();
   if (state.active && p2p::is_tempi_request(*request)) return p2p::start(request);
   return next.MPI_Start(request);
 }
 
 TEMPI_EXPORT int MPI_Startall(int count, MPI_Request requests[]) {
+  TEMPI_MT_ENTRY;
   resolve_next();
   if (!state.active || !any_tempi(count, requests)) return next.MPI_Startall(count, requests);
   int err = MPI_SUCCESS;
@@ -522,6 +563,7 @@ TEMPI_EXPORT int MPI_Startall(int count, MPI_Request requests[]) {
 // receive type); otherwise the library's.
 TEMPI_EXPORT int MPI_Sendrecv_replace(void *buf, int count, MPI_Datatype datatype, int dest, int sendtag, int source,
                                       int recvtag, MPI_Comm comm, MPI_Status *status) {
+  TEMPI_MT_ENTRY;
   resolve_next();
   p2p::Route rr;
   if (state.active && count > 0 &&
@@ -536,6 +578,6 @@ TEMPI_EXPORT int MPI_Sendrecv_replace(void *buf, int count, MPI_Datatype datatyp
                         status);
   }
   if (state.active) p2p::self_spill(comm, source);
-  TEMPI_SPILL_THEN(dest, next.MPI_Sendrecv_replace(buf, count, datatype, dest, sendtag, source, recvtag, comm, status))
+  TEMPI_SPILL_THEN(dest, TEMPI_UNLOCKED(next.MPI_Sendrecv_replace(buf, count, datatype, dest, sendtag, source, recvtag, comm, status)))
 }
 #undef TEMPI_SPILL_THEN

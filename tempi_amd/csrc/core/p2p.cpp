@@ -7,6 +7,7 @@
 #include "env.hpp"
 #include "gpu.hpp"
 #include "log.hpp"
+#include "mt.hpp"
 #include "next_mpi.hpp"
 #include "packer.hpp"
 #include "perf_model.hpp"
@@ -352,11 +353,17 @@ int isend_host(const void *buf, int count, MPI_Datatype dt, int dest, int tag, M
 
 void drain_sends(MPI_Comm comm, int dest) {
   const uint64_t key = gate_key(comm, dest);
-  while (gate_busy(key)) progress();
+  while (gate_busy(key)) {
+    progress();
+    mt::yield();
+  }
 }
 
 void drain_buffered() {
-  while (bufferedUnposted > 0) progress();
+  while (bufferedUnposted > 0) {
+    progress();
+    mt::yield();
+  }
 }
 
 bool is_tempi_request(MPI_Request r) {
@@ -604,6 +611,8 @@ bool progress(bool full) {
 }
 
 // (idle persistent requests are not work; started ones have an inner request)
+int progress_depth() { return progressDepth; }
+
 bool busy() { return active.size() > size_t(persistent_count) || !pendingAcks.empty(); }
 
 namespace {
@@ -618,13 +627,14 @@ int finish_error(int err, MPI_Comm comm) {
 int wait(MPI_Request *req, MPI_Status *status) {
   const uint32_t h = uint32_t(*req);
   Op *op = find_op(*req);
-  if (!op) return next.MPI_Wait(req, status);
+  if (!op) return TEMPI_UNLOCKED(next.MPI_Wait(req, status));
   if (PersistentOp *p = op->persistent()) return persistent_wait(p, status);
   if (!op->done) {
     ScopedNs timer(counters.ns_wait);
     while (!op->done) {
       progress();
       if (!op->done) op->stalled();
+      if (!op->done) mt::yield();
     }
   }
   op->status(status);

@@ -166,6 +166,7 @@ int cancel(MPI_Request r);
 // queued so that a burst shares one launch; waits use full = true
 bool progress(bool full = true);
 bool busy(); // active operations or unacknowledged IPC slabs exist
+int progress_depth(); // progress() passes on this call stack (mt.cpp: no lock hand-off inside one)
 
 // complete a TEMPI request (blocking); fills status, sets *req to NULL
 int wait(MPI_Request *req, MPI_Status *status);

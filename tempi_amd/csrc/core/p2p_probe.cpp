@@ -7,6 +7,7 @@
 #include "env.hpp"
 #include "gpu.hpp"
 #include "log.hpp"
+#include "mt.hpp"
 #include "next_mpi.hpp"
 #include "packer.hpp"
 #include "perf_model.hpp"
@@ -82,13 +83,14 @@ int recv_host_ipc_aware(void *buf, int count, MPI_Datatype dt, int source, int t
     if (rc != MPI_SUCCESS) return rc;
     if (flag) break;
     progress();
+    mt::yield();
   }
   int n = 0;
   MPI_Get_count(&st, MPI_BYTE, &n);
   if (size_t(n) != sizeof(IpcDesc) && size_t(n) != sizeof(DirectDesc) && size_t(n) != sizeof(IpcCopyDesc))
-    return next.MPI_Mrecv(buf, count, dt, &msg, status);
+    return TEMPI_UNLOCKED(next.MPI_Mrecv(buf, count, dt, &msg, status));
   alignas(16) char raw[kDescCap];
-  next.MPI_Mrecv(raw, n, MPI_BYTE, &msg, &st);
+  TEMPI_UNLOCKED(next.MPI_Mrecv(raw, n, MPI_BYTE, &msg, &st));
   return land(raw, n, st);
 }
 
@@ -152,7 +154,8 @@ void report(const Probed &p, MPI_Status *status) {
 
 int probe(int source, int tag, MPI_Comm comm, int *flag, MPI_Status *status) {
   if (source == MPI_PROC_NULL || !state.active || !gpu::available()) // no descriptors can arrive
-    return flag ? next.MPI_Iprobe(source, tag, comm, flag, status) : next.MPI_Probe(source, tag, comm, status);
+    return flag ? next.MPI_Iprobe(source, tag, comm, flag, status)
+                : TEMPI_UNLOCKED(next.MPI_Probe(source, tag, comm, status));
   self_spill(comm, source);
   if (flag && busy()) progress(false);
   for (;;) {
@@ -166,7 +169,7 @@ int probe(int source, int tag, MPI_Comm comm, int *flag, MPI_Status *status) {
     MPI_Status st;
     int rc;
     if (!flag && !busy()) { // nothing of TEMPI's to keep moving: the library may block
-      rc = next.MPI_Probe(source, tag, comm, &st);
+      rc = TEMPI_UNLOCKED(next.MPI_Probe(source, tag, comm, &st));
       f = 1;
     } else {
       rc = next.MPI_Iprobe(source, tag, comm, &f, &st);
@@ -195,12 +198,14 @@ int probe(int source, int tag, MPI_Comm comm, int *flag, MPI_Status *status) {
       return MPI_SUCCESS;
     }
     progress();
+    mt::yield();
   }
 }
 
 int mprobe(int source, int tag, MPI_Comm comm, int *flag, MPI_Message *msg, MPI_Status *status) {
   if (source == MPI_PROC_NULL || !state.active || !gpu::available()) // no descriptors can arrive
-    return flag ? next.MPI_Improbe(source, tag, comm, flag, msg, status) : next.MPI_Mprobe(source, tag, comm, msg, status);
+    return flag ? next.MPI_Improbe(source, tag, comm, flag, msg, status)
+                : TEMPI_UNLOCKED(next.MPI_Mprobe(source, tag, comm, msg, status));
   self_spill(comm, source);
   if (flag && busy()) progress(false);
   auto claim = [&](std::unique_ptr<Probed> p) { // a TEMPI message handle, outside the library's handle space
@@ -220,7 +225,7 @@ int mprobe(int source, int tag, MPI_Comm comm, int *flag, MPI_Message *msg, MPI_
     MPI_Message m = MPI_MESSAGE_NULL;
     int rc;
     if (!flag && !busy()) {
-      rc = next.MPI_Mprobe(source, tag, comm, &m, &st);
+      rc = TEMPI_UNLOCKED(next.MPI_Mprobe(source, tag, comm, &m, &st));
       f = 1;
     } else {
       rc = next.MPI_Improbe(source, tag, comm, &f, &m, &st);
@@ -245,6 +250,7 @@ int mprobe(int source, int tag, MPI_Comm comm, int *flag, MPI_Message *msg, MPI_
       return MPI_SUCCESS;
     }
     progress();
+    mt::yield();
   }
 }
 
@@ -295,12 +301,12 @@ int mrecv(void *buf, int count, MPI_Datatype dt, MPI_Message *msg, MPI_Status *s
   Route route;
   if (!probedMsgs.count(uint32_t(*msg)) && !handles(buf, count, dt, 0, &route)) {
     libMsgComm.erase(*msg);
-    return next.MPI_Mrecv(buf, count, dt, msg, status); // the library's message into host memory
+    return TEMPI_UNLOCKED(next.MPI_Mrecv(buf, count, dt, msg, status)); // the library's message into host memory
   }
   MPI_Request r = MPI_REQUEST_NULL;
   const int rc = imrecv(buf, count, dt, msg, &r);
   if (rc != MPI_SUCCESS) return rc;
-  return is_tempi_request(r) ? wait(&r, status) : next.MPI_Wait(&r, status);
+  return is_tempi_request(r) ? wait(&r, status) : TEMPI_UNLOCKED(next.MPI_Wait(&r, status));
 }
 
 } // namespace p2p

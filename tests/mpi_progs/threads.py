@@ -1,17 +1,27 @@
 """Run under mpiexec -n 1 or -n 2: the thread level TEMPI reports, and
-MPI_THREAD_SERIALIZED use from several application threads.
+several application threads calling MPI at that level.
 
-MPI_Init_thread(REQUIRED) must report at most MPI_THREAD_SERIALIZED (TEMPI's
-transport state is not synchronised: interpose_core.cpp), the same level from
-MPI_Query_thread, and the library's own level with TEMPI_DISABLE=1. Then
-THREADS threads each run ITERS rounds of content-checked strided
-MPI_Isend / MPI_Irecv / MPI_Test to the peer rank (self at one rank), every
-MPI call made under one process-wide lock -- what SERIALIZED allows: calls from
-any thread, never two at once, requests started by one call completed by a
-later one (MPI_Test polling) of the same thread while the other thread's
-requests are in flight. --device puts the objects on the GPU (each thread its own, so the
-HIP device current on a thread that never selected one is exercised).
-usage: threads.py REQUIRED EXPECT [THREADS ITERS] [--device]"""
+MPI_Init_thread(REQUIRED) must report EXPECT, MPI_Query_thread the same:
+MPI_THREAD_MULTIPLE when it was asked for (TEMPI's calls then run under one
+process-wide lock, core/mt.hpp), at most MPI_THREAD_SERIALIZED otherwise,
+and the library's own level with TEMPI_DISABLE=1.
+
+Then THREADS threads each run ITERS content-checked rounds of strided
+MPI_Isend / MPI_Irecv to the peer rank (itself at one rank):
+  default       every MPI call under one Python lock -- what SERIALIZED
+                allows: calls from any thread, never two at once; requests
+                completed by MPI_Test polling while the other threads'
+                requests are in flight;
+  --concurrent  (MULTIPLE) no lock at all. Thread w sends with its own tag
+                and receives the message thread w+1 sends, then blocks in
+                MPI_Wait, so each wait depends on another thread getting into
+                TEMPI while it waits; each round also blocks in a host
+                MPI_Recv for a message another thread sends. A lock held
+                through a wait deadlocks here (the run is killed by the test's
+                timeout).
+--device puts the strided objects on the GPU (each thread on the HIP device
+it finds).
+usage: threads.py REQUIRED EXPECT [THREADS ITERS] [--device] [--concurrent]"""
 import os
 import sys
 import threading
@@ -27,6 +37,7 @@ from tests import typezoo  # noqa: E402
 
 args = [a for a in sys.argv[1:] if not a.startswith("--")]
 device = "--device" in sys.argv
+concurrent = "--concurrent" in sys.argv
 LEVELS = {"SINGLE": "THREAD_SINGLE", "FUNNELED": "THREAD_FUNNELED", "SERIALIZED": "THREAD_SERIALIZED",
           "MULTIPLE": "THREAD_MULTIPLE"}
 mpi = tempi_amd.get_mpi()
@@ -56,6 +67,7 @@ types = [typezoo.build(mpi, r) for r in recipes]
 maps = [pyoracle.TypeMap(r) for r in recipes]
 counts = [2, 3]
 werrors = [0] * threads_n
+HOSTN = 256
 
 
 def call(fn, *a):
@@ -64,13 +76,15 @@ def call(fn, *a):
 
 
 def worker(w):
-    if device:
-        import torch  # noqa: F811  (each thread uses the default device it finds)
-    k = w % len(recipes)
+    # concurrent: this thread sends as w and receives what thread w+1 sends,
+    # all threads with one shape; serialized: each thread with its own
+    partner = (w + 1) % threads_n if concurrent else w
+    k = 0 if concurrent else w % len(recipes)
     t, tm, count = types[k][0], maps[k], counts[k]
     origin, buflen = tm.geometry(count)
     for it in range(iters):
         seed = (w * 100003 + it) * 17
+        pseed = (partner * 100003 + it) * 17
         hsend = np.random.default_rng(seed + rank).integers(0, 256, buflen, dtype=np.uint8)
         canvas = np.random.default_rng(seed + 7).integers(0, 256, buflen, dtype=np.uint8)
         if device:
@@ -80,20 +94,35 @@ def worker(w):
         else:
             s, r = hsend, canvas.copy()
             sp, rp = s.ctypes.data, r.ctypes.data
-        tag = 100 + w  # one tag per thread: its messages pair up with the peer's same thread
-        rq = call(mpi.Irecv, rp + origin, count, t, src, tag)
-        sq = call(mpi.Isend, sp + origin, count, t, peer, tag)
-        # completed by MPI_Test polling: a blocking MPI_Wait under the lock
-        # would hold it while the peer's matching thread waits for this
-        # process's other thread (a deadlock of the application's making)
-        pending = [rq, sq] if it % 2 else [sq, rq]
-        while pending:
-            done, pending[0] = call(mpi.Test, pending[0])
-            if done:
-                pending.pop(0)
+        if concurrent:
+            sq = mpi.Isend(sp + origin, count, t, peer, 100 + w)
+            hs = np.random.default_rng(seed + 5 + rank).integers(0, 256, HOSTN, dtype=np.uint8)
+            hq = mpi.Isend(hs.ctypes.data, HOSTN, mpi.BYTE, peer, 300 + w)
+            rq = mpi.Irecv(rp + origin, count, t, src, 100 + partner)
+            mpi.Wait(rq)  # blocks until thread `partner` of rank src has sent
+            hr = np.zeros(HOSTN, dtype=np.uint8)
+            mpi.Recv(hr.ctypes.data, HOSTN, mpi.BYTE, src, 300 + partner)  # blocking, in the library
+            mpi.Wait(sq)
+            mpi.Wait(hq)
+            if not np.array_equal(hr, np.random.default_rng(pseed + 5 + src).integers(0, 256, HOSTN, dtype=np.uint8)):
+                werrors[w] += 1
+                if werrors[w] < 4:
+                    print(f"rank {rank} thread {w} iter {it}: host message wrong", flush=True)
+        else:
+            tag = 100 + w  # one tag per thread: its messages pair up with the peer's same thread
+            rq = call(mpi.Irecv, rp + origin, count, t, src, tag)
+            sq = call(mpi.Isend, sp + origin, count, t, peer, tag)
+            # completed by MPI_Test polling: a blocking MPI_Wait under the lock
+            # would hold it while the peer's matching thread waits for this
+            # process's other thread (a deadlock of the application's making)
+            pending = [rq, sq] if it % 2 else [sq, rq]
+            while pending:
+                done, pending[0] = call(mpi.Test, pending[0])
+                if done:
+                    pending.pop(0)
         got = r.cpu().numpy() if device else r
         exp = canvas.copy()
-        peer_src = np.random.default_rng(seed + src).integers(0, 256, buflen, dtype=np.uint8)
+        peer_src = np.random.default_rng(pseed + src).integers(0, 256, buflen, dtype=np.uint8)
         tm.unpack(tm.pack(peer_src, origin, count), exp, origin, count)
         if not np.array_equal(got, exp):
             werrors[w] += 1

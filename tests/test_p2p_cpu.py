@@ -128,18 +128,25 @@ def test_mpi_under_torchrun():
     assert r.returncode == 0 and r.stdout.count("RESULT ok") == 2, r.stdout[-3000:]
 
 
-@pytest.mark.parametrize("n,required,expect,env", [
-    (1, "MULTIPLE", "SERIALIZED", {"TEMPI_TEST_HOST_ONLY": "1"}),
-    (2, "MULTIPLE", "SERIALIZED", {"TEMPI_TEST_HOST_ONLY": "1"}),
-    (2, "SERIALIZED", "SERIALIZED", {"TEMPI_TEST_HOST_ONLY": "1"}),
-    (1, "FUNNELED", "FUNNELED", {"TEMPI_TEST_HOST_ONLY": "1"}),
-    (2, "MULTIPLE", "MULTIPLE", {"TEMPI_DISABLE": "1"})])
-def test_thread_level_is_truthful(n, required, expect, env):
-    """MPI_Init_thread / MPI_Query_thread report at most
-    MPI_THREAD_SERIALIZED while TEMPI is active (its transport state is not
-    synchronised; the reference only logs the level, /root/reference/src/
-    init.cpp:36-46), the library's level when TEMPI is disabled; then two
-    threads x 300 content-checked strided Isend / Irecv / Test rounds, the
-    MPI calls serialised as SERIALIZED requires"""
-    rc, out = mpi_launch.run(n, mpi_launch.py("threads.py", required, expect, "2", "300"), env=env, timeout=180)
+@pytest.mark.parametrize("n,required,expect,env,extra", [
+    (1, "SERIALIZED", "SERIALIZED", {"TEMPI_TEST_HOST_ONLY": "1"}, []),
+    (2, "SERIALIZED", "SERIALIZED", {"TEMPI_TEST_HOST_ONLY": "1"}, []),
+    (1, "FUNNELED", "FUNNELED", {"TEMPI_TEST_HOST_ONLY": "1"}, []),
+    (1, "MULTIPLE", "MULTIPLE", {"TEMPI_TEST_HOST_ONLY": "1"}, ["--concurrent"]),
+    (2, "MULTIPLE", "MULTIPLE", {"TEMPI_TEST_HOST_ONLY": "1"}, ["--concurrent"]),
+    (2, "MULTIPLE", "MULTIPLE", {"TEMPI_TEST_HOST_ONLY": "1"}, []),
+    (2, "MULTIPLE", "MULTIPLE", {"TEMPI_DISABLE": "1"}, ["--concurrent"])])
+def test_thread_level_is_truthful(n, required, expect, env, extra):
+    """the level MPI_Init_thread / MPI_Query_thread report
+    is one TEMPI is safe at (the reference only logs it, /root/reference/src/
+    init.cpp:36-46): MPI_THREAD_MULTIPLE when asked for -- TEMPI's calls then
+    run under one lock that waits and blocking library calls give up
+    (core/mt.hpp) -- and at most MPI_THREAD_SERIALIZED otherwise; the
+    library's level when TEMPI is disabled. Then threads x 200 content-checked
+    strided Isend / Irecv rounds: serialized under one application lock, or
+    (--concurrent, 3 threads) with no lock, each thread blocked in MPI_Wait
+    and MPI_Recv on messages other threads send"""
+    threads = "3" if "--concurrent" in extra else "2"
+    rc, out = mpi_launch.run(n, mpi_launch.py("threads.py", required, expect, threads, "200", *extra), env=env,
+                             timeout=180)
     assert rc == 0 and out.count("RESULT errors=0") == n, out[-3000:]

@@ -352,12 +352,24 @@ def test_placement_device(gpu, method):
 
 @pytest.mark.parametrize("n,method", [(1, "AUTO"), (2, "AUTO"), (2, "ONESHOT")])
 def test_serialized_threads_device(gpu, n, method):
-    """MPI_Init_thread(MULTIPLE) under TEMPI provides MPI_THREAD_SERIALIZED;
-    two application threads then take turns with strided device-object
-    Isend / Irecv / Test (each thread's requests in flight while the other
-    thread calls in), 300 rounds each, every byte checked"""
-    rc, out = mpi_launch.run(n, mpi_launch.py("threads.py", "MULTIPLE", "SERIALIZED", "2", "300", "--device"),
+    """MPI_Init_thread(SERIALIZED) under TEMPI: two application threads take
+    turns with strided device-object Isend / Irecv / Test (each thread's
+    requests in flight while the other thread calls in), 300 rounds each,
+    every byte checked"""
+    rc, out = mpi_launch.run(n, mpi_launch.py("threads.py", "SERIALIZED", "SERIALIZED", "2", "300", "--device"),
                              env=METHODS[method], timeout=240)
+    assert rc == 0 and out.count("RESULT errors=0") == n, out[-3000:]
+
+
+@pytest.mark.parametrize("n,method", [(1, "AUTO"), (2, "AUTO"), (2, "ONESHOT"), (2, "IPC")])
+def test_multiple_threads_device(gpu, n, method):
+    """MPI_Init_thread(MULTIPLE) under TEMPI provides MPI_THREAD_MULTIPLE
+    (core/mt.hpp): three threads with no application lock, each blocking in
+    MPI_Wait on a strided device message another thread sends and in a host
+    MPI_Recv, 200 rounds each, every byte checked -- a lock kept through a
+    wait would deadlock (the test's timeout)"""
+    rc, out = mpi_launch.run(n, mpi_launch.py("threads.py", "MULTIPLE", "MULTIPLE", "3", "200", "--device",
+                                              "--concurrent"), env=METHODS[method], timeout=240)
     assert rc == 0 and out.count("RESULT errors=0") == n, out[-3000:]
 
 
