@@ -14,7 +14,7 @@
  *
  *   symbol           replaces the reference's        TEMPI behaviour
  *   MPI_Init         src/init.cpp:22-65              resolve next MPI, env, GPU
- *   MPI_Init_thread  (not interposed: F8)            as MPI_Init; level capped at SERIALIZED
+ *   MPI_Init_thread  (not interposed: F8)            as MPI_Init; MULTIPLE under a lock, else <= SERIALIZED
  *   MPI_Query_thread (not interposed)                the same capped level
  *   MPI_Finalize     src/finalize.cpp:20-45          drain requests, free pools
  *   MPI_Type_commit  src/type_commit.cpp:16-114      canonicalise + cache
