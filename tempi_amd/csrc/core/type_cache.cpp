@@ -43,8 +43,11 @@ const TypeRecord *type_commit(MPI_Datatype t) {
   return slot.get();
 }
 
+// every MPI_Isend / MPI_Irecv / MPI_Pack looks its type up: no lock here.
+// Lookups run inside interposed calls, which never overlap at the levels TEMPI
+// reports (SERIALIZED, or MULTIPLE under TEMPI's own lock, mt.hpp), so they
+// cannot race with the commit or free that changes the cache.
 const TypeRecord *type_lookup(MPI_Datatype t) {
-  std::lock_guard<std::mutex> g(mtx);
   auto it = cache.find(t);
   return it == cache.end() ? nullptr : it->second.get();
 }

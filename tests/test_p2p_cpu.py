@@ -150,3 +150,13 @@ def test_thread_level_is_truthful(n, required, expect, env, extra):
     rc, out = mpi_launch.run(n, mpi_launch.py("threads.py", required, expect, threads, "200", *extra), env=env,
                              timeout=180)
     assert rc == 0 and out.count("RESULT errors=0") == n, out[-3000:]
+
+
+@pytest.mark.parametrize("n", [1, 2])
+def test_many_requests_in_flight(n):
+    """6 000 receives + 6 000 sends in flight per rank, completed in a
+    scrambled order by MPI_Wait / MPI_Test, twice: the direct-mapped request
+    table (core/p2p.cpp) grows past its first 4 096 slots and reuses handles,
+    every handle distinct while in flight, every byte checked"""
+    rc, out = mpi_launch.run(n, mpi_launch.py("manyreq.py", "6000"), env={"TEMPI_TEST_HOST_ONLY": "1"}, timeout=180)
+    assert rc == 0 and out.count("RESULT errors=0") == n, out[-3000:]
