@@ -357,9 +357,13 @@ TEMPI_EXPORT int MPI_Init_thread(int *argc, char ***argv, int required, int *pro
     init_after_mpi();
     if (provided && state.active) {
       mt::on = required == MPI_THREAD_MULTIPLE && *provided == MPI_THREAD_MULTIPLE;
+      // TEMPI_FAULT_NO_MT_LOCK (tools/cpu_tsan.sh's negative control): report
+      // MULTIPLE but leave the lock off, so that TSan shows what it guards
+      const bool unguarded = mt::on && std::getenv("TEMPI_FAULT_NO_MT_LOCK") != nullptr;
       if (mt::on && state.worldRank == 0)
         LOG_DEBUG("MPI_THREAD_MULTIPLE: TEMPI's calls run under one process-wide lock");
       *provided = cap_thread_level(*provided);
+      if (unguarded) mt::on = false;
     }
   }
   return rc;
