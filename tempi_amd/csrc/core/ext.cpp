@@ -4,6 +4,7 @@
 #include "counters.hpp"
 #include "env.hpp"
 #include "gpu.hpp"
+#include "mt.hpp"
 #include "p2p.hpp"
 #include "perf_model.hpp"
 #include "placement.hpp"
@@ -172,6 +173,7 @@ TEMPI_EXPORT int tempi_perf_source(char *path, int cap) {
 }
 
 TEMPI_EXPORT void tempi_perf_reload(void) {
+  TEMPI_MT_ENTRY;
   if (state.active) p2p::reload_perf_model();
 }
 
@@ -186,6 +188,7 @@ TEMPI_EXPORT int tempi_perf_roundtrip(const char *json_in, char *json_out, int c
 }
 
 TEMPI_EXPORT void tempi_set_datatype_method(int m) {
+  TEMPI_MT_ENTRY;
   // 0 AUTO, 1 ONESHOT, 2 DEVICE, 3 STAGED, 4 IPC (as TEMPI_DATATYPE_*)
   static const DatatypeMethod map[] = {DatatypeMethod::AUTO, DatatypeMethod::ONESHOT, DatatypeMethod::DEVICE,
                                        DatatypeMethod::STAGED, DatatypeMethod::IPC};
@@ -193,6 +196,7 @@ TEMPI_EXPORT void tempi_set_datatype_method(int m) {
 }
 
 TEMPI_EXPORT int tempi_choose_method(int64_t bytes, int64_t block, int colocated, int blocking, int *from_model) {
+  TEMPI_MT_ENTRY; // (TEMPI state: under the lock at MPI_THREAD_MULTIPLE)
   bool fm = false;
   const int m = state.active ? p2p::query_method(bytes, block, colocated != 0, blocking != 0, &fm) : 0;
   if (from_model) *from_model = fm ? 1 : 0;

@@ -75,7 +75,8 @@ int staged(const void *sendbuf, const int *scounts, const int *sdispls, MPI_Data
   if (r) gpu::check(tempi_hip_memcpy(hr->host, static_cast<char *>(recvbuf) + rlo, size_t(rhi - rlo)), "a2av D2H");
   const char *hsend = s ? static_cast<const char *>(hs->host) - slo : nullptr;
   char *hrecv = r ? static_cast<char *>(hr->host) - rlo : nullptr;
-  const int rc = TEMPI_UNLOCKED(next.MPI_Alltoallv(hsend, scounts, sdispls, stype, hrecv, rcounts, rdispls, rtype, comm));
+  const int rc =
+      TEMPI_UNLOCKED(next.MPI_Alltoallv(hsend, scounts, sdispls, stype, hrecv, rcounts, rdispls, rtype, comm));
   if (r) gpu::check(tempi_hip_memcpy(static_cast<char *>(recvbuf) + rlo, hr->host, size_t(rhi - rlo)), "a2av H2D");
   if (hs) pinned_pool().put(hs);
   if (hr) pinned_pool().put(hr);
@@ -206,8 +207,8 @@ TEMPI_EXPORT int MPI_Alltoallv(const void *sendbuf, const int sendcounts[], cons
   resolve_next();
   TEMPI_RANGE("MPI_Alltoallv");
   auto lib = [&] {
-    return TEMPI_UNLOCKED(next.MPI_Alltoallv(sendbuf, sendcounts, sdispls, sendtype, recvbuf, recvcounts, rdispls, recvtype,
-                              comm));
+    return TEMPI_UNLOCKED(next.MPI_Alltoallv(sendbuf, sendcounts, sdispls, sendtype, recvbuf, recvcounts, rdispls,
+                                             recvtype, comm));
   };
   if (!state.active || env.alltoallv == AlltoallvMethod::NONE || !gpu::available() || sendbuf == MPI_IN_PLACE)
     return lib();

@@ -273,8 +273,8 @@ TEMPI_EXPORT int MPI_Neighbor_alltoallw(const void *sendbuf, const int sendcount
   resolve_next();
   TEMPI_RANGE("MPI_Neighbor_alltoallw");
   auto lib = [&] {
-    return TEMPI_UNLOCKED(next.MPI_Neighbor_alltoallw(sendbuf, sendcounts, sdispls, sendtypes, recvbuf, recvcounts, rdispls,
-                                       recvtypes, comm));
+    return TEMPI_UNLOCKED(next.MPI_Neighbor_alltoallw(sendbuf, sendcounts, sdispls, sendtypes, recvbuf, recvcounts,
+                                                      rdispls, recvtypes, comm));
   };
   // every rank takes the per-edge route, whatever memory its own blocks are
   // in: its neighbours' device blocks travel on the private duplicate, which
@@ -292,8 +292,8 @@ TEMPI_EXPORT int MPI_Neighbor_alltoallv(const void *sendbuf, const int sendcount
   resolve_next();
   TEMPI_RANGE("MPI_Neighbor_alltoallv");
   auto lib = [&] {
-    return TEMPI_UNLOCKED(next.MPI_Neighbor_alltoallv(sendbuf, sendcounts, sdispls, sendtype, recvbuf, recvcounts, rdispls,
-                                       recvtype, comm));
+    return TEMPI_UNLOCKED(next.MPI_Neighbor_alltoallv(sendbuf, sendcounts, sdispls, sendtype, recvbuf, recvcounts,
+                                                      rdispls, recvtype, comm));
   };
   const Neighbours *nb = state.active && gpu::available() ? neighbours(comm) : nullptr;
   if (!nb) return lib();
@@ -321,8 +321,9 @@ TEMPI_EXPORT int MPI_Dist_graph_create_adjacent(MPI_Comm comm_old, int indegree,
   if (state.active && placement::create(comm_old, indegree, sources, sourceweights, outdegree, destinations,
                                         destweights, info, reorder, comm_dist_graph, &rc))
     return rc;
-  return TEMPI_UNLOCKED(next.MPI_Dist_graph_create_adjacent(comm_old, indegree, sources, sourceweights, outdegree, destinations,
-                                             destweights, info, reorder, comm_dist_graph));
+  return TEMPI_UNLOCKED(next.MPI_Dist_graph_create_adjacent(comm_old, indegree, sources, sourceweights, outdegree,
+                                                            destinations, destweights, info, reorder,
+                                                            comm_dist_graph));
 }
 
 TEMPI_EXPORT int MPI_Dist_graph_neighbors(MPI_Comm comm, int maxindegree, int sources[], int sourceweights[],

@@ -339,8 +339,8 @@ TEMPI_EXPORT int MPI_Sendrecv(const void *sendbuf, int sendcount, MPI_Datatype s
     p2p::self_spill(comm, dest);
     p2p::self_spill(comm, source);
     if (state.active && p2p::send_gated(comm, dest)) p2p::drain_sends(comm, dest); // keep send order
-    return TEMPI_UNLOCKED(next.MPI_Sendrecv(sendbuf, sendcount, sendtype, dest, sendtag, recvbuf, recvcount, recvtype, source,
-                             recvtag, comm, status));
+    return TEMPI_UNLOCKED(next.MPI_Sendrecv(sendbuf, sendcount, sendtype, dest, sendtag, recvbuf, recvcount,
+                                            recvtype, source, recvtag, comm, status));
   }
   MPI_Request r = MPI_REQUEST_NULL, s = MPI_REQUEST_NULL;
   int rc = MPI_Irecv(recvbuf, recvcount, recvtype, source, recvtag, comm, &r);
@@ -578,6 +578,7 @@ TEMPI_EXPORT int MPI_Sendrecv_replace(void *buf, int count, MPI_Datatype datatyp
                         status);
   }
   if (state.active) p2p::self_spill(comm, source);
-  TEMPI_SPILL_THEN(dest, TEMPI_UNLOCKED(next.MPI_Sendrecv_replace(buf, count, datatype, dest, sendtag, source, recvtag, comm, status)))
+  TEMPI_SPILL_THEN(dest, TEMPI_UNLOCKED(next.MPI_Sendrecv_replace(buf, count, datatype, dest, sendtag, source,
+                                                                   recvtag, comm, status)))
 }
 #undef TEMPI_SPILL_THEN
