@@ -690,6 +690,13 @@ template <int W, int ND> __global__ __launch_bounds__(kBlock) void unpack_il_ker
 #define TEMPI_DENSE_RATIO 4
 #endif
 constexpr int kDenseRatio = TEMPI_DENSE_RATIO;
+// Each lane's gather starts at a lane-dependent dword of its 16 bytes: without
+// that, lane L's k-th byte read sits near L * 16 * s / b, for s / b = 2 on 4
+// of a 32-lane group's banks (8-way conflicts; SQ_LDS_BANK_CONFLICT 7x lower
+// with the rotation, profiles/r05/dense_lds_pmc_s16.txt).
+#ifndef TEMPI_DENSE_ROT
+#define TEMPI_DENSE_ROT 1
+#endif
 constexpr int kDenseLds = kBlock * 16 * kDenseRatio + 512;
 constexpr int kDenseMaxBlock = 32;
 // a workgroup's window must fit the CU's 160 KiB of LDS with room for a
@@ -734,7 +741,47 @@ __device__ __forceinline__ void pack_dense_tile(const KArgs<ND> &a, uint32_t blk
     union {
       uint4 v;
       unsigned char b[16];
+      uint32_t d[4];
     } out;
+#if TEMPI_DENSE_ROT
+    // lanes 4k..4k+3 start their 16 bytes at dword k % 4 and wrap, so one
+    // ds_read_u8 instruction spreads its addresses over 4x more banks; the
+    // dwords are rotated back into place before the store
+    const uint32_t rot = (threadIdx.x >> 2) & 3, wrapAt = 16 - 4 * rot;
+    const uint32_t w0 = w;
+    const int64_t idx0 = idx;
+    {
+      const uint32_t qs = uint32_t(q0) + 4 * rot;
+      const uint32_t rs = mdiv(qs, a.mwpr);
+      w = qs - rs * a.wpr;
+      idx = int64_t(base) + int64_t(rs - rl) * stride + w;
+    }
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      if (uint32_t(m) == wrapAt) {
+        idx = idx0;
+        w = w0;
+      }
+      out.b[m] = w8[idx];
+      if (++w == a.wpr) {
+        w = 0;
+        idx += stride - int64_t(a.wpr) + 1;
+      } else {
+        ++idx;
+      }
+    }
+    // slot dword i holds output dword (i + rot) % 4
+    uint32_t d0 = out.d[0], d1 = out.d[1], d2 = out.d[2], d3 = out.d[3];
+    if (rot & 1) {
+      const uint32_t t = d3;
+      d3 = d2; d2 = d1; d1 = d0; d0 = t;
+    }
+    if (rot & 2) {
+      uint32_t t = d0; d0 = d2; d2 = t;
+      t = d1; d1 = d3; d3 = t;
+    }
+    out.d[0] = d0; out.d[1] = d1; out.d[2] = d2; out.d[3] = d3;
+#else
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       out.b[j] = w8[idx];
@@ -745,6 +792,7 @@ __device__ __forceinline__ void pack_dense_tile(const KArgs<ND> &a, uint32_t blk
         ++idx;
       }
     }
+#endif
     st_packed<WTC>(a.flags, reinterpret_cast<uint4 *>(a.chunk0 + size_t(c) * 16), out.v);
   } else { // first / last chunk of the object: only its bytes
     for (int j = 0; j < 16; ++j) {
