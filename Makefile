@@ -15,7 +15,7 @@ CORE_OBJ := $(patsubst tempi_amd/csrc/core/%.cpp,build/core/%.o,$(CORE_SRC))
 HIP_OBJ := $(patsubst tempi_amd/csrc/hip/%.hip,build/hip/%.o,$(HIP_SRC))
 
 HIPFLAGS := --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Iinclude -Wall
-CXXFLAGS := -std=c++17 -O2 -g -fPIC -fvisibility=hidden -Wall -Wextra -Wno-unused-parameter \
+CXXFLAGS := -std=c++17 -O2 -g1 -fPIC -fvisibility=hidden -Wall -Wextra -Wno-unused-parameter \
             -Iinclude -I$(MPI_HOME)/include
 
 APPS := $(LIB)/libtempi_apps.so $(LIB)/halo_exchange $(LIB)/pingpong_nd $(LIB)/pingpong_1d $(LIB)/alltoallv_sparse \
