@@ -71,7 +71,8 @@ static MPI_Datatype build(const rnode *r) {
     break;
   }
   case RK_INDEXED:
-  case RK_HINDEXED: {
+  case RK_HINDEXED:
+  case RK_STRUCT: {
     int n = r->narr[0];
     int *bl = malloc(sizeof(int) * (n ? n : 1));
     int *di = malloc(sizeof(int) * (n ? n : 1));
@@ -81,9 +82,14 @@ static MPI_Datatype build(const rnode *r) {
       di[i] = (int)r->arr[1][i];
       da[i] = (MPI_Aint)r->arr[1][i];
     }
-    if (r->kind == RK_INDEXED)
+    if (r->kind == RK_INDEXED) {
       MPI_Type_indexed(n, bl, di, c, &t);
-    else
+    } else if (r->kind == RK_STRUCT) {
+      MPI_Datatype *ty = malloc(sizeof(MPI_Datatype) * (n ? n : 1));
+      for (int i = 0; i < n; ++i) ty[i] = c;
+      MPI_Type_create_struct(n, bl, da, ty, &t);
+      free(ty);
+    } else
       MPI_Type_create_hindexed(n, bl, da, c, &t);
     free(bl);
     free(di);

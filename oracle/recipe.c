@@ -131,8 +131,8 @@ static rnode *parse_type(pstate *p) {
     n->a[0] = integer(p);
     expect(p, ',');
     n->a[1] = integer(p);
-  } else if (!strcmp(id, "indexed") || !strcmp(id, "hindexed")) {
-    n->kind = id[0] == 'i' ? RK_INDEXED : RK_HINDEXED;
+  } else if (!strcmp(id, "indexed") || !strcmp(id, "hindexed") || !strcmp(id, "struct")) {
+    n->kind = id[0] == 'i' ? RK_INDEXED : id[0] == 'h' ? RK_HINDEXED : RK_STRUCT;
     n->narr[0] = array(p, &n->arr[0]);
     expect(p, ',');
     n->narr[1] = array(p, &n->arr[1]);

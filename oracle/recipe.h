@@ -20,6 +20,9 @@
  *      | indexed_block(bl, [disp..], T)            MPI_Type_create_indexed_block
  *      | hindexed_block(bl, [disp_bytes..], T)     MPI_Type_create_hindexed_block
  *      | dup(T)                                    MPI_Type_dup
+ *      | struct([bl..], [disp_bytes..], T)         MPI_Type_create_struct, T for
+ *                                                  every block (the reference
+ *                                                  refuses struct, types.cpp:230)
  *   BASIC := byte | char | short | int | long | float | double
  *
  * The constructors are the ones the reference decodes in
@@ -47,7 +50,8 @@ enum rkind {
   RK_HINDEXED,
   RK_INDEXED_BLOCK,
   RK_HINDEXED_BLOCK,
-  RK_DUP
+  RK_DUP,
+  RK_STRUCT /* one child type for every block: the type map of HINDEXED */
 };
 
 typedef struct rnode {

@@ -99,6 +99,7 @@ static oracle_tm *build(const rnode *r) {
   }
   case RK_INDEXED:
   case RK_HINDEXED:
+  case RK_STRUCT: /* MPI-3.1 4.1.2: blocks of blen[k] copies at byte disp[k] */
     for (int k = 0; k < r->narr[0]; ++k) {
       const int64_t d = r->kind == RK_INDEXED ? r->arr[1][k] * e : r->arr[1][k];
       for (int64_t j = 0; j < r->arr[0][k]; ++j) append_copy(t, c, d + j * e);

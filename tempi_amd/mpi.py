@@ -197,6 +197,12 @@ class MPI:
         return self._newtype("MPI_Type_create_hindexed", n, (ctypes.c_int * max(n, 1))(*bls),
                              (ctypes.c_int64 * max(n, 1))(*disps), self.h(old))
 
+    def Type_create_struct(self, bls, disps, types):
+        n = len(bls)
+        return self._newtype("MPI_Type_create_struct", n, (ctypes.c_int * max(n, 1))(*bls),
+                             (ctypes.c_int64 * max(n, 1))(*disps),
+                             (self.Handle * max(n, 1))(*[self.h(t).value for t in types]))
+
     def Type_create_indexed_block(self, bl, disps, old):
         n = len(disps)
         return self._newtype("MPI_Type_create_indexed_block", n, bl, (ctypes.c_int * max(n, 1))(*disps),

@@ -6,7 +6,7 @@ object's origin misaligned and packing at a non-zero position.
 
 CPU: the oracle (oracle/typemap.c) against the image's MPICH 3.3.2 MPI_Pack /
 MPI_Unpack, in process, on every case -- the oracle's pin widened from the
-149 golden vectors (tests/test_oracle.py) to these shapes.
+153 golden vectors (tests/test_oracle.py) to these shapes.
 
 GPU: MPI_Pack / MPI_Unpack of device buffers through libtempi.so against the
 same MPICH calls on a host copy: bit-exact packed bytes, the same returned

@@ -21,7 +21,7 @@ from tests import typezoo
 pytestmark = pytest.mark.gpu
 
 CASES = G.cases()
-NOT_STRIDED = {"zoo_hi", "zoo_hib", "hindexed_irregular"}
+NOT_STRIDED = {"zoo_hi", "zoo_hib", "hindexed_irregular", "struct_irregular"}
 
 
 def _torch():

@@ -1,7 +1,7 @@
 """Seeded random MPI datatype recipes (grammar: oracle/recipe.h) for the
 parity fuzz: the constructors the reference decodes
 (/root/reference/src/internal/types.cpp: vector, hvector, subarray, contiguous,
-plus the resized / dup / indexed forms TEMPI canonicalises or hands to the
+plus the resized / dup / indexed / struct forms TEMPI canonicalises or hands to the
 library), nested up to three deep, with negative strides, resized extents,
 misaligned blocks and every named element size. Objects stay small (at most
 a few MiB per element) so hundreds of cases run in seconds."""
@@ -46,13 +46,16 @@ def _leaf(rng, budget):
         Z, Y, X = z + rng.randrange(0, 4), y + rng.randrange(0, 4), x + rng.choice([0, 3, 16])
         return (f"subarray(C,[{Z},{Y},{X}],[{z},{y},{x}],[{rng.randrange(0, Z - z + 1)},"
                 f"{rng.randrange(0, Y - y + 1)},{rng.randrange(0, X - x + 1)}],{name})", es, Z * Y * X * es)
-    if k == 4:  # regular hindexed_block / indexed_block (canonicalises to a vector)
+    if k == 4:  # regular hindexed_block / indexed_block / struct (canonicalises to a vector)
         n, bl = rng.randrange(1, 100), rng.choice([1, 2, 4, 9])
         st = bl + rng.choice([0, 2, 5])
-        if rng.random() < 0.5:
+        u = rng.random()
+        if u < 0.5:
             return f"indexed_block({bl},[{','.join(str(i * st) for i in range(n))}],{name})", es, n * st * es
-        return (f"hindexed_block({bl},[{','.join(str(i * st * es) for i in range(n))}],{name})", es,
-                n * st * es)
+        disps = ','.join(str(i * st * es) for i in range(n))
+        if u < 0.75:
+            return f"hindexed_block({bl},[{disps}],{name})", es, n * st * es
+        return f"struct([{','.join([str(bl)] * n)}],[{disps}],{name})", es, n * st * es
     # contiguous run
     n = rng.randrange(1, 2000)
     return f"contig({n},{name})", es, n * es

@@ -68,7 +68,7 @@ def parse(recipe):
         elif name == "resized":
             a = toks[i]; expect_comma(); b = toks[i]; i += 1
             args = (a, b)
-        elif name in ("indexed", "hindexed"):
+        elif name in ("indexed", "hindexed", "struct"):
             a = arr(); expect(","); b = arr()
             args = (a, b)
         elif name in ("indexed_block", "hindexed_block"):
@@ -118,6 +118,8 @@ def build(mpi, recipe, commit=True):
             t = mpi.Type_indexed(node[1], node[2], child)
         elif kind == "hindexed":
             t = mpi.Type_create_hindexed(node[1], node[2], child)
+        elif kind == "struct":
+            t = mpi.Type_create_struct(node[1], node[2], [child] * len(node[1]))
         elif kind == "indexed_block":
             t = mpi.Type_create_indexed_block(node[1], node[2], child)
         elif kind == "hindexed_block":

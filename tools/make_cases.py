@@ -132,6 +132,12 @@ def cases():
     add("indexed_regular", 1, "indexed([2,2,2,2],[0,5,10,15],int)")
     add("indexed_block_regular", 2, "indexed_block(3,[0,7,14],byte)")
     add("hindexed_irregular", 1, "hindexed([3,1,4],[0,9,20],byte)")
+    # MPI_Type_create_struct with one element type (the reference refuses
+    # every struct, src/internal/types.cpp:230; TEMPI folds these)
+    add("struct_regular", 2, "struct([4,4,4,4],[0,24,48,72],short)")
+    add("struct_of_vector", 1, "struct([1,1,1],[0,4000,8000],vector(30,3,10,byte))")
+    add("struct_irregular", 1, "struct([2,5,1],[0,40,100],int)")
+    add("struct_negative", 1, "struct([3,3],[64,-64],double)")
     add("nested_4level", 1, "hvector(2,1,5000,hvector(3,1,600,vector(4,5,30,byte)))")
     add("basic_double_x7", 7, "double")
     add("basic_byte_x1", 1, "byte")
