@@ -29,7 +29,7 @@ for step in "$@"; do
   echo "== $step $(date +%T)"
   case $step in
   tests)
-    timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 250 --timeout-method thread \
+    timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 250 --timeout-method thread --durations=25 \
       > $O/gpu_tests.log 2>&1
     rc=$?; tail -n 3 $O/gpu_tests.log; [ $rc -eq 0 ] || exit $rc ;;
   focus)
