@@ -679,91 +679,23 @@ def test_synchronous_ticket_visible_device_wide(mpi, gpu, rows, block, stride, f
         mpi.Type_free(t)
 
 
-def _hip():
-    """the HIP runtime libtempi_hip.so uses in this process. (When TEMPI is
-    loaded before torch, a PyTorch process holds two: ROCm's and torch's
-    bundled one, and each sees the other's pinned allocations as device
-    memory -- tools/diag_ptrattr.py)"""
-    import tempi_amd
-
-    ctypes.CDLL(tempi_amd.LIBTEMPI_HIP)
-    with open("/proc/self/maps") as f:
-        libs = sorted({line.split()[-1] for line in f if "libamdhip64" in line})
-    mine = [p for p in libs if "torch" not in p] or libs
-    hip = ctypes.CDLL(mine[0])
-    vp = ctypes.c_void_p
-    hip.hipHostMalloc.argtypes = [ctypes.POINTER(vp), ctypes.c_size_t, ctypes.c_uint]
-    hip.hipHostFree.argtypes = [vp]
-    hip.hipHostRegister.argtypes = [vp, ctypes.c_size_t, ctypes.c_uint]
-    hip.hipHostUnregister.argtypes = [vp]
-    return hip
-
-
-# (Round 4 kept the registered arrays alive for the whole session after one
-# illegal address in the next case's first pageable copy. Round 5 replayed
-# the sequence step by step -- tools/diag_registered.py, profiles/r05/
-# diag_registered_s8.jsonl: hipHostUnregister returns 0, both HIP runtimes
-# then see the range as plain host memory, a fresh array lands on the freed
-# address and both a pageable torch copy and TEMPI's staged MPI_Pack into it
-# are correct -- so the arrays are freed here again, as an application would.)
-
-
 @pytest.mark.parametrize("kind", ["noncoherent", "registered", "coherent"])
-def test_application_pinned_memory_waits_with_stream_sync(mpi, gpu, kind):
+def test_application_pinned_memory_waits_with_stream_sync(gpu, kind):
     """a kernel writing the APPLICATION's pinned host memory --
     hipHostMalloc(NonCoherent) (coarse-grained), a hipHostRegister'ed buffer,
     or coherent -- completes MPI_Pack (packed side there) and MPI_Unpack
     (strided object there) with hipStreamSynchronize, never a ticket; the
-    host reads the bytes right after the call, 40 rounds with fresh data."""
-    torch = _torch()
-    hip = _hip()
-    rows, block, stride = 4096, 24, 4608
-    n = rows * block
-    ext = (rows - 1) * stride + block
-    t = mpi.Type_commit(mpi.Type_vector(rows, block, stride, mpi.BYTE))
-    ptrs, arrays = [], []
+    host reads the bytes right after the call, 40 rounds with fresh data;
+    then the buffers are freed and fresh pageable arrays go through copies
+    and TEMPI's staged pack. Runs in a process of its own with one HIP runtime
+    (tests/mpi_progs/app_pinned.py): inside this process -- TEMPI's runtime
+    beside torch's bundled one -- registering, unregistering and freeing host
+    memory was followed by one illegal address at a later pageable copy in
+    round 4 and again in round 5 (profiles/r05/NOTES.md s21)."""
+    import subprocess
+    import sys
 
-    def host_buf(nbytes):
-        if kind == "registered":
-            a = np.zeros(nbytes + 4096, dtype=np.uint8)
-            p = (a.ctypes.data + 4095) & ~4095
-            assert hip.hipHostRegister(ctypes.c_void_p(p), nbytes, 0x2 | 0x1) == 0  # mapped, portable
-            arrays.append(a)
-            ptrs.append(("unreg", p))
-        else:
-            v = ctypes.c_void_p()
-            flags = 0x2 | 0x1 | (0x80000000 if kind == "noncoherent" else 0x40000000)
-            assert hip.hipHostMalloc(ctypes.byref(v), nbytes, flags) == 0
-            p = v.value
-            ptrs.append(("free", p))
-        return p, np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(p))
-
-    try:
-        hp, hview = host_buf(n)
-        sp, sview = host_buf(ext)
-        src = torch.empty(ext, dtype=torch.uint8, device=gpu)
-        c0 = mpi.counters()
-        rng = np.random.default_rng(5)
-        for r in range(40):
-            h = rng.integers(0, 256, ext, dtype=np.uint8)
-            src.copy_(torch.from_numpy(h))
-            torch.cuda.synchronize()
-            exp = np.lib.stride_tricks.as_strided(h, (rows, block), (stride, 1)).reshape(-1)
-            mpi.Pack(src.data_ptr(), 1, t, hp, n, 0)  # device object -> application pinned packed buffer
-            assert np.array_equal(hview, exp), f"round {r}: pack into {kind} host memory"
-            sview[:] = 0
-            pk = torch.from_numpy(exp.copy()).to(gpu)
-            torch.cuda.synchronize()
-            mpi.Unpack(pk.data_ptr(), n, 0, sp, 1, t)  # device packed -> application pinned object
-            got = np.lib.stride_tricks.as_strided(sview, (rows, block), (stride, 1)).reshape(-1)
-            assert np.array_equal(got, exp), f"round {r}: unpack into {kind} host memory"
-        c1 = mpi.counters()
-        assert c1["packs"] - c0["packs"] == 40 and c1["unpacks"] - c0["unpacks"] == 40  # the GPU path ran
-        assert c1["sync_waits"] - c0["sync_waits"] == 80 and c1["ticket_waits"] == c0["ticket_waits"]
-    finally:
-        mpi.Type_free(t)
-        torch.cuda.synchronize()
-        for how, p in ptrs:
-            rc = (hip.hipHostUnregister if how == "unreg" else hip.hipHostFree)(ctypes.c_void_p(p))
-            assert rc == 0, f"{how} of {p:#x}: hip error {rc}"
-        arrays.clear()  # (the registered arrays go back to malloc once unregistered)
+    root = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+    r = subprocess.run([sys.executable, os.path.join(root, "tests", "mpi_progs", "app_pinned.py"), kind], cwd=root,
+                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=200)
+    assert r.returncode == 0 and "RESULT ok" in r.stdout, r.stdout[-3000:]
