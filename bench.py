@@ -1044,7 +1044,7 @@ def sweep_traffic(specs):
     import sweep_pmc
 
     outdir = os.path.join(ROOT, "gpurun_out") if os.path.isdir(os.path.join(ROOT, "gpurun_out")) else None
-    recs = sweep_pmc.run(specs, outdir)
+    recs = sweep_pmc.run(specs, outdir, echo=False)  # (stdout carries the bench line only)
     keep = ("spec", "shape", "pack_model_over_counted", "unpack_model32_over_counted", "pack_frac_touched",
             "unpack_frac_touched", "pack_frac_counted", "unpack_frac_counted", "pack_rescored_frac_touched",
             "unpack_rescored_frac_touched", "counted", "model")

@@ -226,3 +226,28 @@ def test_shared_gpu_fractions_are_null():
     r = rec["halo"]["roofline"]
     assert r["frac"] is None and r["aggregate_frac"] is None and "note" in r
     assert all(q["xgmi_frac"] is None for q in rec["pingpong_1d"]["points"])
+
+
+def test_sweep_traffic_keeps_stdout_to_the_bench_line(monkeypatch, capsys):
+    """bench.py's stdout carries exactly one JSON line (the driver's
+    contract): the sweep counter check (tools/sweep_pmc.py) records its shapes
+    in the bench detail, never on stdout. Profiler and timing children are
+    replaced here by fixed numbers."""
+    import shutil
+
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import sweep_pmc
+
+    monkeypatch.setattr(shutil, "which", lambda name: "/usr/bin/" + name)
+    for k in [k for k in os.environ if k.startswith("ROCPROF")]:
+        monkeypatch.delenv(k)
+    monkeypatch.setenv("LD_PRELOAD", "")
+    info = {"planes": [1, 1000, 0, 0], "shape": "2d rows=1000 stride=40", "payload": 24000,
+            "pack_ms": 0.01, "unpack_ms": 0.02}
+    monkeypatch.setattr(sweep_pmc, "profile", lambda spec, counter, outdir: (info, {"pack": 20000.0, "unpack": 12000.0}))
+    monkeypatch.setattr(sweep_pmc, "timed", lambda spec: info)
+    recs = bench.sweep_traffic(["2:24:40"])
+    assert recs and recs[0]["spec"] == "2:24:40" and "pack_model_over_counted" in recs[0]
+    assert capsys.readouterr().out == ""
+    sweep_pmc.run(["2:24:40"], None)  # (the command line still prints its records)
+    assert json.loads(capsys.readouterr().out)["spec"] == "2:24:40"

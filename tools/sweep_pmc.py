@@ -142,7 +142,9 @@ def timed(spec):
     return json.loads(next(l for l in r.stdout.splitlines() if l.startswith("{")))
 
 
-def run(specs, outdir):
+def run(specs, outdir, echo=True):
+    """echo: one JSON line per spec on stdout (the command line); bench.py
+    passes False, its stdout carries exactly one line"""
     import bench
 
     recs = []
@@ -175,7 +177,8 @@ def run(specs, outdir):
         if rec["unpack_model32_over_counted"] > 1.10:
             rec["unpack_rescored_frac_touched"] = rec["unpack_frac_counted"]
         recs.append(rec)
-        print(json.dumps(rec), flush=True)
+        if echo:
+            print(json.dumps(rec), flush=True)
     return recs
 
 
