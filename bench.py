@@ -84,6 +84,21 @@ def parse():
     return p.parse_args()
 
 
+class stdout_to_stderr:
+    """fd 1 -> fd 2 for a block: torch's gloo backend prints its connection
+    messages on stdout, which carries the bench line only"""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+
+
 def dist_setup(args):
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -95,9 +110,11 @@ def dist_setup(args):
 
         from tempi_amd import pmi
 
-        dist.init_process_group("gloo", rank=rank, world_size=world)
-        pg = dist
-        keep = pmi.wire_torch_ranks(rank, world, dist)  # one MPI job over the torch ranks
+        with stdout_to_stderr():
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+            dist.barrier()
+            pg = dist
+            keep = pmi.wire_torch_ranks(rank, world, dist)  # one MPI job over the torch ranks
     return rank, world, local, pg, keep
 
 

@@ -17,7 +17,8 @@ echo "N=$N rc=$rc wall_s=$(python3 -c "print(round($t1-$t0,1))")"
 [ $rc -eq 0 ] || exit $rc
 python3 - $O/tr_$N.json <<'PY'
 import json, sys
-lines = [l for l in open(sys.argv[1]) if l.startswith("{")]
+lines = [l for l in open(sys.argv[1]) if l.strip()]
+assert len(lines) == 1 and lines[0].startswith("{"), f"stdout holds {len(lines)} lines besides the bench line"
 l = lines[-1].strip()
 d = json.loads(l)
 print("line bytes", len(l), "value", d["value"], "ms_per_step", d["ms_per_step"], "incomplete", d.get("incomplete"),
