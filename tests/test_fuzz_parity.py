@@ -1,7 +1,7 @@
 """Parity fuzz over seeded random datatypes (tests/typegen.py): vectors and
 hvectors with negative strides, 2-D / 3-D subarrays in C and Fortran order,
 regular (h)indexed blocks, resized extents with shifted lower bounds, dups and
-nestings of these, over every named element size, at counts 1-4, with the
+nestings of these, one-type structs, over every named element size, at counts 1-4, with the
 object's origin misaligned and packing at a non-zero position.
 
 CPU: the oracle (oracle/typemap.c) against the image's MPICH 3.3.2 MPI_Pack /
@@ -13,13 +13,17 @@ same MPICH calls on a host copy: bit-exact packed bytes, the same returned
 position, and an unpack that leaves every byte outside the type map alone.
 This is the reference's pack_unpack test (/root/reference/test/
 pack_unpack.cpp:61-118) run over random types instead of its fixed matrix."""
+import os
+
 import numpy as np
 import pytest
 
 from oracle import pyoracle
 from tests import typegen, typezoo
 
-CHUNKS = 40
+# TEMPI_FUZZ_CHUNKS widens a run (e.g. 1000 chunks = 50 000 types, a
+# one-off GPU session); the suite's default is 40
+CHUNKS = int(os.environ.get("TEMPI_FUZZ_CHUNKS", "40"))
 PER_CHUNK = 50
 
 
