@@ -4,7 +4,8 @@
 # tempi_amd/csrc/hip/), plus the kernel benches kbench / hbench.
 # An argument NAME:FLAGS instead builds the working tree with those compiler
 # flags (e.g. "nowave:-DTEMPI_WAVE_DECODE=0").
-# usage: tools/build_ab.sh [REF | NAME:FLAGS ...]   (then tools/kab.sh on the GPU box)
+# usage: tools/build_ab.sh [REF | NAME:FLAGS ...]   (then tools/kab.sh on the GPU box;
+# tools/_variants is listed in .gpurunignore: drop that line for the A/B session)
 set -e
 cd "$(dirname "$0")/.."
 mkdir -p tools/_variants
