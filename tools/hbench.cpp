@@ -14,6 +14,9 @@
 // Then (HBENCH_CONCURRENT=1) the x faces against the y + z faces: one after
 // the other on one stream, and side by side on two streams -- does the
 // x faces' isolated-line pattern overlap with the streaming faces?
+// HBENCH_SCHEDULE=1: all 26 regions' copies under several launch schedules
+// (one call, by class, chunks of HBENCH_CHUNK (32) on 1 / 2 lanes, x faces
+// apart) -- what batch composition costs the GPU.
 #include "tempi_hip.h"
 
 #include <chrono>
@@ -220,6 +223,92 @@ int main(int argc, char **argv) {
     std::printf("{\"lib\": \"%s\", \"class\": \"x_vs_yz\", \"x_items\": %zu, \"yz_items\": %zu, "
                 "\"sequential_us\": %.1f, \"concurrent_us\": %.1f}\n",
                 argv[1], xs.size(), yz.size(), ms[0] * 1e3, ms[1] * 1e3);
+  }
+  if (std::getenv("HBENCH_SCHEDULE")) {
+    // the 208 copies of one substep (all26, app order) under different
+    // launch schedules: how batch composition and chunking move the GPU time
+    std::vector<tempi_hip_copy_item> all;
+    std::vector<int> cls; // 0 x face, 1 y / z face, 2 edge, 3 corner
+    for (int qi = 0; qi < nq; ++qi)
+      for (const Region &R : regions) {
+        tempi_hip_copy_item cc{};
+        cc.dst = cc.src = R.desc;
+        cc.src_first = bufs[size_t(qi)] + R.srcOff;
+        cc.dst_first = bufs[size_t(qi)] + R.dstOff;
+        all.push_back(cc);
+        const int nz = (R.dx != 0) + (R.dy != 0) + (R.dz != 0);
+        cls.push_back(nz == 1 ? (R.dx ? 0 : 1) : nz == 2 ? 2 : 3);
+      }
+    const int chunk = std::getenv("HBENCH_CHUNK") ? std::atoi(std::getenv("HBENCH_CHUNK")) : 32;
+    std::vector<void *> lanes{s};
+    for (int i = 0; i < 2; ++i) {
+      void *t;
+      CK(tempi_hip_stream_create(&t));
+      lanes.push_back(t);
+    }
+    void *fork, *join[3];
+    CK(tempi_hip_event_create(&fork, 0));
+    for (auto &j : join) CK(tempi_hip_event_create(&j, 0));
+    SYM(tempi_hip_stream_wait_event)
+    typedef std::vector<std::vector<tempi_hip_copy_item>> Chunks;
+    auto chunked = [&](const std::vector<tempi_hip_copy_item> &v, int n) {
+      Chunks c;
+      for (size_t i = 0; i < v.size(); i += size_t(n))
+        c.emplace_back(v.begin() + long(i), v.begin() + long(std::min(v.size(), i + size_t(n))));
+      return c;
+    };
+    std::vector<tempi_hip_copy_item> byClass, xs, rest;
+    for (int k = 0; k < 4; ++k)
+      for (size_t i = 0; i < all.size(); ++i)
+        if (cls[i] == k) byClass.push_back(all[i]);
+    for (size_t i = 0; i < all.size(); ++i) (cls[i] == 0 ? xs : rest).push_back(all[i]);
+    struct Sched {
+      const char *name;
+      Chunks chunks;
+      int nl;
+    };
+    std::vector<Sched> scheds = {
+        {"one_call_app_order", {all}, 1},
+        {"one_call_by_class", {byClass}, 1},
+        {"chunks_app_order_1lane", chunked(all, chunk), 1},
+        {"chunks_app_order_2lanes", chunked(all, chunk), 2},
+        {"chunks_by_class_2lanes", chunked(byClass, chunk), 2},
+        {"x_one_call_then_rest_chunks_1lane", {}, 1},
+        {"x_lane_rest_lane", {}, 2},
+    };
+    scheds[5].chunks.push_back(xs);
+    for (auto &c : chunked(rest, chunk)) scheds[5].chunks.push_back(c);
+    scheds[6].chunks = scheds[5].chunks; // x on lane 0, every rest chunk on lane 1
+    for (Sched &S : scheds) {
+      const bool xlane = std::strcmp(S.name, "x_lane_rest_lane") == 0;
+      auto run = [&]() -> int {
+        if (S.nl > 1) {
+          if (int e = tempi_hip_event_record(fork, s)) return e;
+          for (int l = 1; l < S.nl; ++l)
+            if (int e = tempi_hip_stream_wait_event(lanes[size_t(l)], fork)) return e;
+        }
+        for (size_t i = 0; i < S.chunks.size(); ++i) {
+          const size_t lane = xlane ? (i == 0 ? 0 : 1) : i % size_t(S.nl);
+          if (int e = tempi_hip_copy_batch(S.chunks[i].data(), int(S.chunks[i].size()), lanes[lane])) return e;
+        }
+        for (int l = 1; l < S.nl; ++l) {
+          if (int e = tempi_hip_event_record(join[l], lanes[size_t(l)])) return e;
+          if (int e = tempi_hip_stream_wait_event(s, join[l])) return e;
+        }
+        return 0;
+      };
+      CK(run());
+      CK(run());
+      CK(tempi_hip_event_record(e0, s));
+      for (int i = 0; i < reps; ++i) CK(run());
+      CK(tempi_hip_event_record(e1, s));
+      CK(tempi_hip_event_synchronize(e1));
+      float ms = 0;
+      CK(tempi_hip_event_elapsed_ms(&ms, e0, e1));
+      std::printf("{\"lib\": \"%s\", \"schedule\": \"%s\", \"chunk\": %d, \"launch_calls\": %zu, \"copy_us\": %.1f}\n",
+                  argv[1], S.name, chunk, S.chunks.size(), double(ms) * 1e3 / reps);
+      std::fflush(stdout);
+    }
   }
   return 0;
 }
