@@ -275,10 +275,13 @@ int main(int argc, char **argv) {
         {"chunks_by_class_2lanes", chunked(byClass, chunk), 2},
         {"x_one_call_then_rest_chunks_1lane", {}, 1},
         {"x_lane_rest_lane", {}, 2},
+        {"rest_chunks_2lanes_then_x_joined", {}, 2},
     };
     scheds[5].chunks.push_back(xs);
     for (auto &c : chunked(rest, chunk)) scheds[5].chunks.push_back(c);
     scheds[6].chunks = scheds[5].chunks; // x on lane 0, every rest chunk on lane 1
+    scheds[7].chunks = chunked(rest, chunk);
+    scheds[7].chunks.push_back(xs); // (issued on s after both lanes joined)
     for (Sched &S : scheds) {
       const bool xlane = std::strcmp(S.name, "x_lane_rest_lane") == 0;
       auto run = [&]() -> int {
@@ -287,7 +290,9 @@ int main(int argc, char **argv) {
           for (int l = 1; l < S.nl; ++l)
             if (int e = tempi_hip_stream_wait_event(lanes[size_t(l)], fork)) return e;
         }
-        for (size_t i = 0; i < S.chunks.size(); ++i) {
+        const bool xlast = std::strcmp(S.name, "rest_chunks_2lanes_then_x_joined") == 0;
+        const size_t nchunks = S.chunks.size() - (xlast ? 1 : 0);
+        for (size_t i = 0; i < nchunks; ++i) {
           const size_t lane = xlane ? (i == 0 ? 0 : 1) : i % size_t(S.nl);
           if (int e = tempi_hip_copy_batch(S.chunks[i].data(), int(S.chunks[i].size()), lanes[lane])) return e;
         }
@@ -295,6 +300,7 @@ int main(int argc, char **argv) {
           if (int e = tempi_hip_event_record(join[l], lanes[size_t(l)])) return e;
           if (int e = tempi_hip_stream_wait_event(s, join[l])) return e;
         }
+        if (xlast) return tempi_hip_copy_batch(S.chunks.back().data(), int(S.chunks.back().size()), s);
         return 0;
       };
       CK(run());
