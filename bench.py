@@ -143,6 +143,63 @@ def allreduce_sum(pg, x):
     return float(t.item())
 
 
+def allreduce_sum_vec(pg, xs):
+    if pg is None:
+        return list(xs)
+    import torch
+
+    t = torch.tensor(list(xs), dtype=torch.float64)
+    pg.all_reduce(t, op=pg.ReduceOp.SUM)
+    return [float(v) for v in t.tolist()]
+
+
+_ROUTES = (("ipc", "send_ipc", "bytes_ipc"), ("ipc_copy", "send_ipc_copy", "bytes_ipc_copy"),
+           ("oneshot", "send_oneshot", "bytes_oneshot"), ("staged", "send_staged", "bytes_staged"),
+           ("device", "send_device", "bytes_device"), ("direct", "send_direct", "bytes_direct"))
+
+
+def transport_block(mpi, pg, before, after, shared_gpu, what):
+    """what the transport did over `what`, summed over all
+    ranks -- per-route message and payload-byte counts (IPC includes IPC COPY,
+    which is also counted on its own), device-object messages handed to the
+    library, first-contact canaries, the IPC threshold non-blocking AUTO sends
+    used and whether it came from a perf.json measured on this node. Fields
+    that need ranks on separate GPUs are null with the reason."""
+    import ctypes
+
+    d = {k: after[k] - before[k] for k in after}
+    keys = [k for _, m, b in _ROUTES for k in (m, b)] + ["lib_sends", "self_matched", "canary_ok", "canary_fail",
+                                                         "batches", "ticket_batches"]
+    tot = dict(zip(keys, (int(v) for v in allreduce_sum_vec(pg, [d.get(k, 0) for k in keys]))))
+    out = {"over": what, "routes": {name: {"messages": tot[m], "bytes": tot[b]} for name, m, b in _ROUTES},
+           "library_sends": tot["lib_sends"], "self_matched": tot["self_matched"], "batches": tot["batches"],
+           "ticket_batches": tot["ticket_batches"]}
+    if shared_gpu:
+        out["canary_ok"] = out["canary_fail"] = None
+        out["canary_note"] = ("shared GPU: every peer is on this rank's own GPU, so no first-contact canary (a peer "
+                              "on ANOTHER GPU read back over xGMI) can run")
+    else:
+        out["canary_ok"], out["canary_fail"] = tot["canary_ok"], tot["canary_fail"]
+    L = mpi.L
+    L.tempi_ipc_threshold.restype = ctypes.c_int64
+    L.tempi_ipc_threshold.argtypes = [ctypes.c_int64, ctypes.POINTER(ctypes.c_int)]
+    th = {}
+    fm = ctypes.c_int(0)
+    for bl in (24, 512):  # the halo's x-face rows and (capped) y / z-face rows
+        t = L.tempi_ipc_threshold(bl, ctypes.byref(fm))
+        th[f"block_{bl}"] = None if t == (1 << 63) - 1 else int(t)  # (null: never IPC)
+    out["ipc_threshold"] = dict(th, from_node_perf_json=bool(fm.value))
+    buf = ctypes.create_string_buffer(4096)
+    L.tempi_perf_source.argtypes = [ctypes.c_char_p, ctypes.c_int]
+    loaded = L.tempi_perf_source(buf, 4096)
+    src = buf.value.decode() if loaded == 1 else ""
+    out["perf_json_measured_on_node"] = bool(src) and os.path.abspath(src) == os.path.abspath(
+        os.path.join(tempi_cache_dir(), "perf.json"))
+    if shared_gpu:
+        out["perf_json_note"] = "shared GPU: a node perf.json measured here never crossed xGMI"
+    return out
+
+
 def make_2d(mpi, rows, pitch, block):
     t = mpi.Type_create_subarray([rows, pitch], [rows, block], [0, 0], mpi.ORDER_C, mpi.BYTE)
     return mpi.Type_commit(t)
@@ -1226,6 +1283,14 @@ def _compact_sections(rec, shared_gpu):
             continue
         out[name] = _err(p) or {"cols": list(cols), "points": [[_sig(q.get(k)) for k in cols] for q in p["points"]],
                                 "errors": sum(q.get("errors", 0) for q in p["points"])}
+    t = rec.get("transport")
+    if t:
+        out["transport"] = _err(t) or {
+            "routes": {k: [v["messages"], v["bytes"]] for k, v in t["routes"].items() if v["messages"]},
+            "library_sends": t["library_sends"], "canary_ok": t["canary_ok"], "canary_fail": t["canary_fail"],
+            "ipc_threshold": t["ipc_threshold"], "perf_json_measured_on_node": t["perf_json_measured_on_node"]}
+        if t.get("canary_note"):
+            out["transport"]["null_because"] = "shared GPU"
     if rec.get("perf_model"):
         pm = rec["perf_model"]
         out["perf_model"] = _err(pm) or {"measured_here": pm.get("measured_here"),
@@ -1234,7 +1299,8 @@ def _compact_sections(rec, shared_gpu):
 
 
 # sections dropped, in this order, if the line is still over LINE_LIMIT
-_DROP_ORDER = ("mpi_pack", "type_commit", "perf_model", "cpu_baselines_configs_3_5", "halo_weak", "nbr_alltoallv",
+_DROP_ORDER = ("mpi_pack", "type_commit", "perf_model", "cpu_baselines_configs_3_5", "halo_weak", "transport",
+               "nbr_alltoallv",
                "pingpong_1d", "alltoallv", "pingpong", "config1", "sweep")
 
 
@@ -1286,15 +1352,18 @@ DETAIL_NAME = None  # --detail-name
 
 
 def write_detail(rec, world):
-    """the full record, next to the line (gpurun_out/ is merged back from
-    the GPU box); returns the path relative to the repo, or None"""
+    """the full record, next to the line (gpurun_out/ is merged back from a
+    builder's GPU session); returns the path relative to the repo for the
+    line's "detail" key only when --detail-name named it: the driver's own
+    run does not retrieve gpurun_out/, so its line names no file it cannot
+    read"""
     d = os.path.join(ROOT, "gpurun_out")
     path = os.path.join(d, os.path.basename(DETAIL_NAME or f"bench_detail_n{world}.json"))
     try:
         os.makedirs(d, exist_ok=True)
         with open(path, "w") as f:
             json.dump(rec, f, indent=1)
-        return os.path.relpath(path, ROOT)
+        return os.path.relpath(path, ROOT) if DETAIL_NAME else None
     except OSError:
         return None
 
@@ -1380,13 +1449,20 @@ def main():
             pm = sec.run("perf_model", node_perf_model, args, mpi, pg, rank, world, shared_gpu)
             if rank == 0:
                 rec["perf_model"] = pm
+        c_start = mpi.counters() if world > 1 else None
         if not args.no_halo:
             barrier(pg)
             snap0 = xgmi_snapshot() if world > 1 and rank == 0 else None
+            c_halo0 = mpi.counters() if world > 1 else None
             t0 = time.perf_counter()
             h = sec.run("halo", halo, args, mpi, world)
             barrier(pg)
             el = time.perf_counter() - t0
+            if world > 1:
+                tb = sec.run("transport", transport_block, mpi, pg, c_halo0, mpi.counters(), shared_gpu,
+                             "the halo section (config 4), all ranks")
+                if rank == 0 and h and "error" not in h:
+                    h["transport"] = tb
             if rank == 0:
                 rec["halo"] = h
                 if world > 1 and h and "error" not in h:
@@ -1416,6 +1492,13 @@ def main():
                 rec["pingpong_1d"] = p1
                 rec["alltoallv"] = a2
                 rec["nbr_alltoallv"] = na
+        if world > 1:
+            barrier(pg)
+            tr = sec.run("transport", transport_block, mpi, pg, c_start, mpi.counters(), shared_gpu,
+                         "every N > 1 section (halo, halo_weak, pingpong, pingpong_1d, alltoallv, nbr_alltoallv), "
+                         "all ranks")
+            if rank == 0:
+                rec["transport"] = tr
         if rank == 0 and world == 1:
             if not args.no_traffic:
                 tr = sec.run("traffic", run_traffic_passes, args, "pack_kernel")

@@ -55,6 +55,9 @@ typedef struct tempi_counters_t {
   uint64_t batches;        /* transport batches launched (gathers, scatters, copies) */
   uint64_t gpu_inflight_ns; /* time with a transport batch in flight: from its launch's return to its
                                completion observed by the host (the GPU's busy time, by TEMPI's account) */
+  /* payload bytes of device-object sends by route: IPC (IPC COPY included,
+     and counted again on its own), ONESHOT, STAGED, DEVICE, DIRECT (this process) */
+  uint64_t bytes_ipc, bytes_ipc_copy, bytes_oneshot, bytes_staged, bytes_device, bytes_direct;
 } tempi_counters_t;
 void tempi_get_counters(tempi_counters_t *out);
 void tempi_reset_counters(void);
@@ -81,6 +84,13 @@ int64_t tempi_mpi_constant(const char *name, int *found);
 
 const char *tempi_version(void);
 
+/* the HIP runtimes (distinct libamdhip64 objects) mapped into this process,
+   as ';'-separated paths into paths[cap]; returns their number. More than
+   one (e.g. a PyTorch wheel's bundled runtime beside ROCm's) is reported
+   once at MPI_Init: streams of different runtimes are not ordered with each
+   other. */
+int tempi_hip_runtimes(char *paths, int cap);
+
 /* perf model (include the reference's interpolation rules,
    /root/reference/src/internal/measure_system.cpp:184-293):
    times[i] = seconds for 2^i bytes; table[r*cols+c] = seconds for 2^(2r+6)
@@ -96,6 +106,16 @@ int tempi_perf_source(char *path, int cap);
 /* re-read the model, e.g. after apps/measure_system wrote this node's
    perf.json (call on every rank) */
 void tempi_perf_reload(void);
+/* the message size from which a NON-blocking AUTO send of `block`-byte
+   blocks to a co-located peer takes IPC instead of ONESHOT: priced per batch
+   from this node's own TEMPI_CACHE_DIR/perf.json when one was measured here
+   (*from_model = 1), else the built-in 4096 (*from_model = 0). INT64_MAX:
+   never IPC; -1 before MPI_Init. */
+int64_t tempi_ipc_threshold(int64_t block, int *from_model);
+/* the same pricing over a perf.json document (no MPI needed): the threshold,
+   INT64_MAX for never, -1 when a curve it needs is missing, -2 when the
+   document does not parse */
+int64_t tempi_batch_ipc_threshold(const char *perf_json, int64_t block);
 /* parse + re-emit a perf.json document (schema check); 0 on success */
 int tempi_perf_roundtrip(const char *json_in, char *json_out, int cap);
 /* override TEMPI_DATATYPE_* at run time: 0 AUTO, 1 ONESHOT, 2 DEVICE,

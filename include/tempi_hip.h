@@ -119,6 +119,12 @@ int tempi_hip_copy_batch_ticket(const tempi_hip_copy_item *items, int n, void *s
 
 /* number of packed bytes a descriptor describes */
 int64_t tempi_hip_desc_bytes(const tempi_hip_desc *d);
+/* the word width (1,2,4,8,16) the strided -> strided copy kernel will use for
+   this item; 0 = 16-byte chunks with 8-byte halves at row seams (both sides
+   8 bytes past a 16-byte boundary, blocks and strides multiples of 16);
+   -1 when the copy is unsupported (tempi_hip_copy_supported) */
+int tempi_hip_copy_word_width(void *dst_first, const void *src_first, const tempi_hip_desc *dst,
+                              const tempi_hip_desc *src);
 /* the word width (1,2,4,8,16) the kernels will use for these pointers */
 int tempi_hip_word_width(const void *packed, const void *first,
                          const tempi_hip_desc *d);

@@ -35,6 +35,11 @@ struct Counters {
   // the remote-load kernel agreed with a DMA read (ok) or did not (fail)
   uint64_t canary_ok = 0, canary_fail = 0;
   uint64_t self_matched = 0; // messages to this process matched in TEMPI's self channel
+  // payload bytes of device-object sends by route: IPC
+  // (IPC COPY included, and counted again on its own), ONESHOT, STAGED,
+  // DEVICE (a GPU-aware library) and DIRECT (this same process)
+  uint64_t bytes_ipc = 0, bytes_ipc_copy = 0, bytes_oneshot = 0, bytes_staged = 0, bytes_device = 0,
+           bytes_direct = 0;
   // kernel time of synchronous MPI_Pack / MPI_Unpack while profiling is on
   double pack_kernel_ms = 0, unpack_kernel_ms = 0;
   uint64_t pack_timed = 0, unpack_timed = 0;

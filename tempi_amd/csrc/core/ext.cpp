@@ -20,7 +20,11 @@
 
 using namespace tempi;
 
+// Every entry point that reads TEMPI state a concurrent interposed call may
+// change (the type table, counters, the perf model, placement) takes TEMPI's
+// lock at MPI_THREAD_MULTIPLE, as the interposed calls do.
 TEMPI_EXPORT int tempi_type_describe(int64_t datatype, tempi_type_info *out) {
+  TEMPI_MT_ENTRY;
   std::memset(out, 0, sizeof *out);
   const TypeRecord *rec = type_lookup(MPI_Datatype(datatype));
   if (!rec) return 0;
@@ -45,6 +49,7 @@ TEMPI_EXPORT int tempi_type_describe(int64_t datatype, tempi_type_info *out) {
 }
 
 TEMPI_EXPORT void tempi_get_counters(tempi_counters_t *o) {
+  TEMPI_MT_ENTRY;
   const Counters &c = counters;
   o->packs = c.packs;
   o->unpacks = c.unpacks;
@@ -80,9 +85,16 @@ TEMPI_EXPORT void tempi_get_counters(tempi_counters_t *o) {
   o->persistent_starts = c.persistent_starts;
   o->batches = c.batches;
   o->gpu_inflight_ns = c.ns_gpu_inflight;
+  o->bytes_ipc = c.bytes_ipc;
+  o->bytes_ipc_copy = c.bytes_ipc_copy;
+  o->bytes_oneshot = c.bytes_oneshot;
+  o->bytes_staged = c.bytes_staged;
+  o->bytes_device = c.bytes_device;
+  o->bytes_direct = c.bytes_direct;
 }
 
 TEMPI_EXPORT void tempi_reset_counters(void) {
+  TEMPI_MT_ENTRY;
   settle_kernel_times(); // (pending pairs belong to the counters being reset)
   counters = Counters();
 }
@@ -92,6 +104,7 @@ TEMPI_EXPORT void tempi_set_kernel_profiling(int on) {
 }
 
 TEMPI_EXPORT void tempi_get_kernel_times(tempi_kernel_times *o) {
+  TEMPI_MT_ENTRY;
   settle_kernel_times();
   o->pack_ms = counters.pack_kernel_ms;
   o->unpack_ms = counters.unpack_kernel_ms;
@@ -102,6 +115,14 @@ TEMPI_EXPORT void tempi_get_kernel_times(tempi_kernel_times *o) {
 TEMPI_EXPORT void *tempi_get_stream(int device) { return gpu::available() ? gpu::stream(device) : nullptr; }
 
 TEMPI_EXPORT int tempi_gpu_available(void) { return gpu::available() ? 1 : 0; }
+
+TEMPI_EXPORT int tempi_hip_runtimes(char *paths, int cap) {
+  const std::vector<std::string> rt = gpu::hip_runtimes();
+  std::string all;
+  for (const std::string &r : rt) all += (all.empty() ? "" : ";") + r;
+  if (paths && cap > 0) std::snprintf(paths, size_t(cap), "%s", all.c_str());
+  return int(rt.size());
+}
 
 TEMPI_EXPORT const char *tempi_version(void) { return "tempi-mi355x 0.1 (gfx950)"; }
 
@@ -167,6 +188,7 @@ TEMPI_EXPORT double tempi_interp_2d(const double *table, int rows, int cols, int
 TEMPI_EXPORT int tempi_perf_loaded(void) { return systemPerformanceLoaded ? 1 : 0; }
 
 TEMPI_EXPORT int tempi_perf_source(char *path, int cap) {
+  TEMPI_MT_ENTRY;
   if (!path || cap <= 0) return -1;
   std::snprintf(path, size_t(cap), "%s", systemPerformanceSource.c_str());
   return systemPerformanceLoaded ? 1 : 0;
@@ -203,6 +225,21 @@ TEMPI_EXPORT int tempi_choose_method(int64_t bytes, int64_t block, int colocated
   return m;
 }
 
+TEMPI_EXPORT int64_t tempi_ipc_threshold(int64_t block, int *from_model) {
+  TEMPI_MT_ENTRY;
+  bool fm = false;
+  const int64_t t = state.active ? p2p::query_ipc_threshold(block, &fm) : -1;
+  if (from_model) *from_model = fm ? 1 : 0;
+  return t;
+}
+
+TEMPI_EXPORT int64_t tempi_batch_ipc_threshold(const char *perf_json, int64_t block) {
+  SystemPerformance sp;
+  std::string err;
+  if (!perf_json || !from_json(perf_json, &sp, &err)) return -2;
+  return batch_ipc_threshold(sp, block);
+}
+
 // ---- rank placement (core/placement.hpp)
 
 TEMPI_EXPORT int64_t tempi_partition(int n, const int *xadj, const int *adjncy, const int *adjwgt, int nparts,
@@ -227,6 +264,7 @@ TEMPI_EXPORT int64_t tempi_partition(int n, const int *xadj, const int *adjncy, 
 }
 
 TEMPI_EXPORT int tempi_placement_info(int64_t out[6]) {
+  TEMPI_MT_ENTRY;
   const placement::Info i = placement::last();
   out[0] = i.placed;
   out[1] = i.nodes;

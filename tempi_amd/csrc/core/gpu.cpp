@@ -4,8 +4,13 @@
 #include "log.hpp"
 
 #include <algorithm>
+#include <climits>
 #include <cstdlib>
+#include <cstring>
+#include <link.h>
 #include <mutex>
+#include <set>
+#include <string>
 #include <unistd.h>
 #include <vector>
 
@@ -34,15 +39,47 @@ void choose_lanes(int ranksOnNode) {
 
 bool available() { return nDevices > 0 || hostOnlyTest; }
 
+std::vector<std::string> hip_runtimes() {
+  std::set<std::string> found;
+  dl_iterate_phdr(
+      [](dl_phdr_info *info, size_t, void *data) -> int {
+        const char *name = info->dlpi_name;
+        if (name && std::strstr(name, "libamdhip64")) {
+          char real[PATH_MAX];
+          static_cast<std::set<std::string> *>(data)->insert(realpath(name, real) ? real : name);
+        }
+        return 0;
+      },
+      &found);
+  return std::vector<std::string>(found.begin(), found.end());
+}
+
 void init() {
   int n = 0;
   if (tempi_hip_device_count(&n) != 0) n = 0;
   nDevices = n;
   hostOnlyTest = n == 0 && std::getenv("TEMPI_TEST_HOST_ONLY") != nullptr;
-  std::lock_guard<std::mutex> g(mtx);
-  streams.assign(size_t(n) * kMaxLanes, nullptr);
-  nLanes = 1; // until choose_lanes()
+  {
+    std::lock_guard<std::mutex> g(mtx);
+    streams.assign(size_t(n) * kMaxLanes, nullptr);
+    nLanes = 1; // until choose_lanes()
+  }
   LOG_DEBUG("visible GPUs: " << n);
+  // Two HIP runtimes in one process (a PyTorch wheel bundles its own beside
+  // the ROCm one libtempi_hip.so links): each has its own
+  // streams, so work the other runtime queued is not ordered with TEMPI's
+  // stream, and each sees the other's pinned host allocations as device
+  // memory (tools/diag_ptrattr.py, profiles/r06/diag_hostmalloc_s1.jsonl).
+  // Said once, on rank 0.
+  const std::vector<std::string> rt = hip_runtimes();
+  if (n > 0 && rt.size() > 1 && logRank == 0) {
+    std::string names;
+    for (const std::string &r : rt) names += (names.empty() ? "" : ", ") + r;
+    LOG_WARN(rt.size() << " HIP runtimes in this process (" << names
+                       << "); TEMPI uses the one libtempi_hip.so links. Work queued through another runtime must be "
+                          "complete (that runtime's synchronize) before an MPI call reads or writes its buffers "
+                          "(INTEGRATION.md, 'Two HIP runtimes')");
+  }
 }
 
 void finalize() {

@@ -8,6 +8,9 @@
 // after MPI_Init would then pack on the wrong device).
 #pragma once
 
+#include <string>
+#include <vector>
+
 #include "tempi_hip.h"
 
 #include <cstdint>
@@ -17,6 +20,8 @@ namespace gpu {
 
 // true when at least one GPU is visible (decided at MPI_Init)
 bool available();
+// the distinct libamdhip64 objects mapped into this process (realpath'd)
+std::vector<std::string> hip_runtimes();
 void init();
 void finalize();
 

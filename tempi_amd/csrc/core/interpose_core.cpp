@@ -363,7 +363,11 @@ TEMPI_EXPORT int MPI_Init_thread(int *argc, char ***argv, int required, int *pro
       if (mt::on && state.worldRank == 0)
         LOG_DEBUG("MPI_THREAD_MULTIPLE: TEMPI's calls run under one process-wide lock");
       *provided = cap_thread_level(*provided);
-      if (unguarded) mt::on = false;
+      if (unguarded) { // never silent: a stray variable would make a threaded application unsafe
+        LOG_WARN("TEMPI_FAULT_NO_MT_LOCK is set: MPI_THREAD_MULTIPLE is reported but TEMPI runs WITHOUT its lock "
+                 "(a sanitizer negative control; unsafe for threaded applications)");
+        mt::on = false;
+      }
     }
   }
   return rc;

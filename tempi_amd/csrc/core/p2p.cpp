@@ -216,6 +216,7 @@ int isend(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Co
   if (directEnabled && !blocking && mode != SendMode::SYNC && mode != SendMode::BUFFERED && force < 0 && destWorld == state.worldRank &&
       rec->flat(count, &flat)) {
     counters.send_direct++;
+    counters.bytes_direct += uint64_t(bytes);
     *req = add(new_isend_direct(rec, origin, count, dt, dest, tag, comm, p.device, bytes, flat));
     return MPI_SUCCESS;
   }
@@ -229,10 +230,22 @@ int isend(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Co
   // a buffered send must fit the buffer the application attached for its bytes
   if (mode == SendMode::BUFFERED && m == Method::IPC && bytes < int64_t(sizeof(IpcDesc))) m = Method::ONESHOT;
   switch (m) {
-  case Method::ONESHOT: counters.send_oneshot++; break;
-  case Method::STAGED: counters.send_staged++; break;
-  case Method::DEVICE: counters.send_device++; break;
-  case Method::IPC: counters.send_ipc++; break;
+  case Method::ONESHOT:
+    counters.send_oneshot++;
+    counters.bytes_oneshot += uint64_t(bytes);
+    break;
+  case Method::STAGED:
+    counters.send_staged++;
+    counters.bytes_staged += uint64_t(bytes);
+    break;
+  case Method::DEVICE:
+    counters.send_device++;
+    counters.bytes_device += uint64_t(bytes);
+    break;
+  case Method::IPC:
+    counters.send_ipc++;
+    counters.bytes_ipc += uint64_t(bytes);
+    break;
   default: break;
   }
   // IPC COPY: a large message of wide rows is copied by the receiver straight
@@ -254,6 +267,7 @@ int isend(const void *buf, int count, MPI_Datatype dt, int dest, int tag, MPI_Co
     d.ackTag = half + int32_t(nextCopyTag++ % uint32_t(half)); // slab ids (the IPC acks) stay below
     if (export_object(origin + rec->desc.start, &d)) {
       counters.send_ipc_copy++;
+      counters.bytes_ipc_copy += uint64_t(bytes);
       *req = add(new_isend_copy(rec, origin, count, dt, dest, tag, comm, p.device, bytes, destWorld, d));
       return MPI_SUCCESS;
     }

@@ -55,6 +55,9 @@ void finalize();
 void reload_perf_model();
 // the route a strided message would take (tempi_choose_method): 1 ONESHOT,
 // 2 DEVICE, 3 STAGED, 4 IPC; *fromModel set when the perf model decided
+// the IPC / ONESHOT threshold non-blocking AUTO sends of `block`-byte blocks
+// use; *fromModel when it was priced from this node's perf.json
+int64_t query_ipc_threshold(int64_t block, bool *fromModel);
 int query_method(int64_t bytes, int64_t block, bool colocated, bool blocking, bool *fromModel);
 
 // what handles() found out, handed on to isend / irecv

@@ -84,6 +84,12 @@ int recv_host_ipc_aware(void *buf, int count, MPI_Datatype dt, int source, int t
     if (flag) break;
     progress();
     mt::yield();
+    // at MPI_THREAD_MULTIPLE another thread's probe may have taken this
+    // message (with the source's earlier ones) out of the library while the
+    // lock was handed over: it is kept here, never again in the library
+    // 
+    if (std::unique_ptr<Probed> p = take_probed(source, tag, comm))
+      return land(p->bytes.data(), int(p->bytes.size()), p->st);
   }
   int n = 0;
   MPI_Get_count(&st, MPI_BYTE, &n);
@@ -131,13 +137,22 @@ std::unique_ptr<Probed> receive_probed(MPI_Message *m, int n, MPI_Comm comm) {
 // non-overtaking rule), so they are received first, in order, and
 // kept too: the kept messages of a source are always its earliest, in send
 // order, and every TEMPI receive takes from them before the library.
+//
+// At MPI_THREAD_MULTIPLE the blocking MPI_Probe that found the message ran
+// without TEMPI's lock, so another thread may have received it (or the
+// source's earlier ones) since: the library then has nothing (more) of src,
+// and the caller simply probes again -- as the library's own
+// probe information would be stale in that race too.
 void hold_through(int src, int tag, MPI_Comm comm) {
   for (;;) {
     MPI_Message m = MPI_MESSAGE_NULL;
     MPI_Status st;
     int g = 0;
     next.MPI_Improbe(src, MPI_ANY_TAG, comm, &g, &m, &st); // the earliest message of src
-    if (!g) LOG_FATAL("a probed message could not be matched");
+    if (!g) {
+      if (!mt::on) LOG_FATAL("a probed message could not be matched");
+      return; // taken by another thread: probe again
+    }
     int n = 0;
     MPI_Get_count(&st, MPI_BYTE, &n);
     probed.push_back(receive_probed(&m, n, comm));

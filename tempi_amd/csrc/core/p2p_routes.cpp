@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <climits>
 #include <cstdlib>
 #include <cstring>
 #include <unistd.h>
@@ -132,6 +133,31 @@ bool model_choice(int64_t bytes, bool colocated, int64_t block, Method *out) {
 
 int64_t modelBlock = 512; // block length of the type being sent (set per call)
 
+namespace {
+std::map<int64_t, int64_t> nbThresholdCache; // block -> batch-priced threshold (perf_model.cpp)
+} // namespace
+
+// The IPC threshold of non-blocking AUTO sends: priced
+// per batch from this node's own perf.json when one was measured here
+// (TEMPI_CACHE_DIR, e.g. by bench.py's measure_system run at N > 1), else the
+// built-in ipcMinBytes -- the shipped file was measured with both ranks on one
+// GPU, so its GPU-GPU curve never crossed a link.
+int64_t nb_ipc_threshold(int64_t block, bool *fromModel) {
+  *fromModel = false;
+  if (!systemPerformanceLoaded || !systemPerformanceNode) return ipcMinBytes;
+  auto it = nbThresholdCache.find(block);
+  if (it == nbThresholdCache.end()) {
+    const int64_t t = batch_ipc_threshold(systemPerformance, block);
+    it = nbThresholdCache.emplace(block, t).first;
+    if (t >= 0 && state.worldRank == 0)
+      LOG_DEBUG("non-blocking IPC threshold for " << block << "-byte blocks: "
+                                                  << (t == INT64_MAX ? std::string("never") : std::to_string(t)));
+  }
+  if (it->second < 0) return ipcMinBytes;
+  *fromModel = true;
+  return it->second;
+}
+
 // The measured model prices one message on its own: every term is a
 // synchronous call (a pack kernel launched and waited for, one ping-pong, an
 // unpack), as measure_system times them. Blocking sends are like that.
@@ -143,8 +169,9 @@ int64_t modelBlock = 512; // block length of the type being sent (set per call)
 // 512^3 halo from 1.56-1.67 ms into 2.0-2.4 ms per iteration, on whichever
 // boxes the quick measurement put the crossover there (round 3,
 // profiles/r03/n2_variants_s4.jsonl). So non-blocking
-// sends keep the built-in policy (the reference prices them by the model too,
-// async_operation.cpp:334-389).
+// sends are priced per batch instead (nb_ipc_threshold above) when this node
+// measured its own perf.json, and keep the built-in policy otherwise (the
+// reference prices them by the model too, async_operation.cpp:334-389).
 
 Method choose(int64_t bytes, bool colocated, bool blocking) {
   switch (env.datatype) {
@@ -161,22 +188,31 @@ Method choose(int64_t bytes, bool colocated, bool blocking) {
   default: {
     Method m;
     if (blocking && model_choice(bytes, colocated, modelBlock, &m)) return m;
-    if (colocated && bytes >= ipcMinBytes) return Method::IPC;
+    bool fm;
+    if (colocated && bytes >= (blocking ? ipcMinBytes : nb_ipc_threshold(modelBlock, &fm))) return Method::IPC;
     return Method::ONESHOT;
   }
   }
 }
 
-void clear_model_cache() { modelCache.clear(); }
+void clear_model_cache() {
+  modelCache.clear();
+  nbThresholdCache.clear();
+}
 
 } // namespace detail
+
+int64_t query_ipc_threshold(int64_t block, bool *fromModel) { return detail::nb_ipc_threshold(block, fromModel); }
 
 int query_method(int64_t bytes, int64_t block, bool colocated, bool blocking, bool *fromModel) {
   using namespace detail;
   Method m;
   const int64_t keep = modelBlock;
   modelBlock = block;
-  *fromModel = env.datatype == DatatypeMethod::AUTO && blocking && model_choice(bytes, colocated, block, &m);
+  bool nbModel = false;
+  if (!blocking) nb_ipc_threshold(block, &nbModel);
+  *fromModel = env.datatype == DatatypeMethod::AUTO &&
+               (blocking ? model_choice(bytes, colocated, block, &m) : (colocated && nbModel));
   m = choose(bytes, colocated, blocking);
   modelBlock = keep;
   switch (m) {

@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <cctype>
+#include <climits>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -22,6 +23,7 @@ namespace tempi {
 SystemPerformance systemPerformance;
 bool systemPerformanceLoaded = false;
 std::string systemPerformanceSource;
+bool systemPerformanceNode = false;
 
 bool SystemPerformance::empty() const {
   return intraNodeCpuCpuPingpong.empty() && intraNodeGpuGpuPingpong.empty() && d2h.empty() && packDevice.empty();
@@ -132,6 +134,55 @@ Opt model_staged(const SystemPerformance &sp, bool colocated, int64_t bytes, int
   return sum({interp_2d_opt(sp.packDevice, bytes, bl), interp_time_opt(sp.d2h, bytes),
               interp_time_opt(colocated ? sp.intraNodeCpuCpuPingpong : sp.interNodeCpuCpuPingpong, bytes),
               interp_time_opt(sp.h2d, bytes), interp_2d_opt(sp.unpackDevice, bytes, bl)});
+}
+
+// The IPC / ONESHOT crossover of NON-blocking sends, priced per batch
+// (the reference prices each Isend by the model,
+// /root/reference/src/internal/async_operation.cpp:334-389). The curves are
+// synchronous calls, but a burst of MPI_Isend / MPI_Irecv shares one gather
+// launch and one scatter launch and overlaps its library messages, so a
+// message adds only the MARGINAL cost of its bytes to each stage: the stage's
+// time at its size minus its time at the smallest measured size (launch,
+// completion and latency, paid once per batch). Both methods send one
+// library message per message (IPC: a 128-byte descriptor; ONESHOT: the
+// payload), so the library's per-message cost cancels and ONESHOT keeps the
+// marginal cost of moving its payload through the library:
+//   IPC(b)     = m(packDevice) + m(transfer over xGMI) + m(unpackDevice)
+//   ONESHOT(b) = m(packHost) + m(intra-node CPU ping-pong) + m(unpackHost)
+// where the transfer is the GPU-GPU ping-pong less the contiguous gather and
+// scatter it contains (model_device's viaTempi correction). The threshold is
+// the smallest power of two from which IPC stays cheaper up to 4 MiB; none
+// (INT64_MAX) when ONESHOT is cheaper at 4 MiB, -1 when a curve is missing.
+namespace {
+double marginal2(const std::vector<std::vector<IidTime>> &t, int64_t b, int64_t bl) {
+  const Opt x = interp_2d_opt(t, b, bl), z = interp_2d_opt(t, 64, bl);
+  return x.ok && z.ok ? std::max(0.0, x.v - z.v) : -1;
+}
+double marginal1(const std::vector<IidTime> &c, int64_t b) {
+  const Opt x = interp_time_opt(c, b), z = interp_time_opt(c, 1);
+  return x.ok && z.ok ? std::max(0.0, x.v - z.v) : -1;
+}
+} // namespace
+
+int64_t batch_ipc_threshold(const SystemPerformance &sp, int64_t bl) {
+  constexpr int kLo = 6, kHi = 22;
+  int64_t thr = INT64_MAX;
+  for (int k = kHi; k >= kLo; --k) {
+    const int64_t b = int64_t(1) << k;
+    const double pd = marginal2(sp.packDevice, b, bl), ud = marginal2(sp.unpackDevice, b, bl);
+    const double pd5 = marginal2(sp.packDevice, b, 512), ud5 = marginal2(sp.unpackDevice, b, 512);
+    const double pp = marginal1(sp.intraNodeGpuGpuPingpong, b);
+    const double ph = marginal2(sp.packHost, b, bl), uh = marginal2(sp.unpackHost, b, bl);
+    const double cc = marginal1(sp.intraNodeCpuCpuPingpong, b);
+    if (pd < 0 || ud < 0 || pd5 < 0 || ud5 < 0 || pp < 0 || ph < 0 || uh < 0 || cc < 0) return -1;
+    const double ipc = pd + std::max(0.0, pp - pd5 - ud5) + ud;
+    const double oneshot = ph + cc + uh;
+    if (ipc < oneshot)
+      thr = b; // IPC cheaper from here up
+    else
+      break;
+  }
+  return thr;
 }
 
 // ------------------------------------------------------------------- JSON
@@ -389,8 +440,10 @@ bool import_system_performance(SystemPerformance *sp) {
   // reference), then the shipped MI355X model; with neither, AUTO uses the
   // built-in policy (the reference stops: F10)
   systemPerformanceSource.clear();
+  systemPerformanceNode = false;
   if (load_file(perf_path(), sp)) {
     systemPerformanceSource = perf_path();
+    systemPerformanceNode = true;
     return true;
   }
   if (load_file(shipped_path(), sp)) {

@@ -65,6 +65,11 @@ Opt model_device(const SystemPerformance &sp, bool colocated, int64_t bytes, int
                  bool viaTempi = false);
 Opt model_staged(const SystemPerformance &sp, bool colocated, int64_t bytes, int64_t blockLength);
 
+// the smallest message size from which IPC beats ONESHOT for non-blocking
+// sends of blocks of `blockLength` bytes, priced per batch (perf_model.cpp);
+// INT64_MAX: never, -1: unknown (a curve missing)
+int64_t batch_ipc_threshold(const SystemPerformance &sp, int64_t blockLength);
+
 std::string to_json(const SystemPerformance &sp);
 bool from_json(const std::string &text, SystemPerformance *sp, std::string *err);
 
@@ -75,5 +80,6 @@ bool export_system_performance(const SystemPerformance &sp);
 extern SystemPerformance systemPerformance;
 extern bool systemPerformanceLoaded;
 extern std::string systemPerformanceSource; // the file AUTO's model came from ("" = built-in policy)
+extern bool systemPerformanceNode;          // ... and it is this node's own TEMPI_CACHE_DIR/perf.json
 
 } // namespace tempi

@@ -37,8 +37,10 @@
 #include "ticket.hpp"
 
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <mutex>
+#include <string>
 #include <vector>
 
 namespace {
@@ -177,6 +179,10 @@ __device__ __forceinline__ void wg_signal(const Sig &sg, bool fence) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
+    if (sg.slots) { // slot form (ticket.hpp): this workgroup's slot, nothing counted
+      __hip_atomic_store(sg.slots + blockIdx.x, sg.ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return;
+    }
     using namespace tempi_ticket;
     const uint32_t k = blockIdx.x % kShards;
     const uint32_t old = __hip_atomic_fetch_add(sg.counter + k * kCounterStride, 1u, __ATOMIC_RELAXED,
@@ -192,6 +198,42 @@ __device__ __forceinline__ void wg_signal(const Sig &sg, bool fence) {
 constexpr int kBlock = TEMPI_BLOCK;
 // the interleaved tiles index whole 64-lane waves (tile + wave * 64, j * 64 + lane over kBlock entries)
 static_assert(kBlock % 64 == 0 && kBlock >= 64 && kBlock <= 1024, "packer workgroups are whole 64-lane waves");
+
+// TEMPI_LAUNCH_CHECK=1: every launch is followed by a
+// stream synchronisation; a launch that faults is reported with the kernel,
+// its grid and the descriptor(s) of the entry point that launched it, and the
+// process aborts there -- instead of a later, unrelated call (another
+// runtime's copy, say) reporting a sticky error. A diagnostic mode: it
+// serialises every call.
+bool launch_check() {
+  static const bool on = [] {
+    const char *e = std::getenv("TEMPI_LAUNCH_CHECK");
+    return e && std::strtol(e, nullptr, 10) != 0;
+  }();
+  return on;
+}
+thread_local std::string gDesc; // what the current entry point launches (only kept under launch_check())
+void check_launch(const char *kernel, const dim3 &grid, hipStream_t s) {
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e == hipSuccess) return;
+  std::fprintf(stderr, "[TEMPI_LAUNCH_CHECK] %s, grid %u x %u: %s (%d) -- %s\n", kernel, grid.x, grid.y,
+               hipGetErrorString(e), int(e), gDesc.c_str());
+  std::fflush(stderr);
+  std::abort();
+}
+std::string describe(const tempi_hip_desc &d, const void *a, const void *b) {
+  std::string r = "{" + std::to_string(uintptr_t(a)) + " <- " + std::to_string(uintptr_t(b)) + ": block " +
+                  std::to_string(d.block);
+  for (int k = 0; k < d.ndims && k < TEMPI_HIP_MAX_DIMS; ++k)
+    r += " (" + std::to_string(d.counts[k]) + " x " + std::to_string(d.strides[k]) + ")";
+  return r + "}";
+}
+#define TEMPI_LAUNCH(K, G, B, SH, S, ...)                                                                          \
+  do {                                                                                                             \
+    hipLaunchKernelGGL(K, G, B, SH, S, __VA_ARGS__);                                                               \
+    if (launch_check()) check_launch(#K, G, S);                                                                    \
+  } while (0)
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
@@ -1005,9 +1047,16 @@ bool scatter_write_through(const Norm &n) {
 Sig take_fold_from(tempi_ticket::Fold *f, uint32_t blocks, bool writeThrough) {
   using tempi_ticket::kShards;
   Sig sg{};
-  if (!f || f->taken || !f->t || !f->t->counter || blocks == 0 ||
-      blocks > (writeThrough ? f->max_blocks_wt : f->max_blocks))
+  if (!f || f->taken || !f->t || blocks == 0 || blocks > (writeThrough ? f->max_blocks_wt : f->max_blocks)) return sg;
+  if (f->slots_ok && blocks <= tempi_ticket::kMaxSlots) { // one slot per workgroup, nothing counted
+    f->taken = true;
+    f->slots = blocks;
+    sg.slots = f->t->dev + tempi_ticket::kSlotFirst;
+    sg.flag = f->t->dev;
+    sg.ticket = f->ticket;
     return sg;
+  }
+  if (!f->t->counter) return sg;
   uint32_t *counted = f->t->counted;
   for (uint32_t k = 0; k < uint32_t(kShards); ++k) { // workgroups b with b % kShards == k
     if (blocks > k) counted[k] += (blocks - k + kShards - 1) / kShards;
@@ -1067,10 +1116,10 @@ int launch_nd(bool pack, char *packed, char *first, const Norm &n, hipStream_t s
   const bool wtc = (a.flags & kWriteThrough) != 0;
   if (pack) {
     auto *k = wtc ? pack_kernel<W, ND, true> : pack_kernel<W, ND, false>;
-    hipLaunchKernelGGL(k, dim3(blocks), dim3(kBlock), 0, s, a, sg);
+    TEMPI_LAUNCH(k, dim3(blocks), dim3(kBlock), 0, s, a, sg);
   } else {
     auto *k = wtc ? unpack_kernel<W, ND, kScatterWT> : unpack_kernel<W, ND, false>;
-    hipLaunchKernelGGL(k, dim3(blocks), dim3(kBlock), 0, s, a, sg);
+    TEMPI_LAUNCH(k, dim3(blocks), dim3(kBlock), 0, s, a, sg);
   }
   return int(hipGetLastError());
 }
@@ -1113,28 +1162,28 @@ int launch_batch_nd(bool pack, const std::vector<Job> &jobs, hipStream_t s, temp
       const KArgs<ND> &a = b.item[0];
       if (il)
         if (pack)
-          hipLaunchKernelGGL((wtc ? pack_il_kernel<W, ND, true> : pack_il_kernel<W, ND, false>), dim3(total),
+          TEMPI_LAUNCH((wtc ? pack_il_kernel<W, ND, true> : pack_il_kernel<W, ND, false>), dim3(total),
                              dim3(kBlock), 0, s, a, sg);
         else
-          hipLaunchKernelGGL((unpack_il_kernel<W, ND>), dim3(total), dim3(kBlock), 0, s, a, sg);
+          TEMPI_LAUNCH((unpack_il_kernel<W, ND>), dim3(total), dim3(kBlock), 0, s, a, sg);
       else if (pack)
-        hipLaunchKernelGGL((wtc ? pack_kernel<W, ND, true> : pack_kernel<W, ND, false>), dim3(total), dim3(kBlock),
+        TEMPI_LAUNCH((wtc ? pack_kernel<W, ND, true> : pack_kernel<W, ND, false>), dim3(total), dim3(kBlock),
                            0, s, a, sg);
       else
-        hipLaunchKernelGGL((wtc ? unpack_kernel<W, ND, kScatterWT> : unpack_kernel<W, ND, false>), dim3(total),
+        TEMPI_LAUNCH((wtc ? unpack_kernel<W, ND, kScatterWT> : unpack_kernel<W, ND, false>), dim3(total),
                            dim3(kBlock), 0, s, a, sg);
     } else if (total) {
       if (il)
         if (pack)
-          hipLaunchKernelGGL((wtc ? pack_il_batch_kernel<W, ND, true> : pack_il_batch_kernel<W, ND, false>),
+          TEMPI_LAUNCH((wtc ? pack_il_batch_kernel<W, ND, true> : pack_il_batch_kernel<W, ND, false>),
                              dim3(total), dim3(kBlock), 0, s, b, sg);
         else
-          hipLaunchKernelGGL((unpack_il_batch_kernel<W, ND>), dim3(total), dim3(kBlock), 0, s, b, sg);
+          TEMPI_LAUNCH((unpack_il_batch_kernel<W, ND>), dim3(total), dim3(kBlock), 0, s, b, sg);
       else if (pack)
-        hipLaunchKernelGGL((wtc ? pack_batch_kernel<W, ND, true> : pack_batch_kernel<W, ND, false>), dim3(total),
+        TEMPI_LAUNCH((wtc ? pack_batch_kernel<W, ND, true> : pack_batch_kernel<W, ND, false>), dim3(total),
                            dim3(kBlock), 0, s, b, sg);
       else
-        hipLaunchKernelGGL((wtc ? unpack_batch_kernel<W, ND, kScatterWT> : unpack_batch_kernel<W, ND, false>),
+        TEMPI_LAUNCH((wtc ? unpack_batch_kernel<W, ND, kScatterWT> : unpack_batch_kernel<W, ND, false>),
                            dim3(total), dim3(kBlock), 0, s, b, sg);
     }
     b.nitems = 0;
@@ -1214,7 +1263,7 @@ template <int ND> int launch_dense_nd(char *packed, char *first, const Norm &n, 
   const Sig sg = take_fold(blocks, true);
   if (sg.flag) a.flags |= kWriteThrough;
   auto *k = sg.flag ? pack_dense_kernel<ND, true> : pack_dense_kernel<ND, false>;
-  hipLaunchKernelGGL(k, dim3(blocks), dim3(kBlock), 0, s, a, sg);
+  TEMPI_LAUNCH(k, dim3(blocks), dim3(kBlock), 0, s, a, sg);
   return int(hipGetLastError());
 }
 
@@ -1240,9 +1289,9 @@ template <int W, int ND> int launch_il_nd(bool pack, char *packed, char *first, 
   if (sg.flag && pack) a.flags |= kWriteThrough;
   if (pack) {
     auto *k = sg.flag ? pack_il_kernel<W, ND, true> : pack_il_kernel<W, ND, false>;
-    hipLaunchKernelGGL(k, dim3(blocks), dim3(kBlock), 0, s, a, sg);
+    TEMPI_LAUNCH(k, dim3(blocks), dim3(kBlock), 0, s, a, sg);
   } else {
-    hipLaunchKernelGGL((unpack_il_kernel<W, ND>), dim3(blocks), dim3(kBlock), 0, s, a, sg);
+    TEMPI_LAUNCH((unpack_il_kernel<W, ND>), dim3(blocks), dim3(kBlock), 0, s, a, sg);
   }
   return int(hipGetLastError());
 }
@@ -1327,6 +1376,12 @@ int launch_split(bool pack, char *packed, char *first, const Norm &n, hipStream_
 // only: the stream runs launches in order, so its ticket follows all of them
 int run_batch(bool pack, const tempi_hip_batch_item *items, int n, hipStream_t s,
               tempi_ticket::Fold *fold = nullptr) {
+  if (launch_check()) {
+    gDesc = std::string(pack ? "pack" : "unpack") + " batch of " + std::to_string(n) + ":";
+    for (int i = 0; i < n; ++i)
+      gDesc += " " + (pack ? describe(items[i].desc, items[i].packed, items[i].first)
+                           : describe(items[i].desc, items[i].first, items[i].packed));
+  }
   // group by (word width, rank): one launch per group and per kMax objects
   std::vector<Job> groups[5][TEMPI_HIP_MAX_DIMS + 1];
   for (int i = 0; i < n; ++i) {
@@ -1505,8 +1560,75 @@ template <int W> __device__ __forceinline__ void copy_body(const CArgs &a, uint3
   }
 }
 
+// ---- the PEELED copy (W = 0 below)
+//
+// Both sides start 8 bytes past a 16-byte boundary, with rows of a multiple
+// of 16 bytes at strides that are multiples of 16: the halo's y / z faces, 4
+// KiB rows whose region starts 24 B into 512-B-aligned pitched rows. The
+// plain plan moves those in 8-byte words (word_width ORs the bases), and a
+// 1 GiB copy of that shape runs at 4.5-4.8 TB/s against 5.4 TB/s in 16-byte
+// words (tools/kbench.cpp with KBENCH_OFFSET 24 / 32, profiles/r06/
+// koff_s1.jsonl). Here the VIRTUAL byte v = b + 8 (b: the byte in type-map
+// order) has v = address (mod 16) on both sides, so virtual chunk c (bytes
+// b in [16c - 8, 16c + 8)) is one aligned dwordx4 on each side, unless its
+// second half starts a row on either side (a row seam in its middle) or it is
+// the first / last chunk (half outside the object): those move as two 8-byte
+// halves. a.nwords counts 8-byte words (even), the sides' wpr too.
+__device__ __forceinline__ int64_t side_offset_seam(uint32_t q0, const CSide &c, bool *seam) {
+  uint32_t row = mdiv(q0, c.mwpr);
+  const uint32_t w = q0 - row * c.wpr;
+  *seam = w + 1 == c.wpr; // word q0 ends its row: the next word starts one
+  int64_t off = int64_t(w) * 8;
+#pragma unroll
+  for (int k = 0; k < kCopyND - 1; ++k) {
+    const uint32_t r2 = mdiv(row, c.mcnt[k]);
+    off += int64_t(row - r2 * c.cnt[k]) * c.stride[k];
+    row = r2;
+  }
+  return off + int64_t(row) * c.stride[kCopyND - 1];
+}
+
+__device__ __forceinline__ void copy_half(const CArgs &a, uint32_t q, const char *s, char *d) {
+  const uint2 v = ld_src(a, reinterpret_cast<const uint2 *>(s + side_offset<8>(q, a.s)), false);
+  st(reinterpret_cast<uint2 *>(d + side_offset<8>(q, a.d)), v, false);
+}
+
+__device__ void copy_body_peel(const CArgs &a, uint32_t blk, uint32_t nblk) {
+  const uint32_t nchunks = a.nwords / 2 + 1;
+  for (uint32_t c = blk * kCopyBlock + threadIdx.x; c < nchunks; c += nblk * kCopyBlock) {
+    const uint32_t q1 = 2 * c; // the 8-byte word of the chunk's second half
+    bool ss = true, ds = true;
+    int64_t so = 0, dof = 0;
+    if (c > 0 && q1 < a.nwords) {
+      so = side_offset_seam(q1 - 1, a.s, &ss);
+      dof = side_offset_seam(q1 - 1, a.d, &ds);
+    }
+    if (!ss && !ds) { // one aligned 16-byte word on each side
+      const uint4 v = ld_src(a, reinterpret_cast<const uint4 *>(a.s.first + so), true);
+      uint4 v2;
+      if (a.s2) v2 = ld_src(a, reinterpret_cast<const uint4 *>(a.s2 + so), true);
+      st(reinterpret_cast<uint4 *>(a.d.first + dof), v, true);
+      if (a.s2) st(reinterpret_cast<uint4 *>(a.d2 + dof), v2, true);
+      continue;
+    }
+    for (int h = 0; h < 2; ++h) { // a seam, or the object's first / last chunk
+      const uint32_t q = q1 - 1 + uint32_t(h);
+      if ((h == 0 && c == 0) || q >= a.nwords) continue;
+      copy_half(a, q, a.s.first, a.d.first);
+      if (a.s2) copy_half(a, q, a.s2, a.d2);
+    }
+  }
+}
+
+template <int W> __device__ __forceinline__ void copy_any(const CArgs &a, uint32_t blk, uint32_t nblk) {
+  if constexpr (W == 0)
+    copy_body_peel(a, blk, nblk);
+  else
+    copy_body<W>(a, blk, nblk);
+}
+
 template <int W> __global__ __launch_bounds__(kCopyBlock) void copy_kernel(const CArgs a, const Sig sg) {
-  copy_body<W>(a, xcd_tile(blockIdx.x, gridDim.x, a.flags), gridDim.x);
+  copy_any<W>(a, xcd_tile(blockIdx.x, gridDim.x, a.flags), gridDim.x);
   wg_signal(sg, true);
 }
 
@@ -1527,7 +1649,7 @@ template <int W> __global__ __launch_bounds__(kCopyBlock) void copy_batch_kernel
       hi = mid;
   }
   const uint32_t n = b.first[lo + 1] - b.first[lo];
-  copy_body<W>(b.item[lo], xcd_tile(blockIdx.x - b.first[lo], n, b.item[lo].flags), n); // (within the item)
+  copy_any<W>(b.item[lo], xcd_tile(blockIdx.x - b.first[lo], n, b.item[lo].flags), n); // (within the item)
   wg_signal(sg, true);
 }
 
@@ -1558,8 +1680,31 @@ bool make_side(char *first, const Norm &n, int W, CSide *c) {
 
 struct CopyJob {
   CArgs a;
-  int w;
+  int w; // word width; 0: the peeled copy (16-byte chunks, 8-byte seam halves)
 };
+
+#ifndef TEMPI_COPY_PEEL
+#define TEMPI_COPY_PEEL 1
+#endif
+// the peeled copy applies: 8-byte words only because both bases sit 8 bytes
+// past a 16-byte boundary, every block and stride a multiple of 16
+// (TEMPI_COPY_PEEL=0 in the environment turns it off, for A/B runs)
+bool peel_enabled() {
+  static const bool on = [] {
+    const char *e = std::getenv("TEMPI_COPY_PEEL");
+    return TEMPI_COPY_PEEL && (!e || std::strtol(e, nullptr, 10) != 0);
+  }();
+  return on;
+}
+bool peel_ok(uintptr_t dst, uintptr_t src, const Norm &nd, const Norm &ns) {
+  if (!peel_enabled() || (dst & 15) != 8 || (src & 15) != 8) return false;
+  for (const Norm *n : {&nd, &ns}) {
+    if (n->block % 16) return false;
+    for (int k = 0; k < n->nd; ++k)
+      if (n->str[k] % 16) return false;
+  }
+  return true;
+}
 
 // the copy as one kernel item, or false when it needs the pack + unpack route
 bool plan_copy(void *dst, const void *src, const tempi_hip_desc *dd, const tempi_hip_desc *sd, CopyJob *job) {
@@ -1570,9 +1715,11 @@ bool plan_copy(void *dst, const void *src, const tempi_hip_desc *dd, const tempi
   int w = word_width(reinterpret_cast<uintptr_t>(dst), reinterpret_cast<uintptr_t>(src), ns);
   const int wd = word_width(reinterpret_cast<uintptr_t>(dst), reinterpret_cast<uintptr_t>(src), nd);
   if (wd < w) w = wd;
+  const bool peel = w == 8 && peel_ok(reinterpret_cast<uintptr_t>(dst), reinterpret_cast<uintptr_t>(src), nd, ns);
   if (!make_side(const_cast<char *>(static_cast<const char *>(src)), ns, w, &job->a.s)) return false;
   if (!make_side(static_cast<char *>(dst), nd, w, &job->a.d)) return false;
   job->a.nwords = uint32_t(bytes / w);
+  if (peel) w = 0; // (the sides count 8-byte words, as the peeled body expects)
   job->a.flags = xcd_flag(static_cast<char *>(dst), nd, false);
   job->a.s2 = job->a.d2 = nullptr;
   job->w = w;
@@ -1614,8 +1761,9 @@ std::vector<CopyJob> pair_jobs(const std::vector<CopyJob> &in) {
 }
 
 uint32_t copy_blocks(const CopyJob &j) {
-  const uint64_t tile = uint64_t(kCopyBlock) * (16 / j.w) * TEMPI_COPY_U;
-  uint64_t b = (uint64_t(j.a.nwords) + tile - 1) / tile;
+  const uint64_t tile = j.w ? uint64_t(kCopyBlock) * (16 / j.w) * TEMPI_COPY_U : uint64_t(kCopyBlock);
+  const uint64_t units = j.w ? uint64_t(j.a.nwords) : uint64_t(j.a.nwords) / 2 + 1; // (peeled: chunks)
+  uint64_t b = (units + tile - 1) / tile;
   if (b > TEMPI_MAX_BLOCKS) b = TEMPI_MAX_BLOCKS;
   return uint32_t(b);
 }
@@ -1630,9 +1778,9 @@ template <int W> int launch_copy_group(const std::vector<CopyJob> &jobs, hipStre
     b.first[b.nitems] = total;
     const Sig sg = last && fold ? take_fold_from(fold, total, false) : Sig{};
     if (b.nitems == 1)
-      hipLaunchKernelGGL(copy_kernel<W>, dim3(total), dim3(kCopyBlock), 0, s, b.item[0], sg);
+      TEMPI_LAUNCH(copy_kernel<W>, dim3(total), dim3(kCopyBlock), 0, s, b.item[0], sg);
     else
-      hipLaunchKernelGGL(copy_batch_kernel<W>, dim3(total), dim3(kCopyBlock), 0, s, b, sg);
+      TEMPI_LAUNCH(copy_batch_kernel<W>, dim3(total), dim3(kCopyBlock), 0, s, b, sg);
     b.nitems = 0;
     total = 0;
     return int(hipGetLastError());
@@ -1654,21 +1802,28 @@ template <int W> int launch_copy_group(const std::vector<CopyJob> &jobs, hipStre
 
 // the copy batch; fold: a completion ticket for its last launch (run_batch)
 int copy_batch(const tempi_hip_copy_item *items, int n, void *stream, tempi_ticket::Fold *fold) {
-  std::vector<CopyJob> groups[5];
+  if (launch_check()) {
+    gDesc = "copy batch of " + std::to_string(n) + ":";
+    for (int i = 0; i < n; ++i)
+      gDesc += " " + describe(items[i].dst, items[i].dst_first, nullptr) + " <- " +
+               describe(items[i].src, items[i].src_first, nullptr) +
+               ((items[i].flags & TEMPI_HIP_ITEM_REMOTE) ? " remote" : "");
+  }
+  std::vector<CopyJob> groups[6];
   for (int i = 0; i < n; ++i) {
     CopyJob j;
     if (!plan_copy(items[i].dst_first, items[i].src_first, &items[i].dst, &items[i].src, &j))
       return int(hipErrorInvalidValue);
     j.a.flags |= items[i].flags & TEMPI_HIP_ITEM_REMOTE;
     if (j.a.nwords == 0) continue;
-    const int wi = j.w == 1 ? 0 : j.w == 2 ? 1 : j.w == 4 ? 2 : j.w == 8 ? 3 : 4;
+    const int wi = j.w == 1 ? 0 : j.w == 2 ? 1 : j.w == 4 ? 2 : j.w == 8 ? 3 : j.w == 16 ? 4 : 5;
     groups[wi].push_back(j);
   }
   hipStream_t s = static_cast<hipStream_t>(stream);
   int lastGroup = -1;
-  for (int wi = 0; wi < 5; ++wi)
+  for (int wi = 0; wi < 6; ++wi)
     if (!groups[wi].empty()) lastGroup = wi;
-  for (int wi = 0; wi < 5; ++wi) {
+  for (int wi = 0; wi < 6; ++wi) {
     if (groups[wi].empty()) continue;
     tempi_ticket::Fold *f = wi == lastGroup ? fold : nullptr;
     int e = 0;
@@ -1677,7 +1832,8 @@ int copy_batch(const tempi_hip_copy_item *items, int n, void *stream, tempi_tick
     case 1: e = launch_copy_group<2>(pair_jobs(groups[wi]), s, f); break;
     case 2: e = launch_copy_group<4>(pair_jobs(groups[wi]), s, f); break;
     case 3: e = launch_copy_group<8>(pair_jobs(groups[wi]), s, f); break;
-    default: e = launch_copy_group<16>(pair_jobs(groups[wi]), s, f); break;
+    case 4: e = launch_copy_group<16>(pair_jobs(groups[wi]), s, f); break;
+    default: e = launch_copy_group<0>(pair_jobs(groups[wi]), s, f); break;
     }
     if (e) return e;
   }
@@ -1694,11 +1850,18 @@ int tempi_hip_copy_supported(void *dst_first, const void *src_first, const tempi
   return plan_copy(dst_first, src_first, dst, src, &j) ? 1 : 0;
 }
 
+int tempi_hip_copy_word_width(void *dst_first, const void *src_first, const tempi_hip_desc *dst,
+                              const tempi_hip_desc *src) {
+  CopyJob j;
+  return plan_copy(dst_first, src_first, dst, src, &j) ? j.w : -1;
+}
+
 int tempi_hip_copy_batch(const tempi_hip_copy_item *items, int n, void *stream) {
   return copy_batch(items, n, stream, nullptr);
 }
 
 int tempi_hip_pack(void *packed, const void *first, const tempi_hip_desc *d, void *stream) {
+  if (launch_check()) gDesc = "pack " + describe(*d, packed, first);
   Norm n;
   if (!normalise(d, &n)) return int(hipErrorInvalidValue);
   return launch_split(true, static_cast<char *>(packed),
@@ -1707,6 +1870,7 @@ int tempi_hip_pack(void *packed, const void *first, const tempi_hip_desc *d, voi
 }
 
 int tempi_hip_unpack(void *first, const void *packed, const tempi_hip_desc *d, void *stream) {
+  if (launch_check()) gDesc = "unpack " + describe(*d, first, packed);
   Norm n;
   if (!normalise(d, &n)) return int(hipErrorInvalidValue);
   return launch_split(false, const_cast<char *>(static_cast<const char *>(packed)),
@@ -1722,6 +1886,7 @@ namespace {
 // launch order on the stream.
 int with_ticket(bool pack, char *packed, char *first, const tempi_hip_desc *d, hipStream_t s, const uint32_t **flag,
                 uint32_t *ticket) {
+  if (launch_check()) gDesc = std::string(pack ? "pack " : "unpack ") + "(ticket) " + describe(*d, packed, first);
   Norm n;
   if (!normalise(d, &n)) return int(hipErrorInvalidValue);
   bool single = norm_bytes(n) < kMaxLaunchBytes; // launch_split makes exactly one launch
@@ -1734,15 +1899,23 @@ int with_ticket(bool pack, char *packed, char *first, const tempi_hip_desc *d, h
   fold.ticket = ++t->next;
   fold.max_blocks = single ? tempi_ticket::fold_max_blocks() : 0;
   fold.max_blocks_wt = single ? tempi_ticket::fold_max_blocks_wt() : 0;
+  fold.slots_ok = tempi_ticket::slots_enabled(); // (the caller waits with tempi_hip_ticket_wait)
   gFold = &fold;
   const int e = launch_split(pack, packed, first, n, s);
   gFold = nullptr;
   if (e) {
-    if (fold.taken) t->broken = true; // the host counted a launch that never ran
+    if (fold.taken && !fold.slots) t->broken = true; // the host counted a launch that never ran
     return e;
   }
   *flag = t->host;
   *ticket = fold.ticket;
+  if (fold.slots) { // the header of this slot ticket: the launch's slot count
+    uint32_t *hdr = t->host + tempi_ticket::kHdrFirst + fold.ticket % tempi_ticket::kHdrCount;
+    *hdr = fold.slots;
+    *flag = hdr;
+    tempi_ticket::stats().folded++;
+    return 0;
+  }
   if (fold.taken) tempi_ticket::stats().folded++;
   return fold.taken ? 0 : int(tempi_ticket::queue_kernel(*t, s, fold.ticket));
 }

@@ -43,6 +43,7 @@ _COUNTER_FIELDS = [
     "neighbor_colls", "send_ipc_copy", "copy_resends", "ipc_maps_replaced", "canary_ok", "canary_fail",
     "self_matched", "staged_packs", "staged_unpacks", "ticket_waits", "sync_waits",
     "ticket_batches", "persistent_starts", "batches", "gpu_inflight_ns",
+    "bytes_ipc", "bytes_ipc_copy", "bytes_oneshot", "bytes_staged", "bytes_device", "bytes_direct",
 ]
 
 

@@ -1,9 +1,12 @@
 """Run under mpiexec -n 1 with TEMPI_CACHE_DIR set: which perf model TEMPI
 loaded at MPI_Init (tempi_perf_source) and what AUTO picks from it
 (tempi_choose_method) for blocking strided sends of 2^6 .. 2^22 bytes in
-512-byte blocks, to a co-located and to an off-node peer. Prints one JSON
-line {"source": ..., "loaded": 0|1, "picks": [[bytes, colocated, method,
-from_model], ...]}."""
+512-byte blocks, to a co-located and to an off-node peer, and the IPC
+threshold of non-blocking sends (tempi_ipc_threshold) for 8- and 512-byte
+blocks. Prints one JSON line {"source": ..., "loaded": 0|1, "picks":
+[[bytes, colocated, method, from_model], ...], "nb_threshold": [[block,
+threshold, from_model], ...], "nb_picks": [[bytes, method, from_model],
+...]}."""
 import ctypes
 import json
 import os
@@ -27,5 +30,16 @@ for lg in range(6, 23, 2):
         fm = ctypes.c_int(-1)
         m = L.tempi_choose_method(1 << lg, 512, co, 1, ctypes.byref(fm))
         picks.append([1 << lg, co, m, fm.value])
+L.tempi_ipc_threshold.restype = ctypes.c_int64
+L.tempi_ipc_threshold.argtypes = [ctypes.c_int64, ctypes.POINTER(ctypes.c_int)]
+nb = []
+for bl in (8, 512):
+    fm = ctypes.c_int(-1)
+    nb.append([bl, L.tempi_ipc_threshold(bl, ctypes.byref(fm)), fm.value])
+nb_picks = []
+for lg in range(6, 23, 2):
+    fm = ctypes.c_int(-1)
+    nb_picks.append([1 << lg, L.tempi_choose_method(1 << lg, 512, 1, 0, ctypes.byref(fm)), fm.value])
 mpi.Finalize()
-print(json.dumps({"source": buf.value.decode(), "loaded": loaded, "picks": picks}), flush=True)
+print(json.dumps({"source": buf.value.decode(), "loaded": loaded, "picks": picks, "nb_threshold": nb,
+                  "nb_picks": nb_picks}), flush=True)

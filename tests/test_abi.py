@@ -59,3 +59,47 @@ def test_kernels_are_gfx950():
                          text=True)
     blob = open(tempi_amd.LIBTEMPI_HIP, "rb").read()
     assert b"gfx950" in blob
+
+
+
+_RUNTIMES = """
+import ctypes, sys
+sys.path.insert(0, {root!r})
+import tempi_amd
+if {order!r} == "torch_first":
+    import torch  # noqa: F401  (its wheel bundles a HIP runtime of its own)
+L = ctypes.CDLL(tempi_amd.LIBTEMPI)
+if {order!r} == "tempi_first":
+    import torch  # noqa: F401,F811
+buf = ctypes.create_string_buffer(8192)
+n = L.tempi_hip_runtimes(buf, 8192)
+print(n, buf.value.decode())
+"""
+
+
+@pytest.mark.parametrize("order", ["tempi_only", "torch_first", "tempi_first"])
+def test_hip_runtime_detection(order):
+    """TEMPI counts the distinct HIP runtimes mapped into
+    the process (dl_iterate_phdr over libamdhip64 objects) and reports more
+    than one at MPI_Init (core/gpu.cpp). The count depends on load order:
+    torch's wheel bundles libamdhip64.so with the SONAME libamdhip64.so.7,
+    which is what libtempi_hip.so needs, so torch imported FIRST satisfies it
+    (one runtime, torch's); libtempi loaded first maps ROCm's, and torch's
+    libraries then load their own (they need the unversioned name): two.
+    No GPU is needed to count them."""
+    import sys
+
+    code = _RUNTIMES.format(root=tempi_amd.ROOT, order=order)
+    r = subprocess.run([sys.executable, "-c", code], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    n, _, paths = r.stdout.strip().partition(" ")
+    paths = paths.split(";")
+    assert int(n) == len(paths), r.stdout
+    assert all("libamdhip64" in p for p in paths), paths
+    if order == "tempi_only":
+        assert paths == [p for p in paths if "torch" not in p] and int(n) == 1, paths
+    elif order == "torch_first":
+        assert int(n) == 1 and "torch" in paths[0], paths
+    else:
+        assert int(n) == 2 and sum("torch" in p for p in paths) == 1, paths

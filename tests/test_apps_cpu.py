@@ -180,3 +180,32 @@ def test_timeline_records_entry_points(tmp_path):
     p = subprocess.run([sys.executable, os.path.join(mpi_launch.ROOT, "tools", "halo_timeline.py"), f"{pre}.r0.csv",
                         "-", "3"], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=60)
     assert p.returncode == 0 and "substeps" in p.stdout, p.stdout
+
+
+def test_nonblocking_ipc_threshold_follows_node_perf_json(tmp_path):
+    """non-blocking AUTO sends take IPC from a threshold
+    priced per batch from THIS node's perf.json (TEMPI_CACHE_DIR) when one was
+    measured here -- a synthetic file whose curves cross at ~12 KiB moves it
+    to 16 KiB, a costlier per-message IPC to 64 KiB, and tempi_choose_method's
+    non-blocking picks follow it -- and stay at the built-in 4 KiB with only
+    the shipped model (measured with both ranks on one GPU). Blocking sends
+    keep pricing each message by the model."""
+    from tests.test_perf_model import _synthetic_perf
+
+    def pick(cache):
+        rc, log = mpi_launch.run(1, mpi_launch.py("perf_pick.py"), env={"TEMPI_CACHE_DIR": str(cache)}, timeout=120)
+        assert rc == 0, log[-3000:]
+        return json.loads(next(l for l in log.splitlines() if l.startswith("{")))
+
+    shipped = pick(tmp_path / "none")
+    assert shipped["loaded"] == 1 and shipped["source"].endswith("perf_mi355x.json"), shipped
+    assert shipped["nb_threshold"] == [[8, 4096, 0], [512, 4096, 0]], shipped
+    for fixed, exp in ((1.1e-6, 16384), (4.4e-6, 65536)):
+        d = tmp_path / f"node_{exp}"
+        d.mkdir()
+        (d / "perf.json").write_text(json.dumps(_synthetic_perf(fixed, 100e9)))
+        node = pick(d)
+        assert node["source"] == str(d / "perf.json"), node
+        assert node["nb_threshold"] == [[8, exp, 1], [512, exp, 1]], node
+        for b, m, fm in node["nb_picks"]:  # 4 = IPC, 1 = ONESHOT (co-located peer)
+            assert (m, fm) == ((4, 1) if b >= exp else (1, 1)), (b, m, fm, node)

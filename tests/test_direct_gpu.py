@@ -417,3 +417,82 @@ def test_copy_xcd_mapped_large(gpu):
         got = dst[off:].view(rows, ds)
         assert torch.equal(got[:, :bl], src.view(rows, ss)[:, :bl]), (rows, bl, ss, ds)
         assert int(got[:, bl:].count_nonzero()) == 0 and int(dst[:off].count_nonzero()) == 0
+
+
+@pytest.mark.parametrize("remote", [False, True])
+def test_copy_peeled_rows(mpi, gpu, remote):
+    """The peeled copy (pack_kernels.hip copy_body_peel):
+    both sides 8 bytes past a 16-byte boundary, blocks and strides multiples
+    of 16, so 16-byte chunks move as one aligned dwordx4 a side except the
+    chunks a row seam splits (two 8-byte halves) and the object's first and
+    last. Shapes: the halo's y / z faces at a 4608-byte pitch, a single
+    16-byte row, rows of 16 / 32 / 48 bytes, and sides of different shapes
+    (seams at different chunks on each side), several in one batch with a
+    same-shape pair; every destination byte against numpy, gaps untouched,
+    and the plan is the peeled one (tempi_hip_copy_word_width == 0)."""
+    import torch
+
+    H = _hip()
+    H.tempi_hip_copy_word_width.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(HipDesc),
+                                            ctypes.POINTER(HipDesc)]
+
+    def desc(block, dims):
+        d = HipDesc()
+        d.block, d.ndims = block, len(dims)
+        for j, (c, st) in enumerate(dims):
+            d.counts[j], d.strides[j] = c, st
+        return d
+
+    def view(_, off, block, dims):
+        """the object's bytes in type-map order, as numpy indices"""
+        idx = np.arange(block, dtype=np.int64)
+        for c, st in reversed(dims):
+            idx = (np.arange(c, dtype=np.int64)[:, None] * st + idx[None, :]).reshape(-1)
+        return off + idx
+
+    rng = np.random.default_rng(11)
+    plane = 4608 * 70
+    specs = [  # (src block, src dims), (dst block, dst dims): equal byte counts
+        ((4096, [(9, plane), (3, 4608)]), (4096, [(9, plane), (3, 4608)])),  # y face
+        ((4096, [(3, plane), (64, 4608)]), (4096, [(3, plane), (64, 4608)])),  # z face
+        ((4096, [(3, plane), (64, 4608)]), (4096, [(3, plane), (64, 4608)])),  # its pair (same shape)
+        ((16, []), (16, [])),
+        ((16, [(1000, 48)]), (32, [(500, 80)])),
+        ((48, [(7, 4096), (11, 64)]), (16, [(231, 32)])),
+        ((32, [(3000, 32)]), (96, [(1000, 128), (1, 0)])),
+    ]
+    cases = []
+    for (sb, sdims), (db, ddims) in specs:
+        sdims = [d for d in sdims if d[0] != 1]
+        ddims = [d for d in ddims if d[0] != 1]
+        sd, dd = desc(sb, sdims), desc(db, ddims)
+        sidx, didx = view(None, 8, sb, sdims), view(None, 8, db, ddims)
+        assert sidx.size == didx.size
+        sh = rng.integers(0, 256, int(sidx.max()) + 64, dtype=np.uint8)
+        canvas = rng.integers(0, 256, int(didx.max()) + 64, dtype=np.uint8)
+        src = torch.from_numpy(sh).to(gpu)
+        dst = torch.from_numpy(canvas).to(gpu)
+        assert src.data_ptr() % 16 == 0 and dst.data_ptr() % 16 == 0  # (so +8 is the phase)
+        it = CopyItem()
+        it.src_first, it.dst_first = src.data_ptr() + 8, dst.data_ptr() + 8
+        it.src, it.dst = sd, dd
+        it.flags = ITEM_REMOTE if remote else 0
+        assert H.tempi_hip_copy_word_width(it.dst_first, it.src_first, ctypes.byref(dd), ctypes.byref(sd)) == 0
+        exp = canvas.copy()
+        exp[didx] = sh[sidx]
+        cases.append((it, dst, exp, src))  # (src kept alive: torch's allocator would hand its memory on)
+    items = (CopyItem * len(cases))(*[c[0] for c in cases])
+    torch.cuda.synchronize()
+    if remote:
+        release_l2(H)
+    assert H.tempi_hip_copy_batch(items, len(cases), None) == 0
+    torch.cuda.synchronize()
+    for k, (it, dst, exp, _) in enumerate(cases):
+        assert np.array_equal(dst.cpu().numpy(), exp), f"case {k}"
+    # one phase off on one side, or a 16-byte-misaligned stride: not peeled
+    sd = desc(32, [(100, 48)])
+    p = cases[0][1].data_ptr()
+    assert H.tempi_hip_copy_word_width(p + 8, p + 24 + 4096, ctypes.byref(sd), ctypes.byref(sd)) == 0
+    assert H.tempi_hip_copy_word_width(p + 8, p + 4 + 4096, ctypes.byref(sd), ctypes.byref(sd)) == 4
+    odd = desc(32, [(100, 40)])
+    assert H.tempi_hip_copy_word_width(p + 8, p + 8 + 8192, ctypes.byref(odd), ctypes.byref(odd)) == 8

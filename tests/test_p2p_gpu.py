@@ -395,3 +395,15 @@ def test_measure_system_writes_a_model_auto_uses(gpu, tmp_path):
     assert pick["loaded"] == 1 and pick["source"] == str(out), pick
     colocated = [p for p in pick["picks"] if p[1] == 1]
     assert all(fm == 1 and m in (1, 3, 4) for _, _, m, fm in colocated), pick  # ONESHOT / STAGED / IPC, priced
+
+
+def test_multiple_threads_probe_holds_a_waited_message(gpu):
+    """at MPI_THREAD_MULTIPLE, thread A blocks in a host
+    MPI_Recv(0, tag A) while thread B's MPI_Probe(0, tag B) finds a strided
+    device message (a descriptor) that rank 0 sent right behind A's message:
+    the probe must receive A's message to look at B (non-overtaking) and
+    keeps it, and A's receive must take it from what is kept instead of
+    asking the library forever. 100 rounds, every byte checked; a hang is
+    the join timing out."""
+    rc, out = mpi_launch.run(2, mpi_launch.py("probe_threads.py", "100"), timeout=240)
+    assert rc == 0 and out.count("RESULT errors=0") == 2, out[-3000:]

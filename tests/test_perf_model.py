@@ -127,3 +127,50 @@ def test_shipped_mi355x_model():
         assert len(doc[k]) == 9 and all(len(r) == 10 for r in doc[k]), k
     out = ctypes.create_string_buffer(1 << 17)
     assert L.tempi_perf_roundtrip(open(path, "rb").read(), out, 1 << 17) == 0
+
+
+L.tempi_batch_ipc_threshold.restype = ctypes.c_int64
+L.tempi_batch_ipc_threshold.argtypes = [ctypes.c_char_p, ctypes.c_int64]
+INT64_MAX = (1 << 63) - 1
+
+
+def _synthetic_perf(fixed_ipc, xgmi, pack_host=True):
+    """a perf.json whose curves are straight lines: device (un)pack 10 us +
+    b / 2 TB/s, host (un)pack 10 us + b / 40 GB/s, CPU ping-pong 1 us + b /
+    20 GB/s, and the GPU-GPU ping-pong 20 us at 1 byte, 20 us + fixed_ipc +
+    b / xgmi above -- so per batch (marginal costs) IPC costs about fixed_ipc
+    + b / xgmi and ONESHOT b / 10 GB/s"""
+    def line(a, rate, b):
+        return {"time": a + b / rate, "iid": True}
+    table = lambda a, rate: [[line(a, rate, 1 << (2 * i + 6)) for _ in range(10)] for i in range(9)]
+    gpu = [{"time": 20e-6, "iid": True}] + [line(20e-6 + fixed_ipc, xgmi, 1 << i) for i in range(1, 24)]
+    return {"cudaKernelLaunch": 3e-6,
+            "intraNodeCpuCpuPingpong": [line(1e-6, 20e9, 1 << i) for i in range(24)],
+            "intraNodeGpuGpuPingpong": gpu, "interNodeCpuCpuPingpong": [], "interNodeGpuGpuPingpong": [],
+            "d2h": [line(5e-6, 50e9, 1 << i) for i in range(24)], "h2d": [line(5e-6, 50e9, 1 << i) for i in range(24)],
+            "packDevice": table(10e-6, 2e12), "unpackDevice": table(10e-6, 2e12),
+            "packHost": table(10e-6, 40e9) if pack_host else [], "unpackHost": table(10e-6, 40e9)}
+
+
+@pytest.mark.parametrize("fixed,xgmi,block,exp", [
+    (1.1e-6, 100e9, 512, 16384),   # crossover at ~12 KiB: IPC from 16 KiB up
+    (4.4e-6, 100e9, 512, 65536),   # a larger per-message IPC cost moves it to 64 KiB
+    (4.4e-6, 100e9, 8, 65536),     # (straight-line tables: the block does not matter)
+    (0.0, 100e9, 512, 64),         # IPC cheaper at every size: the smallest priced
+    (1.1e-6, 9e9, 512, INT64_MAX),  # xGMI slower than the host path: never IPC
+])
+def test_batch_ipc_threshold(fixed, xgmi, block, exp):
+    """the IPC / ONESHOT threshold of non-blocking AUTO
+    sends, priced per batch from a perf.json (perf_model.cpp
+    batch_ipc_threshold: marginal cost of each stage's bytes, launch and
+    latency paid once per batch), moves with the curves"""
+    doc = json.dumps(_synthetic_perf(fixed, xgmi)).encode()
+    assert L.tempi_batch_ipc_threshold(doc, block) == exp
+
+
+def test_batch_ipc_threshold_unknown():
+    """a curve the pricing needs is missing (-1: the built-in 4 KiB stays), or
+    the document does not parse (-2)"""
+    assert L.tempi_batch_ipc_threshold(json.dumps(_synthetic_perf(1.1e-6, 100e9, pack_host=False)).encode(),
+                                       512) == -1
+    assert L.tempi_batch_ipc_threshold(b"{not json", 512) == -2

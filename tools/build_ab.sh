@@ -8,11 +8,12 @@
 # tools/_variants is listed in .gpurunignore: drop that line for the A/B session)
 set -e
 cd "$(dirname "$0")/.."
-mkdir -p tools/_variants
-rm -f tools/_variants/*.so
+V=${KAB_DIR:-tools/_variants} # KAB_DIR=tools/bin/v: a directory that travels to the GPU box
+mkdir -p $V
+rm -f $V/*.so
 build() { # name dir [flags]
   hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Iinclude $3 \
-    -o tools/_variants/libtempi_hip_$1.so $2/*.hip -Wl,-rpath,/opt/rocm/lib
+    -o $V/libtempi_hip_$1.so $2/*.hip -Wl,-rpath,/opt/rocm/lib
 }
 build cur tempi_amd/csrc/hip &
 for ref in "$@"; do
@@ -25,6 +26,6 @@ for ref in "$@"; do
   build "$(echo "$ref" | tr -c 'A-Za-z0-9_\n' '_')" $d &
 done
 wait
-g++ -O2 -std=c++17 -Iinclude -o tools/_variants/kbench tools/kbench.cpp -ldl
-g++ -O2 -std=c++17 -Iinclude -o tools/_variants/hbench tools/hbench.cpp -ldl
-ls tools/_variants
+g++ -O2 -std=c++17 -Iinclude -o $V/kbench tools/kbench.cpp -ldl
+g++ -O2 -std=c++17 -Iinclude -o $V/hbench tools/hbench.cpp -ldl
+ls $V

@@ -19,6 +19,22 @@
 #   torchrun     the driver's torchrun command at NS (default "2") ranks
 #   n8           the driver's torchrun command at 8 ranks (tools/gpu_n8.sh)
 #   kab          kernel A/B: tools/kab.sh $KAB_OUT $KAB_ROUNDS $KAB_ITERS $KAB_SHAPES
+#   koff         tools/bin/kbench on the in-tree library, KBENCH_OFFSET in turn
+#                each of $KOFF_OFFSETS (default "24 32"), $KOFF_ROUNDS rotations,
+#                shapes $KOFF_SHAPES -> gpurun_out/koff.jsonl
+#   launchsplit  tools/bin/launchsplit: dispatch / execution / visibility of
+#                the config-1 synchronous call -> gpurun_out/launchsplit.jsonl
+#   halo-ab      1-rank halo_exchange $HALO_ITERS (default 30) 512 under each
+#                environment of $HALO_AB ("A=1,B=2 A=0" style, "-" for none),
+#                $HALO_ROUNDS rotations -> gpurun_out/halo_ab.jsonl
+#   ls-ab        launchsplit with TEMPI_TICKET_SLOTS=1 / 0, $LS_ROUNDS rotations
+#   launch-check the GPU tests LC_FOCUS selects with TEMPI_LAUNCH_CHECK=1 (every
+#                TEMPI launch synchronised and checked)
+#   kpmc         rocprofv3 --pmc passes ($KPMC_PASSES, ';'-separated counter
+#                lists, one run each) over tools/bin/kbench (pack / unpack /
+#                memcpy, no copies) of $KPMC_SHAPES -> gpurun_out/kpmc.txt
+#   diag-hostmalloc  tools/diag_hostmalloc.py (both HIP runtimes in one
+#                process; may end in a HIP error: run it LAST)
 set -o pipefail
 cd "$(dirname "$0")/.."
 O=gpurun_out
@@ -78,6 +94,62 @@ for step in "$@"; do
   kab)
     bash tools/kab.sh $KAB_OUT ${KAB_ROUNDS:-3} ${KAB_ITERS:-20} $KAB_SHAPES || exit 16
     python3 tools/kab_summary.py $O/$KAB_OUT 2>&1 | tail -40 ;;
+  koff)
+    rm -f $O/koff.jsonl
+    for r in $(seq ${KOFF_ROUNDS:-3}); do
+      for off in ${KOFF_OFFSETS:-24 32}; do
+        KBENCH_OFFSET=$off timeout -k 10 300 tools/bin/kbench tempi_amd/lib/libtempi_hip.so ${KOFF_ITERS:-20} $KOFF_SHAPES \
+          | sed "s/^{/{\"round\": $r, /" >> $O/koff.jsonl || exit 19
+      done
+    done
+    cat $O/koff.jsonl ;;
+  launchsplit)
+    timeout -k 10 120 tools/bin/launchsplit ${LS_REPS:-2000} > $O/launchsplit.jsonl 2>&1 || exit 20
+    cat $O/launchsplit.jsonl ;;
+  halo-ab)
+    rm -f $O/halo_ab.jsonl
+    for r in $(seq ${HALO_ROUNDS:-3}); do
+      for v in $HALO_AB; do
+        envs=$([ "$v" = "-" ] && echo "" || echo "$v" | tr ',' ' ')
+        env $envs timeout -k 10 300 tempi_amd/lib/halo_exchange ${HALO_ITERS:-30} 512 2>> $O/halo_ab.err \
+          | grep '^{' | sed "s/^{/{\"variant\": \"$v\", \"round\": $r, /" >> $O/halo_ab.jsonl || exit 21
+      done
+    done
+    python3 -c "
+import json,collections
+d=collections.defaultdict(list)
+for l in open('$O/halo_ab.jsonl'): j=json.loads(l); d[j['variant']].append(round(j['us_per_iter'],1))
+for k,v in d.items(): print(k, v)" ;;
+  ls-ab)
+    rm -f $O/launchsplit_ab.jsonl
+    for r in $(seq ${LS_ROUNDS:-3}); do
+      for v in 1 0; do
+        TEMPI_TICKET_SLOTS=$v timeout -k 10 120 tools/bin/launchsplit ${LS_REPS:-2000} 2>&1 \
+          | sed "s/^{/{\"slots\": $v, \"round\": $r, /" >> $O/launchsplit_ab.jsonl || exit 22
+      done
+    done
+    cat $O/launchsplit_ab.jsonl ;;
+  launch-check)
+    TEMPI_LAUNCH_CHECK=1 timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+      -k "$LC_FOCUS" > $O/launch_check.log 2>&1
+    rc=$?; tail -n 15 $O/launch_check.log; [ $rc -eq 0 ] || exit $rc ;;
+  kpmc)
+    rm -rf $O/kpmc_*; rm -f $O/kpmc.txt
+    IFS=';' read -ra passes <<< "$KPMC_PASSES"
+    for shape in $KPMC_SHAPES; do
+      i=0
+      for pass in "${passes[@]}"; do
+        i=$((i+1)); d=$O/kpmc_${shape//:/_}_$i
+        KBENCH_NO_COPY=1 timeout -s KILL 120 rocprofv3 --pmc $pass -d $d -o run --output-format csv \
+          -- tools/bin/kbench tempi_amd/lib/libtempi_hip.so ${KPMC_ITERS:-3} $shape > $d.log 2>&1 || exit 23
+      done
+      echo "== $shape (KBENCH_OFFSET=${KBENCH_OFFSET:-0})" >> $O/kpmc.txt
+      python3 tools/pmc_kernels.py $O/kpmc_${shape//:/_}_* >> $O/kpmc.txt 2>&1 || exit 24
+    done
+    cat $O/kpmc.txt ;;
+  diag-hostmalloc)
+    timeout -k 10 300 python3 -u tools/diag_hostmalloc.py > $O/diag_hostmalloc.jsonl 2>&1
+    rc=$?; tail -n 40 $O/diag_hostmalloc.jsonl; exit $rc ;;
   *)
     echo "unknown step $step"; exit 2 ;;
   esac

@@ -8,11 +8,12 @@ set -o pipefail
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 OUT=gpurun_out/$1; ROUNDS=$2; REPS=$3; shift 3
+V=${KAB_DIR:-tools/_variants}  # (tools/bin/v travels to the box: tools/_variants is gpurun-ignored)
 rm -f $OUT
 for r in $(seq $ROUNDS); do
-  for lib in tools/_variants/libtempi_hip_*.so; do
+  for lib in $V/libtempi_hip_*.so; do
     v=$(basename $lib .so); v=${v#libtempi_hip_}
-    timeout -k 10 300 tools/_variants/kbench $lib $REPS "$@" | sed "s/^{/{\"variant\": \"$v\", \"round\": $r, /" >> $OUT || exit 5
+    timeout -k 10 300 $V/kbench $lib $REPS "$@" | sed "s/^{/{\"variant\": \"$v\", \"round\": $r, /" >> $OUT || exit 5
   done
 done
 echo "wrote $(wc -l < $OUT) lines to $OUT"

@@ -8,6 +8,9 @@
 // system-scope loads a reader on another GPU uses; here on local memory).
 // Prints one JSON line per shape: kernel ms (HIP events, back-to-back
 // launches) and algorithmic GB/s (2 x payload per pack, unpack or copy).
+// KBENCH_OFFSET=B starts both strided objects B bytes into their allocations
+// (the halo's regions start 24 B into 512-B-aligned rows), KBENCH_POFF=B the
+// packed buffer.
 #include "tempi_hip.h"
 
 #include <cstdio>
@@ -62,12 +65,16 @@ int main(int argc, char **argv) {
     // extent: outermost count * stride (enough for positive strides)
     extent = d.ndims ? d.counts[0] * d.strides[0] : d.block;
     const long long payload = tempi_hip_desc_bytes(&d);
-    void *strided, *packed, *other = nullptr;
-    CK(tempi_hip_malloc(&strided, size_t(extent)));
-    CK(tempi_hip_malloc(&packed, size_t(payload)));
-    CK(tempi_hip_memset_async(strided, 1, size_t(extent), s));
+    void *strided0, *packed0, *other0 = nullptr;
+    const long long off = std::getenv("KBENCH_OFFSET") ? std::atoll(std::getenv("KBENCH_OFFSET")) : 0;
+    const long long poff = std::getenv("KBENCH_POFF") ? std::atoll(std::getenv("KBENCH_POFF")) : 0;
+    CK(tempi_hip_malloc(&strided0, size_t(extent + off)));
+    CK(tempi_hip_malloc(&packed0, size_t(payload + poff)));
+    CK(tempi_hip_memset_async(strided0, 1, size_t(extent + off), s));
     const bool copies = std::getenv("KBENCH_NO_COPY") == nullptr;
-    if (copies) CK(tempi_hip_malloc(&other, size_t(extent)));
+    if (copies) CK(tempi_hip_malloc(&other0, size_t(extent + off)));
+    char *strided = static_cast<char *>(strided0) + off, *packed = static_cast<char *>(packed0) + poff;
+    char *other = other0 ? static_cast<char *>(other0) + off : nullptr;
     tempi_hip_copy_item ci{};
     ci.dst_first = other;
     ci.src_first = strided;
@@ -91,15 +98,15 @@ int main(int argc, char **argv) {
       ms[mode] /= float(reps);
     }
     auto gbs = [&](float m) { return 2.0 * double(payload) / (double(m) * 1e-3) / 1e9; };
-    std::printf("{\"lib\": \"%s\", \"shape\": \"%s\", \"payload\": %lld, \"pack_ms\": %.4f, \"unpack_ms\": %.4f, "
+    std::printf("{\"lib\": \"%s\", \"shape\": \"%s\", \"offset\": %lld, \"poff\": %lld, \"payload\": %lld, \"pack_ms\": %.4f, \"unpack_ms\": %.4f, "
                 "\"memcpy_ms\": %.4f, \"pack_gbs\": %.1f, \"unpack_gbs\": %.1f, \"memcpy_gbs\": %.1f, "
                 "\"copy_gbs\": %.1f, \"copy_remote_gbs\": %.1f}\n",
-                argv[1], argv[a], payload, ms[0], ms[1], ms[2], gbs(ms[0]), gbs(ms[1]), gbs(ms[2]),
+                argv[1], argv[a], off, poff, payload, ms[0], ms[1], ms[2], gbs(ms[0]), gbs(ms[1]), gbs(ms[2]),
                 copies ? gbs(ms[3]) : 0.0, copies ? gbs(ms[4]) : 0.0);
     std::fflush(stdout);
-    tempi_hip_free(strided);
-    tempi_hip_free(packed);
-    if (other) tempi_hip_free(other);
+    tempi_hip_free(strided0);
+    tempi_hip_free(packed0);
+    if (other0) tempi_hip_free(other0);
   }
   return 0;
 }
