@@ -179,10 +179,6 @@ __device__ __forceinline__ void wg_signal(const Sig &sg, bool fence) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    if (sg.slots) { // slot form (ticket.hpp): this workgroup's slot, nothing counted
-      __hip_atomic_store(sg.slots + blockIdx.x, sg.ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      return;
-    }
     using namespace tempi_ticket;
     const uint32_t k = blockIdx.x % kShards;
     const uint32_t old = __hip_atomic_fetch_add(sg.counter + k * kCounterStride, 1u, __ATOMIC_RELAXED,
@@ -1047,16 +1043,9 @@ bool scatter_write_through(const Norm &n) {
 Sig take_fold_from(tempi_ticket::Fold *f, uint32_t blocks, bool writeThrough) {
   using tempi_ticket::kShards;
   Sig sg{};
-  if (!f || f->taken || !f->t || blocks == 0 || blocks > (writeThrough ? f->max_blocks_wt : f->max_blocks)) return sg;
-  if (f->slots_ok && blocks <= tempi_ticket::kMaxSlots) { // one slot per workgroup, nothing counted
-    f->taken = true;
-    f->slots = blocks;
-    sg.slots = f->t->dev + tempi_ticket::kSlotFirst;
-    sg.flag = f->t->dev;
-    sg.ticket = f->ticket;
+  if (!f || f->taken || !f->t || !f->t->counter || blocks == 0 ||
+      blocks > (writeThrough ? f->max_blocks_wt : f->max_blocks))
     return sg;
-  }
-  if (!f->t->counter) return sg;
   uint32_t *counted = f->t->counted;
   for (uint32_t k = 0; k < uint32_t(kShards); ++k) { // workgroups b with b % kShards == k
     if (blocks > k) counted[k] += (blocks - k + kShards - 1) / kShards;
@@ -1593,8 +1582,12 @@ __device__ __forceinline__ void copy_half(const CArgs &a, uint32_t q, const char
   st(reinterpret_cast<uint2 *>(d + side_offset<8>(q, a.d)), v, false);
 }
 
+// the peeled copy's whole chunks go nontemporal unless the item carries
+// kCopyPlain (TEMPI_COPY_PEEL=2, an A/B switch)
+constexpr uint32_t kCopyPlain = 1u << 29; // internal flag bit (never a TEMPI_HIP_ITEM_*)
 __device__ void copy_body_peel(const CArgs &a, uint32_t blk, uint32_t nblk) {
   const uint32_t nchunks = a.nwords / 2 + 1;
+  const bool nt = !(a.flags & kCopyPlain);
   for (uint32_t c = blk * kCopyBlock + threadIdx.x; c < nchunks; c += nblk * kCopyBlock) {
     const uint32_t q1 = 2 * c; // the 8-byte word of the chunk's second half
     bool ss = true, ds = true;
@@ -1604,11 +1597,11 @@ __device__ void copy_body_peel(const CArgs &a, uint32_t blk, uint32_t nblk) {
       dof = side_offset_seam(q1 - 1, a.d, &ds);
     }
     if (!ss && !ds) { // one aligned 16-byte word on each side
-      const uint4 v = ld_src(a, reinterpret_cast<const uint4 *>(a.s.first + so), true);
+      const uint4 v = ld_src(a, reinterpret_cast<const uint4 *>(a.s.first + so), nt);
       uint4 v2;
-      if (a.s2) v2 = ld_src(a, reinterpret_cast<const uint4 *>(a.s2 + so), true);
-      st(reinterpret_cast<uint4 *>(a.d.first + dof), v, true);
-      if (a.s2) st(reinterpret_cast<uint4 *>(a.d2 + dof), v2, true);
+      if (a.s2) v2 = ld_src(a, reinterpret_cast<const uint4 *>(a.s2 + so), nt);
+      st(reinterpret_cast<uint4 *>(a.d.first + dof), v, nt);
+      if (a.s2) st(reinterpret_cast<uint4 *>(a.d2 + dof), v2, nt);
       continue;
     }
     for (int h = 0; h < 2; ++h) { // a seam, or the object's first / last chunk
@@ -1689,13 +1682,15 @@ struct CopyJob {
 // the peeled copy applies: 8-byte words only because both bases sit 8 bytes
 // past a 16-byte boundary, every block and stride a multiple of 16
 // (TEMPI_COPY_PEEL=0 in the environment turns it off, for A/B runs)
-bool peel_enabled() {
-  static const bool on = [] {
+// (TEMPI_COPY_PEEL=2: peeled, with plain loads and stores)
+int peel_mode() {
+  static const int m = [] {
     const char *e = std::getenv("TEMPI_COPY_PEEL");
-    return TEMPI_COPY_PEEL && (!e || std::strtol(e, nullptr, 10) != 0);
+    return TEMPI_COPY_PEEL ? (e ? int(std::strtol(e, nullptr, 10)) : 1) : 0;
   }();
-  return on;
+  return m;
 }
+bool peel_enabled() { return peel_mode() != 0; }
 bool peel_ok(uintptr_t dst, uintptr_t src, const Norm &nd, const Norm &ns) {
   if (!peel_enabled() || (dst & 15) != 8 || (src & 15) != 8) return false;
   for (const Norm *n : {&nd, &ns}) {
@@ -1720,7 +1715,7 @@ bool plan_copy(void *dst, const void *src, const tempi_hip_desc *dd, const tempi
   if (!make_side(static_cast<char *>(dst), nd, w, &job->a.d)) return false;
   job->a.nwords = uint32_t(bytes / w);
   if (peel) w = 0; // (the sides count 8-byte words, as the peeled body expects)
-  job->a.flags = xcd_flag(static_cast<char *>(dst), nd, false);
+  job->a.flags = xcd_flag(static_cast<char *>(dst), nd, false) | (peel && peel_mode() == 2 ? kCopyPlain : 0u);
   job->a.s2 = job->a.d2 = nullptr;
   job->w = w;
   return true;
@@ -1899,23 +1894,15 @@ int with_ticket(bool pack, char *packed, char *first, const tempi_hip_desc *d, h
   fold.ticket = ++t->next;
   fold.max_blocks = single ? tempi_ticket::fold_max_blocks() : 0;
   fold.max_blocks_wt = single ? tempi_ticket::fold_max_blocks_wt() : 0;
-  fold.slots_ok = tempi_ticket::slots_enabled(); // (the caller waits with tempi_hip_ticket_wait)
   gFold = &fold;
   const int e = launch_split(pack, packed, first, n, s);
   gFold = nullptr;
   if (e) {
-    if (fold.taken && !fold.slots) t->broken = true; // the host counted a launch that never ran
+    if (fold.taken) t->broken = true; // the host counted a launch that never ran
     return e;
   }
   *flag = t->host;
   *ticket = fold.ticket;
-  if (fold.slots) { // the header of this slot ticket: the launch's slot count
-    uint32_t *hdr = t->host + tempi_ticket::kHdrFirst + fold.ticket % tempi_ticket::kHdrCount;
-    *hdr = fold.slots;
-    *flag = hdr;
-    tempi_ticket::stats().folded++;
-    return 0;
-  }
   if (fold.taken) tempi_ticket::stats().folded++;
   return fold.taken ? 0 : int(tempi_ticket::queue_kernel(*t, s, fold.ticket));
 }

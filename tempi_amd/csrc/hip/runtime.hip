@@ -151,21 +151,16 @@ Stats &stats() {
 Ticket *of(hipStream_t s) {
   Ticket &t = tickets[s];
   if (!t.host) {
-    // the flag + slot block (ticket.hpp), aligned to its own 8 KiB so that a
-    // flag's offset in it tells the ticket forms apart
-    constexpr size_t kBytes = kBlockWords * sizeof(uint32_t);
     void *h = nullptr, *d = nullptr;
-    hipError_t e = hipHostMalloc(&h, 2 * kBytes, hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable);
+    hipError_t e = hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable);
     if (e == hipSuccess) e = hipHostGetDevicePointer(&d, h, 0);
     if (e != hipSuccess) {
       (void)hipGetLastError();
       return nullptr;
     }
-    const size_t skip = (kBytes - (reinterpret_cast<uintptr_t>(h) & (kBytes - 1))) & (kBytes - 1);
-    t.host = reinterpret_cast<uint32_t *>(static_cast<char *>(h) + skip);
-    t.dev = reinterpret_cast<uint32_t *>(static_cast<char *>(d) + skip);
-    for (uint32_t i = 0; i < kBlockWords; ++i) __atomic_store_n(t.host + i, 0u, __ATOMIC_RELAXED);
-    __atomic_thread_fence(__ATOMIC_RELEASE);
+    t.host = static_cast<uint32_t *>(h);
+    t.dev = static_cast<uint32_t *>(d);
+    __atomic_store_n(t.host, 0u, __ATOMIC_RELEASE);
   }
   if (!t.counter || t.broken) { // (re)start the workgroup count at 0 once the stream is idle
     if (!t.counter && hipMalloc(reinterpret_cast<void **>(&t.counter), kCounterWords * sizeof(uint32_t)) != hipSuccess) {
@@ -193,22 +188,6 @@ hipError_t queue_kernel(Ticket &t, hipStream_t s, uint32_t ticket) {
 }
 
 int wait(hipStream_t s, const uint32_t *flag, uint32_t ticket) {
-  const uintptr_t off = reinterpret_cast<uintptr_t>(flag) & (kBlockWords * sizeof(uint32_t) - 1);
-  if (off) { // a slot ticket: flag is its header, holding the launch's slot count
-    const uint32_t *slots = flag - off / sizeof(uint32_t) + kSlotFirst;
-    const uint32_t n = *flag;
-    uint32_t i = 0; // slots [0, i) have reached the ticket
-    for (uint32_t spins = 1;; ++spins) {
-      while (i < n && int32_t(__atomic_load_n(slots + i, __ATOMIC_ACQUIRE) - ticket) >= 0) ++i;
-      if (i == n) return 0;
-      if ((spins & 1023) == 0) {
-        const hipError_t e = hipStreamQuery(s);
-        if (e == hipSuccess) return 0;
-        if (e != hipErrorNotReady) return int(e);
-      }
-      __builtin_ia32_pause();
-    }
-  }
   for (uint32_t spins = 1;; ++spins) {
     if (int32_t(__atomic_load_n(flag, __ATOMIC_ACQUIRE) - ticket) >= 0) return 0;
     if ((spins & 1023) == 0) { // ~20 µs of pause loops
@@ -218,14 +197,6 @@ int wait(hipStream_t s, const uint32_t *flag, uint32_t ticket) {
     }
     __builtin_ia32_pause();
   }
-}
-
-bool slots_enabled() {
-  static const bool v = [] {
-    const char *e = std::getenv("TEMPI_TICKET_SLOTS");
-    return !e || std::strtoul(e, nullptr, 10) != 0;
-  }();
-  return v;
 }
 
 uint32_t fold_max_blocks() {

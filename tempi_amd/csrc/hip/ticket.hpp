@@ -52,29 +52,8 @@ constexpr int kShards = 8;
 constexpr int kCounterStride = 32; // uint32 words between counters (128 B)
 constexpr int kCounterWords = (kShards + 1) * kCounterStride;
 
-// Per-workgroup SLOTS (round 6): a synchronous call's
-// single launch of at most kMaxSlots workgroups does not count itself at all.
-// Each workgroup, once its stores are done (and released when they went
-// through L2 write-back), stores the ticket into its own slot of the stream's
-// pinned page, and the host waits until every slot of the launch has reached
-// the ticket. The counted fold's end of a kernel is a chain of two returning
-// system-scope atomics (shard, then top) before the flag store; here the last
-// workgroup's only extra step is one posted store to host memory, and the
-// scan over <= kMaxSlots words is host-local reads.
-// The stream's pinned block (kBlockWords words, aligned to its own size):
-//   word 0                      the flag of every other ticket form
-//   words [kHdrFirst, +kHdrCount) one header per slot ticket (ticket % kHdrCount):
-//                               the number of slots the launch stores; a slot
-//                               ticket's flag points AT its header word
-//   words [kSlotFirst, +kMaxSlots) the slots, one per workgroup index
-// so tempi_hip_ticket_wait tells the two forms apart by the flag's offset in
-// the block (0: a flag; anything else: a header).
-constexpr uint32_t kBlockWords = 2048; // 8 KiB
-constexpr uint32_t kHdrFirst = 16, kHdrCount = 1008;
-constexpr uint32_t kSlotFirst = 1024, kMaxSlots = 1024;
-
 struct Ticket {
-  uint32_t *host = nullptr, *dev = nullptr; // the flag (pinned, coherent): word 0 of the 8 KiB block
+  uint32_t *host = nullptr, *dev = nullptr; // the flag (pinned, coherent)
   uint32_t next = 0;                        // last ticket issued
   uint32_t *counter = nullptr;              // device: kShards shard counters + the top counter
   uint32_t counted[kShards + 1] = {};       // the host's running totals of the same (mod 2^32)
@@ -95,16 +74,13 @@ struct Fold {
   uint32_t ticket = 0;
   uint32_t max_blocks = 0;    // launches whose stores go through L2 write-back
   uint32_t max_blocks_wt = 0; // launches that store write-through (gathers)
-  bool slots_ok = false;      // the caller waits with tempi_hip_ticket_wait: slots may be used
   bool taken = false;
-  uint32_t slots = 0; // taken in slot form: the launch's workgroup count (0: counted)
 };
 
 // the kernel-side view, passed as a kernel argument (flag == nullptr: none)
 struct Sig {
   uint32_t *counter;
   uint32_t *flag;
-  uint32_t *slots; // slot form: slot 0 (device pointer), workgroup b stores the ticket at slots[b]
   uint32_t target[kShards]; // each shard's count once this launch's workgroups of that shard have counted
   uint32_t top;             // the top counter's value once this launch's last shard completes
   uint32_t ticket;
@@ -119,8 +95,6 @@ hipError_t queue_kernel(Ticket &t, hipStream_t s, uint32_t ticket);
 // spin until the flag reaches `ticket`; the stream is queried every ~20 us,
 // so a faulted stream ends the wait with its error
 int wait(hipStream_t s, const uint32_t *flag, uint32_t ticket);
-// slot tickets in use (TEMPI_TICKET_SLOTS, default 1; 0: always counted)
-bool slots_enabled();
 // largest grid a work kernel takes a fold for (TEMPI_FOLD_MAX_BLOCKS, 0 = never)
 uint32_t fold_max_blocks();
 // the same for launches whose work is stored write-through (TEMPI_FOLD_MAX_BLOCKS_WT)
