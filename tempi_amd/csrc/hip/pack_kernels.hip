@@ -1297,7 +1297,20 @@ template <int W> int launch_il(bool pack, char *packed, char *first, const Norm 
   }
 }
 
+// (with the copy kernels below) a pack / unpack whose packed side sits at
+// the strided side's phase 8 (mod 16), rows and strides multiples of 16, runs
+// as the peeled copy: 16-byte accesses on both sides instead of 8-byte words
+bool pack_peel_ok(const char *packed, const char *first, const Norm &n);
+struct PeelItem {
+  char *packed, *first;
+  Norm n;
+  uint32_t flags; // TEMPI_HIP_ITEM_REMOTE (an unpack's packed side)
+};
+int launch_pack_peel(bool pack, const std::vector<PeelItem> &items, hipStream_t s, tempi_ticket::Fold *fold);
+
 int launch_one(bool pack, char *packed, char *first, const Norm &n, hipStream_t s) {
+  if (pack_peel_ok(packed, first, n))
+    return launch_pack_peel(pack, std::vector<PeelItem>{{packed, first, n, gItemFlags}}, s, gFold);
   const int w = word_width(reinterpret_cast<uintptr_t>(packed),
                            reinterpret_cast<uintptr_t>(first), n);
   if (pack && dense_ok(n, w)) return launch_dense(packed, first, n, s);
@@ -1371,8 +1384,10 @@ int run_batch(bool pack, const tempi_hip_batch_item *items, int n, hipStream_t s
       gDesc += " " + (pack ? describe(items[i].desc, items[i].packed, items[i].first)
                            : describe(items[i].desc, items[i].first, items[i].packed));
   }
-  // group by (word width, rank): one launch per group and per kMax objects
+  // group by (word width, rank): one launch per group and per kMax objects;
+  // phase-8 items of 16-byte rows go to the peeled copy, launched last
   std::vector<Job> groups[5][TEMPI_HIP_MAX_DIMS + 1];
+  std::vector<PeelItem> peel;
   for (int i = 0; i < n; ++i) {
     Job j;
     j.packed = static_cast<char *>(items[i].packed);
@@ -1388,6 +1403,10 @@ int run_batch(bool pack, const tempi_hip_batch_item *items, int n, hipStream_t s
       if (e) return e;
       continue;
     }
+    if (pack_peel_ok(j.packed, j.first, j.n)) {
+      peel.push_back({j.packed, j.first, j.n, j.flags});
+      continue;
+    }
     const int w = word_width(reinterpret_cast<uintptr_t>(j.packed), reinterpret_cast<uintptr_t>(j.first), j.n);
     const int wi = w == 1 ? 0 : w == 2 ? 1 : w == 4 ? 2 : w == 8 ? 3 : 4;
     groups[wi][j.n.nd].push_back(j);
@@ -1399,7 +1418,7 @@ int run_batch(bool pack, const tempi_hip_batch_item *items, int n, hipStream_t s
     for (int nd = 0; nd <= TEMPI_HIP_MAX_DIMS; ++nd) {
       const std::vector<Job> &g = groups[wi][nd];
       if (g.empty()) continue;
-      tempi_ticket::Fold *f = wi * (TEMPI_HIP_MAX_DIMS + 1) + nd == lastGroup ? fold : nullptr;
+      tempi_ticket::Fold *f = peel.empty() && wi * (TEMPI_HIP_MAX_DIMS + 1) + nd == lastGroup ? fold : nullptr;
       int e = 0;
       switch (wi) {
       case 0: e = launch_batch_w<1>(pack, nd, g, s, f); break;
@@ -1410,7 +1429,7 @@ int run_batch(bool pack, const tempi_hip_batch_item *items, int n, hipStream_t s
       }
       if (e) return e;
     }
-  return 0;
+  return peel.empty() ? 0 : launch_pack_peel(pack, peel, s, fold);
 }
 
 // ------------------------------------------------------ strided -> strided copy
@@ -1835,6 +1854,35 @@ int copy_batch(const tempi_hip_copy_item *items, int n, void *stream, tempi_tick
   return 0;
 }
 
+bool pack_peel_ok(const char *packed, const char *first, const Norm &n) {
+  if (n.nd > kCopyND || norm_bytes(n) >= kMaxLaunchBytes) return false;
+  Norm flat{};
+  flat.block = norm_bytes(n);
+  return peel_ok(reinterpret_cast<uintptr_t>(packed), reinterpret_cast<uintptr_t>(first), flat, n);
+}
+
+// the peeled copy between each item's packed bytes (one contiguous side) and
+// its strided object; a pack reads the strided side, an unpack writes it (and
+// reads a remote packed side with system-scope loads)
+int launch_pack_peel(bool pack, const std::vector<PeelItem> &items, hipStream_t s, tempi_ticket::Fold *fold) {
+  std::vector<CopyJob> jobs;
+  for (const PeelItem &it : items) {
+    Norm flat{};
+    flat.block = norm_bytes(it.n);
+    CopyJob j;
+    char *dst = pack ? it.packed : it.first, *src = pack ? it.first : it.packed;
+    if (!make_side(src, pack ? it.n : flat, 8, &j.a.s) || !make_side(dst, pack ? flat : it.n, 8, &j.a.d))
+      return int(hipErrorInvalidValue);
+    j.a.nwords = uint32_t(flat.block / 8);
+    j.a.flags = (pack ? 0u : xcd_flag(it.first, it.n, false)) | (peel_mode() == 2 ? kCopyPlain : 0u) |
+                (it.flags & TEMPI_HIP_ITEM_REMOTE);
+    j.a.s2 = j.a.d2 = nullptr;
+    j.w = 0;
+    jobs.push_back(j);
+  }
+  return launch_copy_group<0>(jobs, s, fold);
+}
+
 } // namespace
 
 extern "C" {
@@ -1987,6 +2035,7 @@ int64_t tempi_hip_desc_bytes(const tempi_hip_desc *d) {
 int tempi_hip_word_width(const void *packed, const void *first, const tempi_hip_desc *d) {
   Norm n;
   if (!normalise(d, &n)) return -1;
+  if (pack_peel_ok(static_cast<const char *>(packed), static_cast<const char *>(first), n)) return 0;
   return word_width(reinterpret_cast<uintptr_t>(packed), reinterpret_cast<uintptr_t>(first), n);
 }
 

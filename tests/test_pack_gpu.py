@@ -699,3 +699,130 @@ def test_application_pinned_memory_waits_with_stream_sync(gpu, kind):
     r = subprocess.run([sys.executable, os.path.join(root, "tests", "mpi_progs", "app_pinned.py"), kind], cwd=root,
                        stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=200)
     assert r.returncode == 0 and "RESULT ok" in r.stdout, r.stdout[-3000:]
+
+
+PEEL_SHAPES = [  # (block, dims outermost first): rows and strides multiples of 16
+    (4096, [(9, 4608 * 70), (3, 4608)]),   # halo y face at a 4608-byte pitch
+    (4096, [(3, 4608 * 70), (64, 4608)]),  # halo z face
+    (16, [(1000, 48)]),
+    (48, [(7, 4096), (11, 64)]),
+    (32, [(3000, 32)]),                    # (normalises to one contiguous block)
+    (16, []),
+]
+
+
+@pytest.mark.parametrize("remote", [False, True])
+def test_pack_unpack_peeled(gpu, remote):
+    """a pack / unpack whose packed side sits at the
+    strided side's phase (both 8 bytes past a 16-byte boundary), rows and
+    strides multiples of 16, runs as the peeled copy (16-byte accesses, the
+    row seams in 8-byte halves; tempi_hip_word_width reports 0): single
+    objects through tempi_hip_pack / tempi_hip_unpack and the ticketed
+    synchronous forms, and a batch mixing peeled items with ordinary ones
+    (packed at phase 0: 8-byte words) -- packed bytes and unpacked canvases
+    exact against numpy, gaps and neighbours untouched. remote: the unpacks'
+    packed side is read with system-scope loads (TEMPI_HIP_ITEM_REMOTE)."""
+    torch = _torch()
+    import tempi_amd
+
+    H = ctypes.CDLL(tempi_amd.LIBTEMPI_HIP)
+    vp = ctypes.c_void_p
+    for f in ("tempi_hip_pack", "tempi_hip_unpack"):
+        getattr(H, f).argtypes = [vp, vp, ctypes.POINTER(HipDesc), vp]
+    H.tempi_hip_word_width.argtypes = [vp, vp, ctypes.POINTER(HipDesc)]
+    H.tempi_hip_pack_batch.argtypes = [vp, ctypes.c_int, vp]
+    H.tempi_hip_unpack_batch.argtypes = [vp, ctypes.c_int, vp]
+    for f in ("tempi_hip_pack_ticket", "tempi_hip_unpack_ticket"):
+        getattr(H, f).argtypes = [vp, vp, ctypes.POINTER(HipDesc), vp, ctypes.POINTER(ctypes.POINTER(ctypes.c_uint32)),
+                                  ctypes.POINTER(ctypes.c_uint32)]
+    H.tempi_hip_ticket_wait.argtypes = [vp, ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32]
+
+    def desc(block, dims):
+        d = HipDesc()
+        d.block, d.ndims = block, len(dims)
+        for j, (c, st) in enumerate(dims):
+            d.counts[j], d.strides[j] = c, st
+        return d
+
+    def index(block, dims):
+        idx = np.arange(block, dtype=np.int64)
+        for c, st in reversed(dims):
+            idx = (np.arange(c, dtype=np.int64)[:, None] * st + idx[None, :]).reshape(-1)
+        return idx
+
+    rng = np.random.default_rng(5)
+    cases = []
+    for k, (bl, dims) in enumerate(PEEL_SHAPES * 2):
+        idx = index(bl, dims)
+        host = rng.integers(0, 256, int(idx.max()) + 64, dtype=np.uint8)
+        src = torch.from_numpy(host).to(gpu)
+        ppos = 8 if k < len(PEEL_SHAPES) else 0  # the second round: packed at phase 0 (not peeled)
+        packed = torch.full((idx.size + 32,), 0xA5, dtype=torch.uint8, device=gpu)
+        cases.append(dict(d=desc(bl, dims), idx=idx, host=host, src=src, packed=packed, ppos=ppos))
+    torch.cuda.synchronize()
+    for c in cases:
+        first, pk = c["src"].data_ptr() + 8, c["packed"].data_ptr() + c["ppos"]
+        w = H.tempi_hip_word_width(pk, first, ctypes.byref(c["d"]))
+        assert (w == 0) == (c["ppos"] == 8), (w, c["ppos"])
+
+    def check_packed(c):
+        got = c["packed"].cpu().numpy()
+        n = c["idx"].size
+        assert np.array_equal(got[c["ppos"]:c["ppos"] + n], c["host"][8 + c["idx"]])
+        assert (got[:c["ppos"]] == 0xA5).all() and (got[c["ppos"] + n:] == 0xA5).all()
+
+    def check_unpacked(c, dst):
+        exp = np.full_like(c["host"], 0x5A)
+        exp[8 + c["idx"]] = c["host"][8 + c["idx"]]
+        assert np.array_equal(dst.cpu().numpy(), exp)
+
+    # single objects, plain and ticketed
+    for c in cases[:len(PEEL_SHAPES)]:
+        for ticket in (False, True):
+            c["packed"].fill_(0xA5)
+            dst = torch.full_like(c["src"], 0x5A)
+            torch.cuda.synchronize()
+            first, pk = c["src"].data_ptr() + 8, c["packed"].data_ptr() + c["ppos"]
+            if ticket:
+                flag, tk = ctypes.POINTER(ctypes.c_uint32)(), ctypes.c_uint32()
+                assert H.tempi_hip_pack_ticket(pk, first, ctypes.byref(c["d"]), None, ctypes.byref(flag),
+                                               ctypes.byref(tk)) == 0
+                assert H.tempi_hip_ticket_wait(None, flag, tk.value) == 0
+            else:
+                assert H.tempi_hip_pack(pk, first, ctypes.byref(c["d"]), None) == 0
+            torch.cuda.synchronize()
+            check_packed(c)
+            if remote:
+                release_l2(H)
+            if ticket:
+                assert H.tempi_hip_unpack_ticket(dst.data_ptr() + 8, pk, ctypes.byref(c["d"]), None,
+                                                 ctypes.byref(flag), ctypes.byref(tk)) == 0
+                assert H.tempi_hip_ticket_wait(None, flag, tk.value) == 0
+            else:
+                assert H.tempi_hip_unpack(dst.data_ptr() + 8, pk, ctypes.byref(c["d"]), None) == 0
+            torch.cuda.synchronize()
+            check_unpacked(c, dst)
+    # one batch: peeled and ordinary items together
+    for c in cases:
+        c["packed"].fill_(0xA5)
+        c["dst"] = torch.full_like(c["src"], 0x5A)
+    items = (HipItem * len(cases))()
+    for k, c in enumerate(cases):
+        items[k].packed = c["packed"].data_ptr() + c["ppos"]
+        items[k].first = c["src"].data_ptr() + 8
+        items[k].desc = c["d"]
+        items[k].flags = 0
+    torch.cuda.synchronize()
+    assert H.tempi_hip_pack_batch(items, len(cases), None) == 0
+    torch.cuda.synchronize()
+    for c in cases:
+        check_packed(c)
+    for k, c in enumerate(cases):
+        items[k].first = c["dst"].data_ptr() + 8
+        items[k].flags = ITEM_REMOTE if remote else 0
+    if remote:
+        release_l2(H)
+    assert H.tempi_hip_unpack_batch(items, len(cases), None) == 0
+    torch.cuda.synchronize()
+    for c in cases:
+        check_unpacked(c, c["dst"])

@@ -24,7 +24,7 @@
 #                shapes $KOFF_SHAPES -> gpurun_out/koff.jsonl
 #   launchsplit  tools/bin/launchsplit: dispatch / execution / visibility of
 #                the config-1 synchronous call -> gpurun_out/launchsplit.jsonl
-#   halo-ab      1-rank halo_exchange $HALO_ITERS (default 30) 512 under each
+#   halo-ab      halo_exchange $HALO_ITERS (default 30) 512 at $HALO_RANKS (default 1) under each
 #                environment of $HALO_AB ("A=1,B=2 A=0" style, "-" for none),
 #                $HALO_ROUNDS rotations -> gpurun_out/halo_ab.jsonl
 #   ls-ab        launchsplit with TEMPI_TICKET_SLOTS=1 / 0, $LS_ROUNDS rotations
@@ -111,7 +111,7 @@ for step in "$@"; do
     for r in $(seq ${HALO_ROUNDS:-3}); do
       for v in $HALO_AB; do
         envs=$([ "$v" = "-" ] && echo "" || echo "$v" | tr ',' ' ')
-        env $envs timeout -k 10 300 tempi_amd/lib/halo_exchange ${HALO_ITERS:-30} 512 2>> $O/halo_ab.err \
+        env $envs timeout -k 10 300 $MPIEXEC -n ${HALO_RANKS:-1} tempi_amd/lib/halo_exchange ${HALO_ITERS:-30} 512 2>> $O/halo_ab.err \
           | grep '^{' | sed "s/^{/{\"variant\": \"$v\", \"round\": $r, /" >> $O/halo_ab.jsonl || exit 21
       done
     done
