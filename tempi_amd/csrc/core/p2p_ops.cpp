@@ -292,21 +292,6 @@ void flush() {
 
 namespace {
 
-// An IPC slab holds the packed bytes at the object's own phase (mod 16) when
-// that lets the gather here and the receiver's scatter (whose object shares
-// the phase in a halo exchange) move 16-byte words instead of 8-byte ones:
-// the first byte 8 bytes past a 16-byte boundary, rows and strides multiples
-// of 16 -- the halo's y / z faces (pack_kernels.hip, the peeled copy;
-// VERDICT r05 next 2). The descriptor's offset carries it to the receiver.
-size_t ipc_phase(const TypeRecord *rec, const char *origin, int count) {
-  const StridedBlock &sb = rec->desc;
-  if (!sb.valid || ((reinterpret_cast<uintptr_t>(origin) + uintptr_t(sb.start)) & 15) != 8 || sb.block % 16)
-    return 0;
-  for (const auto &d : sb.dims)
-    if (d.stride % 16) return 0;
-  return count > 1 && sb.extent % 16 ? 0 : 8;
-}
-
 struct IsendOp : Op {
   RecordRef rec;      // the type (kept alive: MPI_Type_free may come first)
   const char *origin; // GPU-visible
@@ -316,7 +301,6 @@ struct IsendOp : Op {
   Method method;
   int64_t bytes;
   Slab *dslab = nullptr, *hslab = nullptr;
-  size_t phase = 0; // IPC: the packed bytes start this far into the slab (ipc_phase)
   IpcDesc desc{};
 
   uint64_t key;
@@ -334,9 +318,8 @@ struct IsendOp : Op {
       hslab = pinned_pool().get(size_t(bytes), device);
       pendingPack.add_items(this, *rec->packer, hslab->dev, origin, count);
     } else {
-      phase = method == Method::IPC ? ipc_phase(r, o, c) : 0;
-      dslab = device_pool().get(size_t(bytes) + phase, device);
-      pendingPack.add_items(this, *rec->packer, static_cast<char *>(dslab->dev) + phase, origin, count);
+      dslab = device_pool().get(size_t(bytes), device);
+      pendingPack.add_items(this, *rec->packer, dslab->dev, origin, count);
       if (method == Method::STAGED) {
         hslab = pinned_pool().get(size_t(bytes), device);
         pendingPack.stages.push_back({hslab->host, dslab->dev, size_t(bytes), device});
@@ -368,7 +351,7 @@ struct IsendOp : Op {
       desc.magic[0] = kMagic0;
       desc.magic[1] = kMagic1;
       desc.slabId = dslab->id;
-      desc.offset = phase;
+      desc.offset = 0;
       desc.bytes = bytes;
       desc.senderWorld = state.worldRank;
       desc.senderPid = state.pid;

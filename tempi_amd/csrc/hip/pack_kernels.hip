@@ -1297,20 +1297,7 @@ template <int W> int launch_il(bool pack, char *packed, char *first, const Norm 
   }
 }
 
-// (with the copy kernels below) a pack / unpack whose packed side sits at
-// the strided side's phase 8 (mod 16), rows and strides multiples of 16, runs
-// as the peeled copy: 16-byte accesses on both sides instead of 8-byte words
-bool pack_peel_ok(const char *packed, const char *first, const Norm &n);
-struct PeelItem {
-  char *packed, *first;
-  Norm n;
-  uint32_t flags; // TEMPI_HIP_ITEM_REMOTE (an unpack's packed side)
-};
-int launch_pack_peel(bool pack, const std::vector<PeelItem> &items, hipStream_t s, tempi_ticket::Fold *fold);
-
 int launch_one(bool pack, char *packed, char *first, const Norm &n, hipStream_t s) {
-  if (pack_peel_ok(packed, first, n))
-    return launch_pack_peel(pack, std::vector<PeelItem>{{packed, first, n, gItemFlags}}, s, gFold);
   const int w = word_width(reinterpret_cast<uintptr_t>(packed),
                            reinterpret_cast<uintptr_t>(first), n);
   if (pack && dense_ok(n, w)) return launch_dense(packed, first, n, s);
@@ -1384,10 +1371,8 @@ int run_batch(bool pack, const tempi_hip_batch_item *items, int n, hipStream_t s
       gDesc += " " + (pack ? describe(items[i].desc, items[i].packed, items[i].first)
                            : describe(items[i].desc, items[i].first, items[i].packed));
   }
-  // group by (word width, rank): one launch per group and per kMax objects;
-  // phase-8 items of 16-byte rows go to the peeled copy, launched last
+  // group by (word width, rank): one launch per group and per kMax objects
   std::vector<Job> groups[5][TEMPI_HIP_MAX_DIMS + 1];
-  std::vector<PeelItem> peel;
   for (int i = 0; i < n; ++i) {
     Job j;
     j.packed = static_cast<char *>(items[i].packed);
@@ -1403,10 +1388,6 @@ int run_batch(bool pack, const tempi_hip_batch_item *items, int n, hipStream_t s
       if (e) return e;
       continue;
     }
-    if (pack_peel_ok(j.packed, j.first, j.n)) {
-      peel.push_back({j.packed, j.first, j.n, j.flags});
-      continue;
-    }
     const int w = word_width(reinterpret_cast<uintptr_t>(j.packed), reinterpret_cast<uintptr_t>(j.first), j.n);
     const int wi = w == 1 ? 0 : w == 2 ? 1 : w == 4 ? 2 : w == 8 ? 3 : 4;
     groups[wi][j.n.nd].push_back(j);
@@ -1418,7 +1399,7 @@ int run_batch(bool pack, const tempi_hip_batch_item *items, int n, hipStream_t s
     for (int nd = 0; nd <= TEMPI_HIP_MAX_DIMS; ++nd) {
       const std::vector<Job> &g = groups[wi][nd];
       if (g.empty()) continue;
-      tempi_ticket::Fold *f = peel.empty() && wi * (TEMPI_HIP_MAX_DIMS + 1) + nd == lastGroup ? fold : nullptr;
+      tempi_ticket::Fold *f = wi * (TEMPI_HIP_MAX_DIMS + 1) + nd == lastGroup ? fold : nullptr;
       int e = 0;
       switch (wi) {
       case 0: e = launch_batch_w<1>(pack, nd, g, s, f); break;
@@ -1429,7 +1410,7 @@ int run_batch(bool pack, const tempi_hip_batch_item *items, int n, hipStream_t s
       }
       if (e) return e;
     }
-  return peel.empty() ? 0 : launch_pack_peel(pack, peel, s, fold);
+  return 0;
 }
 
 // ------------------------------------------------------ strided -> strided copy
@@ -1632,11 +1613,22 @@ __device__ void copy_body_peel(const CArgs &a, uint32_t blk, uint32_t nblk) {
   }
 }
 
+// Peeled items travel in the 8-byte-word launches (their sides count 8-byte
+// words too), flagged per item: a flush of a halo then stays ONE launch in
+// which the x faces' isolated rows and the y / z faces' streams overlap.
+// Launched on their own, after the 8-byte-word items, the peeled faces made
+// the 1-rank 512^3 halo 6 % and the 2-rank one 8 % slower than no peel at all
+// (profiles/r06/halo_peel_ab_s4.jsonl), although a 1 GiB copy of that row
+// shape runs 13-25 % faster peeled.
+constexpr uint32_t kPeelItem = 1u << 28; // internal flag bit (never a TEMPI_HIP_ITEM_*)
 template <int W> __device__ __forceinline__ void copy_any(const CArgs &a, uint32_t blk, uint32_t nblk) {
-  if constexpr (W == 0)
-    copy_body_peel(a, blk, nblk);
-  else
-    copy_body<W>(a, blk, nblk);
+  if constexpr (W == 8) {
+    if (a.flags & kPeelItem) {
+      copy_body_peel(a, blk, nblk);
+      return;
+    }
+  }
+  copy_body<W>(a, blk, nblk);
 }
 
 template <int W> __global__ __launch_bounds__(kCopyBlock) void copy_kernel(const CArgs a, const Sig sg) {
@@ -1710,8 +1702,16 @@ int peel_mode() {
   return m;
 }
 bool peel_enabled() { return peel_mode() != 0; }
+// TEMPI_PEEL_MIN_BYTES (A/B): objects below it keep the 8-byte-word plan
+int64_t peel_min_bytes() {
+  static const int64_t v = [] {
+    const char *e = std::getenv("TEMPI_PEEL_MIN_BYTES");
+    return e ? int64_t(std::strtoll(e, nullptr, 10)) : int64_t(0);
+  }();
+  return v;
+}
 bool peel_ok(uintptr_t dst, uintptr_t src, const Norm &nd, const Norm &ns) {
-  if (!peel_enabled() || (dst & 15) != 8 || (src & 15) != 8) return false;
+  if (!peel_enabled() || (dst & 15) != 8 || (src & 15) != 8 || norm_bytes(ns) < peel_min_bytes()) return false;
   for (const Norm *n : {&nd, &ns}) {
     if (n->block % 16) return false;
     for (int k = 0; k < n->nd; ++k)
@@ -1733,8 +1733,9 @@ bool plan_copy(void *dst, const void *src, const tempi_hip_desc *dd, const tempi
   if (!make_side(const_cast<char *>(static_cast<const char *>(src)), ns, w, &job->a.s)) return false;
   if (!make_side(static_cast<char *>(dst), nd, w, &job->a.d)) return false;
   job->a.nwords = uint32_t(bytes / w);
-  if (peel) w = 0; // (the sides count 8-byte words, as the peeled body expects)
-  job->a.flags = xcd_flag(static_cast<char *>(dst), nd, false) | (peel && peel_mode() == 2 ? kCopyPlain : 0u);
+  if (peel) w = 0; // (the sides count 8-byte words, as the peeled body expects; launched with W = 8)
+  job->a.flags = xcd_flag(static_cast<char *>(dst), nd, false) | (peel ? kPeelItem : 0u) |
+                 (peel && peel_mode() == 2 ? kCopyPlain : 0u);
   job->a.s2 = job->a.d2 = nullptr;
   job->w = w;
   return true;
@@ -1823,21 +1824,21 @@ int copy_batch(const tempi_hip_copy_item *items, int n, void *stream, tempi_tick
                describe(items[i].src, items[i].src_first, nullptr) +
                ((items[i].flags & TEMPI_HIP_ITEM_REMOTE) ? " remote" : "");
   }
-  std::vector<CopyJob> groups[6];
+  std::vector<CopyJob> groups[5];
   for (int i = 0; i < n; ++i) {
     CopyJob j;
     if (!plan_copy(items[i].dst_first, items[i].src_first, &items[i].dst, &items[i].src, &j))
       return int(hipErrorInvalidValue);
     j.a.flags |= items[i].flags & TEMPI_HIP_ITEM_REMOTE;
     if (j.a.nwords == 0) continue;
-    const int wi = j.w == 1 ? 0 : j.w == 2 ? 1 : j.w == 4 ? 2 : j.w == 8 ? 3 : j.w == 16 ? 4 : 5;
+    const int wi = j.w == 1 ? 0 : j.w == 2 ? 1 : j.w == 4 ? 2 : j.w == 8 || j.w == 0 ? 3 : 4;
     groups[wi].push_back(j);
   }
   hipStream_t s = static_cast<hipStream_t>(stream);
   int lastGroup = -1;
-  for (int wi = 0; wi < 6; ++wi)
+  for (int wi = 0; wi < 5; ++wi)
     if (!groups[wi].empty()) lastGroup = wi;
-  for (int wi = 0; wi < 6; ++wi) {
+  for (int wi = 0; wi < 5; ++wi) {
     if (groups[wi].empty()) continue;
     tempi_ticket::Fold *f = wi == lastGroup ? fold : nullptr;
     int e = 0;
@@ -1846,41 +1847,11 @@ int copy_batch(const tempi_hip_copy_item *items, int n, void *stream, tempi_tick
     case 1: e = launch_copy_group<2>(pair_jobs(groups[wi]), s, f); break;
     case 2: e = launch_copy_group<4>(pair_jobs(groups[wi]), s, f); break;
     case 3: e = launch_copy_group<8>(pair_jobs(groups[wi]), s, f); break;
-    case 4: e = launch_copy_group<16>(pair_jobs(groups[wi]), s, f); break;
-    default: e = launch_copy_group<0>(pair_jobs(groups[wi]), s, f); break;
+    default: e = launch_copy_group<16>(pair_jobs(groups[wi]), s, f); break;
     }
     if (e) return e;
   }
   return 0;
-}
-
-bool pack_peel_ok(const char *packed, const char *first, const Norm &n) {
-  if (n.nd > kCopyND || norm_bytes(n) >= kMaxLaunchBytes) return false;
-  Norm flat{};
-  flat.block = norm_bytes(n);
-  return peel_ok(reinterpret_cast<uintptr_t>(packed), reinterpret_cast<uintptr_t>(first), flat, n);
-}
-
-// the peeled copy between each item's packed bytes (one contiguous side) and
-// its strided object; a pack reads the strided side, an unpack writes it (and
-// reads a remote packed side with system-scope loads)
-int launch_pack_peel(bool pack, const std::vector<PeelItem> &items, hipStream_t s, tempi_ticket::Fold *fold) {
-  std::vector<CopyJob> jobs;
-  for (const PeelItem &it : items) {
-    Norm flat{};
-    flat.block = norm_bytes(it.n);
-    CopyJob j;
-    char *dst = pack ? it.packed : it.first, *src = pack ? it.first : it.packed;
-    if (!make_side(src, pack ? it.n : flat, 8, &j.a.s) || !make_side(dst, pack ? flat : it.n, 8, &j.a.d))
-      return int(hipErrorInvalidValue);
-    j.a.nwords = uint32_t(flat.block / 8);
-    j.a.flags = (pack ? 0u : xcd_flag(it.first, it.n, false)) | (peel_mode() == 2 ? kCopyPlain : 0u) |
-                (it.flags & TEMPI_HIP_ITEM_REMOTE);
-    j.a.s2 = j.a.d2 = nullptr;
-    j.w = 0;
-    jobs.push_back(j);
-  }
-  return launch_copy_group<0>(jobs, s, fold);
 }
 
 } // namespace
@@ -2035,7 +2006,6 @@ int64_t tempi_hip_desc_bytes(const tempi_hip_desc *d) {
 int tempi_hip_word_width(const void *packed, const void *first, const tempi_hip_desc *d) {
   Norm n;
   if (!normalise(d, &n)) return -1;
-  if (pack_peel_ok(static_cast<const char *>(packed), static_cast<const char *>(first), n)) return 0;
   return word_width(reinterpret_cast<uintptr_t>(packed), reinterpret_cast<uintptr_t>(first), n);
 }
 

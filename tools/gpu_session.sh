@@ -27,7 +27,7 @@
 #   halo-ab      halo_exchange $HALO_ITERS (default 30) 512 at $HALO_RANKS (default 1) under each
 #                environment of $HALO_AB ("A=1,B=2 A=0" style, "-" for none),
 #                $HALO_ROUNDS rotations -> gpurun_out/halo_ab.jsonl
-#   ls-ab        launchsplit with TEMPI_TICKET_SLOTS=1 / 0, $LS_ROUNDS rotations
+#   ls-ab        launchsplit under each environment of $LS_AB (as HALO_AB), $LS_ROUNDS rotations
 #   launch-check the GPU tests LC_FOCUS selects with TEMPI_LAUNCH_CHECK=1 (every
 #                TEMPI launch synchronised and checked)
 #   kpmc         rocprofv3 --pmc passes ($KPMC_PASSES, ';'-separated counter
@@ -123,9 +123,10 @@ for k,v in d.items(): print(k, v)" ;;
   ls-ab)
     rm -f $O/launchsplit_ab.jsonl
     for r in $(seq ${LS_ROUNDS:-3}); do
-      for v in 1 0; do
-        TEMPI_TICKET_SLOTS=$v timeout -k 10 120 tools/bin/launchsplit ${LS_REPS:-2000} 2>&1 \
-          | sed "s/^{/{\"slots\": $v, \"round\": $r, /" >> $O/launchsplit_ab.jsonl || exit 22
+      for v in ${LS_AB:--}; do
+        envs=$([ "$v" = "-" ] && echo "" || echo "$v" | tr ',' ' ')
+        env $envs timeout -k 10 120 tools/bin/launchsplit ${LS_REPS:-2000} 2>&1 \
+          | sed "s/^{/{\"variant\": \"$v\", \"round\": $r, /" >> $O/launchsplit_ab.jsonl || exit 22
       done
     done
     cat $O/launchsplit_ab.jsonl ;;
