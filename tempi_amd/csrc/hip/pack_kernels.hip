@@ -1008,10 +1008,21 @@ bool partial_pages(const Norm &n) {
   return inner >= 4096 && n.block < 4096 && inner - n.block >= 128;
 }
 
+// One exception above TEMPI_XCD_MAX_BLOCK: 2D rows of
+// 4-8 KiB a few bytes apart (the sweep's 4096 : 4112). Each row's last line
+// is shared with the next row's first, and in the dealt order the two halves
+// come from workgroups on different XCDs: two partial-line writes (32-byte
+// requests, 2.1 per row, profiles/r06/kpmc_rowends_s3.txt) instead of one
+// line. Mapped: unpack +6 to +9.5 % (5.54 -> 5.90 TB/s); the same rule on
+// 1 and 2 KiB rows and on the 3D forms of all three costs 0.5-2 %
+// (profiles/r06/xcd_4112_ab_s5.jsonl, xcd_ab_wide_s6.jsonl), so it stays
+// this narrow.
+bool wide_shared_line_rows(const Norm &n) { return n.nd == 1 && n.block >= 4096 && n.block < 8192; }
+
 uint32_t xcd_flag(const char *first, const Norm &n, bool pack) {
   if (!TEMPI_XCD_MAP) return 0;
   if (TEMPI_XCD_PAGES && (!pack || TEMPI_XCD_PAGES_PACK) && partial_pages(n)) return kXcdRange;
-  if (pack || n.nd == 0 || n.block >= TEMPI_XCD_MAX_BLOCK) return 0;
+  if (pack || n.nd == 0 || (n.block >= TEMPI_XCD_MAX_BLOCK && !wide_shared_line_rows(n))) return 0;
   const int64_t inner = n.str[n.nd - 1];
   if (inner < n.block || inner - n.block >= 128) return 0;
   uint64_t g = reinterpret_cast<uintptr_t>(first) | uint64_t(n.block);
