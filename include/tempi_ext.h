@@ -109,8 +109,8 @@ void tempi_perf_reload(void);
 /* the message size from which a NON-blocking AUTO send of `block`-byte
    blocks to a co-located peer takes IPC instead of ONESHOT: priced per batch
    from this node's own TEMPI_CACHE_DIR/perf.json when one was measured here
-   (*from_model = 1), else the built-in 4096 (*from_model = 0). INT64_MAX:
-   never IPC; -1 before MPI_Init. */
+   (*from_model = 1; the model may lower the built-in 4096, never raise it),
+   else the built-in 4096 (*from_model = 0); -1 before MPI_Init. */
 int64_t tempi_ipc_threshold(int64_t block, int *from_model);
 /* the same pricing over a perf.json document (no MPI needed): the threshold,
    INT64_MAX for never, -1 when a curve it needs is missing, -2 when the

@@ -316,6 +316,7 @@ bool local_copy(const void *sbuf, int scount, MPI_Datatype stype, void *rbuf, in
 
 MPI_Request start_local_copies(const LocalCopies &plan) {
   counters.send_direct += plan.items.size();
+  counters.bytes_direct += uint64_t(plan.bytes);
   return add(new_local_copies(plan));
 }
 

@@ -141,7 +141,15 @@ std::map<int64_t, int64_t> nbThresholdCache; // block -> batch-priced threshold 
 // per batch from this node's own perf.json when one was measured here
 // (TEMPI_CACHE_DIR, e.g. by bench.py's measure_system run at N > 1), else the
 // built-in ipcMinBytes -- the shipped file was measured with both ranks on one
-// GPU, so its GPU-GPU curve never crossed a link.
+// GPU, so its GPU-GPU curve never crossed a link. The model may LOWER the
+// threshold, never raise it above ipcMinBytes: every measurement that moved
+// burst messages from IPC to ONESHOT lost -- per-message pricing in round 3
+// (halo 1.3-2x slower), and the batch pricing itself in the round-6 N = 8
+// rehearsal, where a node file measured on one shared GPU put the threshold
+// at 16-64 KiB and the halo ran 4.6 ms/iter against 3.75 at 4 KiB
+// (profiles/r06/bench_line_torchrun_n8_s7.json): single-message marginal
+// costs from a 2-rank ping-pong do not see 8 ranks' bursts contending for
+// the host link that every ONESHOT byte crosses.
 int64_t nb_ipc_threshold(int64_t block, bool *fromModel) {
   *fromModel = false;
   if (!systemPerformanceLoaded || !systemPerformanceNode) return ipcMinBytes;
@@ -155,7 +163,7 @@ int64_t nb_ipc_threshold(int64_t block, bool *fromModel) {
   }
   if (it->second < 0) return ipcMinBytes;
   *fromModel = true;
-  return it->second;
+  return std::min(it->second, ipcMinBytes);
 }
 
 // The measured model prices one message on its own: every term is a

@@ -185,11 +185,11 @@ def test_timeline_records_entry_points(tmp_path):
 def test_nonblocking_ipc_threshold_follows_node_perf_json(tmp_path):
     """non-blocking AUTO sends take IPC from a threshold
     priced per batch from THIS node's perf.json (TEMPI_CACHE_DIR) when one was
-    measured here -- a synthetic file whose curves cross at ~12 KiB moves it
-    to 16 KiB, a costlier per-message IPC to 64 KiB, and tempi_choose_method's
-    non-blocking picks follow it -- and stay at the built-in 4 KiB with only
-    the shipped model (measured with both ranks on one GPU). Blocking sends
-    keep pricing each message by the model."""
+    measured here -- synthetic files whose curves cross at ~150 B and ~1.2 KiB
+    move it to 256 B and 2 KiB, and tempi_choose_method's non-blocking picks
+    follow it; one crossing at ~12 KiB is held at the built-in 4 KiB, which
+    the model may lower but never raise (p2p_routes.cpp) -- and stay at 4 KiB
+    with only the shipped model (measured with both ranks on one GPU)."""
     from tests.test_perf_model import _synthetic_perf
 
     def pick(cache):
@@ -200,7 +200,7 @@ def test_nonblocking_ipc_threshold_follows_node_perf_json(tmp_path):
     shipped = pick(tmp_path / "none")
     assert shipped["loaded"] == 1 and shipped["source"].endswith("perf_mi355x.json"), shipped
     assert shipped["nb_threshold"] == [[8, 4096, 0], [512, 4096, 0]], shipped
-    for fixed, exp in ((1.1e-6, 16384), (4.4e-6, 65536)):
+    for fixed, exp in ((0.0135e-6, 256), (0.11e-6, 2048), (1.1e-6, 4096)):
         d = tmp_path / f"node_{exp}"
         d.mkdir()
         (d / "perf.json").write_text(json.dumps(_synthetic_perf(fixed, 100e9)))

@@ -203,7 +203,8 @@ def test_full_size_2d_exact(mpi, gpu, rows, pitch, bl):
 
 @pytest.mark.parametrize("z,y,pitch,bl", [(4000, 4000, 8, 4),       # 3D, planes 24 B off line alignment
                                           (3001, 3000, 18, 2),       # 3D, 2-byte words
-                                          (1, 1000003, 144, 128)])   # 2D, 16-byte gap
+                                          (1, 1000003, 144, 128),    # 2D, 16-byte gap
+                                          (1, 262147, 4112, 4096)])  # 2D 4 KiB rows, 16-byte gap (round 6)
 def test_xcd_mapped_scatter_exact(mpi, gpu, z, y, pitch, bl):
     """Shapes whose unpack takes the XCD-range tile map (partial sectors,
     neighbouring rows sharing lines), with tile counts that are not multiples

@@ -25,4 +25,5 @@ print("line bytes", len(l), "value", d["value"], "ms_per_step", d["ms_per_step"]
       "dropped", d.get("dropped"))
 print("halo", d.get("halo"))
 print("alltoallv", d.get("alltoallv"))
+print("transport", d.get("transport"))
 PY
