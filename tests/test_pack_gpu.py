@@ -826,3 +826,18 @@ def test_pack_unpack_phase8_rows(gpu, remote):
     torch.cuda.synchronize()
     for c in cases:
         check_unpacked(c, c["dst"])
+
+
+def test_goldens_with_torch_runtime_only(gpu):
+    """The 153 MPICH goldens through TEMPI in a process whose ONLY HIP
+    runtime is torch's (torch imported before libtempi is loaded: the
+    configuration bench.py and smoke() run in; this pytest process holds two,
+    DESIGN §2.2): packed bytes, positions and unpacked buffers bit-exact, the
+    strided cases on the GPU path (tests/mpi_progs/torch_runtime_parity.py)"""
+    import subprocess
+    import sys
+
+    root = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+    r = subprocess.run([sys.executable, os.path.join(root, "tests", "mpi_progs", "torch_runtime_parity.py")],
+                       cwd=root, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=300)
+    assert r.returncode == 0 and f"RESULT ok {len(CASES)} cases" in r.stdout, r.stdout[-3000:]
