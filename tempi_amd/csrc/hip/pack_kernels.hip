@@ -1560,7 +1560,7 @@ template <int W> __device__ __forceinline__ void copy_body(const CArgs &a, uint3
   }
 }
 
-// ---- the PEELED copy (W = 0 below)
+// ---- the PEELED copy (kPeelItem items of the 8-byte-word launches)
 //
 // Both sides start 8 bytes past a 16-byte boundary, with rows of a multiple
 // of 16 bytes at strides that are multiples of 16: the halo's y / z faces, 4
@@ -1629,8 +1629,9 @@ __device__ void copy_body_peel(const CArgs &a, uint32_t blk, uint32_t nblk) {
 // which the x faces' isolated rows and the y / z faces' streams overlap.
 // Launched on their own, after the 8-byte-word items, the peeled faces made
 // the 1-rank 512^3 halo 6 % and the 2-rank one 8 % slower than no peel at all
-// (profiles/r06/halo_peel_ab_s4.jsonl), although a 1 GiB copy of that row
-// shape runs 13-25 % faster peeled.
+// (profiles/r06/halo_peel_ab_n1_s4.jsonl, _n2_s4), although a 1 GiB copy of
+// that row shape runs 13-25 % faster peeled; merged, the halo is within noise
+// of no peel (halo_peel_merged_ab_n1_s5.jsonl).
 constexpr uint32_t kPeelItem = 1u << 28; // internal flag bit (never a TEMPI_HIP_ITEM_*)
 template <int W> __device__ __forceinline__ void copy_any(const CArgs &a, uint32_t blk, uint32_t nblk) {
   if constexpr (W == 8) {
@@ -1695,7 +1696,7 @@ bool make_side(char *first, const Norm &n, int W, CSide *c) {
 
 struct CopyJob {
   CArgs a;
-  int w; // word width; 0: the peeled copy (16-byte chunks, 8-byte seam halves)
+  int w; // word width; 0: the peeled copy (16-byte chunks, 8-byte seam halves; launched with W = 8)
 };
 
 #ifndef TEMPI_COPY_PEEL
