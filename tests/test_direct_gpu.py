@@ -496,3 +496,91 @@ def test_copy_peeled_rows(mpi, gpu, remote):
     assert H.tempi_hip_copy_word_width(p + 8, p + 4 + 4096, ctypes.byref(sd), ctypes.byref(sd)) == 4
     odd = desc(32, [(100, 40)])
     assert H.tempi_hip_copy_word_width(p + 8, p + 8 + 8192, ctypes.byref(odd), ctypes.byref(odd)) == 8
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_copy_peeled_random(mpi, gpu, seed):
+    """The peeled copy on random shapes: both sides 8 bytes past a 16-byte
+    boundary, blocks of 16-byte multiples (16 B - 4 KiB) over 1-3 strided
+    dimensions with strides that are multiples of 16 (positive and
+    negative), the destination another random shape of the same byte count
+    or the same shape; 1-40 items a batch mixed with 8-byte-word items, some
+    paired (same shapes), half of them remote. Every destination byte
+    against numpy, gaps untouched."""
+    import torch
+
+    H = _hip()
+    H.tempi_hip_copy_word_width.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(HipDesc),
+                                            ctypes.POINTER(HipDesc)]
+    rng = random.Random(seed)
+
+    def shape(total=None):
+        """(block, [(count, stride) outermost first]) with strides multiples of 16"""
+        while True:
+            bl = 16 * rng.choice([1, 2, 3, 4, 8, 16, 32, 64, 256])
+            nd = rng.choice([0, 1, 1, 2, 2, 3])
+            dims, inner = [], bl
+            for _ in range(nd):
+                c = rng.choice([1, 2, 3, 5, 7, 16, 33])
+                st = inner + 16 * rng.choice([0, 1, 2, 5, 32])
+                st = -st if rng.random() < 0.15 else st
+                dims.insert(0, (c, st))
+                inner = c * abs(st)
+            size = bl
+            for c, _ in dims:
+                size *= c
+            if total is None or size == total:
+                return bl, dims
+            if total % bl == 0 and total // bl < 100000:  # the same bytes as one strided dimension
+                n = total // bl
+                return bl, [(n, bl + 16 * rng.choice([0, 1, 3]))]
+
+    def index(block, dims):
+        idx = np.arange(block, dtype=np.int64)
+        for c, st in reversed(dims):
+            idx = (np.arange(c, dtype=np.int64)[:, None] * st + idx[None, :]).reshape(-1)
+        return idx
+
+    def desc(block, dims):
+        d = HipDesc()
+        d.block, d.ndims = block, len(dims)
+        for j, (c, st) in enumerate(dims):
+            d.counts[j], d.strides[j] = c, st
+        return d
+
+    cases = []
+    n = rng.choice([1, 5, 17, 40])
+    for i in range(n):
+        sb, sdims = shape()
+        size = sb
+        for c, _ in sdims:
+            size *= c
+        db, ddims = (sb, sdims) if rng.random() < 0.4 else shape(size)
+        sidx, didx = index(sb, sdims), index(db, ddims)
+        if sidx.size != didx.size:
+            continue
+        phase = 8 if rng.random() < 0.8 else 0  # (some ordinary 16-byte-aligned items in the batch)
+        sh0, dh0 = int(-sidx.min()) + phase, int(-didx.min()) + phase  # room for negative strides
+        host = np.random.default_rng(seed * 1000 + i).integers(0, 256, sh0 + int(sidx.max()) + 64, dtype=np.uint8)
+        canvas = np.random.default_rng(seed * 3000 + i).integers(0, 256, dh0 + int(didx.max()) + 64, dtype=np.uint8)
+        src, dst = torch.from_numpy(host).to(gpu), torch.from_numpy(canvas).to(gpu)
+        it = CopyItem()
+        it.src_first, it.dst_first = src.data_ptr() + sh0, dst.data_ptr() + dh0
+        it.src, it.dst = desc(sb, sdims), desc(db, ddims)
+        it.flags = ITEM_REMOTE if i % 2 else 0
+        w = H.tempi_hip_copy_word_width(it.dst_first, it.src_first, ctypes.byref(it.dst), ctypes.byref(it.src))
+        if w < 0:
+            continue
+        assert (w == 0) == (phase == 8), (w, phase, sb, sdims, db, ddims)
+        exp = canvas.copy()
+        exp[dh0 + didx] = host[sh0 + sidx]
+        cases.append((it, src, dst, exp))
+    if not cases:
+        pytest.skip("no supported item drawn")
+    items = (CopyItem * len(cases))(*[c[0] for c in cases])
+    torch.cuda.synchronize()
+    release_l2(H)
+    assert H.tempi_hip_copy_batch(items, len(cases), None) == 0
+    torch.cuda.synchronize()
+    for k, (it, src, dst, exp) in enumerate(cases):
+        assert np.array_equal(dst.cpu().numpy(), exp), f"item {k}"
