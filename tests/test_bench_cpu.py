@@ -169,7 +169,29 @@ def _n8_record():
         for p in rec[name]["points"]:
             p["ranks"] = 8
     rec["perf_model"]["auto_model"] = "/some/very/long/path/" + "x" * 200 + "/perf.json"
+    # the transport block (round 6), every route used, with the largest counts
+    big = {"messages": 123456789, "bytes": 123456789012345}
+    rec["transport"] = {"over": "every N > 1 section, all ranks",
+                        "routes": {k: dict(big) for k in ("ipc", "ipc_copy", "oneshot", "staged", "device", "direct")},
+                        "library_sends": 123456789, "self_matched": 123456, "batches": 1234567, "ticket_batches": 12345,
+                        "canary_ok": 56, "canary_fail": 0, "ipc_threshold": {"block_24": 4096, "block_512": 4096,
+                                                                              "from_node_perf_json": True},
+                        "perf_json_measured_on_node": True}
     return rec
+
+
+def test_transport_block_in_the_line():
+    """the N > 1 line carries the transport block's
+    per-route [messages, bytes], library sends, canaries, the IPC threshold
+    and where the model came from; with the ranks on one GPU the canaries
+    are null with the reason"""
+    rec = _n8_record()
+    t = bench.compact_line(rec, False)["transport"]
+    assert t["routes"]["ipc"] == [123456789, 123456789012345] and t["canary_ok"] == 56
+    assert t["ipc_threshold"]["from_node_perf_json"] is True and t["perf_json_measured_on_node"] is True
+    rec["transport"].update(canary_ok=None, canary_fail=None, canary_note="shared GPU: ...")
+    t = bench.compact_line(rec, True)["transport"]
+    assert t["canary_ok"] is None and t["null_because"] == "shared GPU"
 
 
 @pytest.mark.parametrize("which", ["n1", "n8", "n8_shared"])
