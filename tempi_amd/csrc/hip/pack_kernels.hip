@@ -1714,16 +1714,8 @@ int peel_mode() {
   return m;
 }
 bool peel_enabled() { return peel_mode() != 0; }
-// TEMPI_PEEL_MIN_BYTES (A/B): objects below it keep the 8-byte-word plan
-int64_t peel_min_bytes() {
-  static const int64_t v = [] {
-    const char *e = std::getenv("TEMPI_PEEL_MIN_BYTES");
-    return e ? int64_t(std::strtoll(e, nullptr, 10)) : int64_t(0);
-  }();
-  return v;
-}
 bool peel_ok(uintptr_t dst, uintptr_t src, const Norm &nd, const Norm &ns) {
-  if (!peel_enabled() || (dst & 15) != 8 || (src & 15) != 8 || norm_bytes(ns) < peel_min_bytes()) return false;
+  if (!peel_enabled() || (dst & 15) != 8 || (src & 15) != 8) return false;
   for (const Norm *n : {&nd, &ns}) {
     if (n->block % 16) return false;
     for (int k = 0; k < n->nd; ++k)
