@@ -828,16 +828,49 @@ def test_pack_unpack_phase8_rows(gpu, remote):
         check_unpacked(c, c["dst"])
 
 
-def test_goldens_with_torch_runtime_only(gpu):
+@pytest.mark.parametrize("launch_check", [False, True])
+def test_goldens_with_torch_runtime_only(gpu, launch_check):
     """The 153 MPICH goldens through TEMPI in a process whose ONLY HIP
     runtime is torch's (torch imported before libtempi is loaded: the
     configuration bench.py and smoke() run in; this pytest process holds two,
     DESIGN §2.2): packed bytes, positions and unpacked buffers bit-exact, the
-    strided cases on the GPU path (tests/mpi_progs/torch_runtime_parity.py)"""
+    strided cases on the GPU path (tests/mpi_progs/torch_runtime_parity.py).
+    launch_check: the same under TEMPI_LAUNCH_CHECK=1 (every launch
+    synchronised and checked): the same bytes, no report."""
     import subprocess
     import sys
 
     root = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+    env = dict(os.environ, **({"TEMPI_LAUNCH_CHECK": "1"} if launch_check else {}))
     r = subprocess.run([sys.executable, os.path.join(root, "tests", "mpi_progs", "torch_runtime_parity.py")],
-                       cwd=root, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=300)
+                       cwd=root, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=300, env=env)
     assert r.returncode == 0 and f"RESULT ok {len(CASES)} cases" in r.stdout, r.stdout[-3000:]
+    assert "TEMPI_LAUNCH_CHECK" not in r.stdout and "HIP runtimes in this process" not in r.stdout
+
+
+_TWO_RUNTIMES = """
+import sys
+sys.path.insert(0, {root!r})
+import tempi_amd
+mpi = tempi_amd.get_mpi()  # libtempi (and ROCm's runtime) first
+import torch  # then torch, which loads its own
+torch.cuda.init()
+mpi.Init()
+mpi.Finalize()
+print("RESULT ok")
+"""
+
+
+def test_two_runtimes_reported_at_init(gpu):
+    """libtempi loaded before torch leaves two HIP runtimes in
+    the process, and MPI_Init says so once, naming both (the torch-first
+    order above reports nothing)"""
+    import subprocess
+    import sys
+
+    root = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+    r = subprocess.run([sys.executable, "-c", _TWO_RUNTIMES.format(root=root)], cwd=root, stdout=subprocess.PIPE,
+                       stderr=subprocess.STDOUT, text=True, timeout=300)
+    assert r.returncode == 0 and "RESULT ok" in r.stdout, r.stdout[-3000:]
+    warn = [l for l in r.stdout.splitlines() if "HIP runtimes in this process" in l]
+    assert len(warn) == 1 and "torch" in warn[0] and warn[0].count("libamdhip64") == 2, r.stdout[-3000:]
