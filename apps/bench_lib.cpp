@@ -702,6 +702,17 @@ EXPORT int tempi_bench_sync_phases(int reps, char *json, int jsonCap) {
       total.push_back(t5 - t3);
     }
   }
+  // the resident packer called at the C ABI (no interposer around it)
+  std::vector<double> res;
+  int resServed = 1;
+  for (int r = 0; r < reps + 20; ++r) {
+    int served = 0;
+    double t0 = now_us();
+    errs += tempi_hip_pack_resident(dst, src, &d, s, &served) != 0;
+    double t1 = now_us();
+    resServed &= served;
+    if (r >= 20) res.push_back(t1 - t0);
+  }
   for (int r = 0; r < reps + 20; ++r) {
     HIPCHECK(hipStreamSynchronize(s));
     double t0 = now_us();
@@ -750,10 +761,12 @@ EXPORT int tempi_bench_sync_phases(int reps, char *json, int jsonCap) {
                 "{\"workload\": \"config 1: MPI_Pack of vector(1024, 512, 1024), 512 KiB, medians of %d calls in C, each phase in a loop of its own\", "
                 "\"mpi_pack_device_us\": %.2f, \"mpich_host_us\": %.2f, \"c_speedup\": %.3f, "
                 "\"phases_us\": {\"pointer_info_x2\": %.2f, \"launch\": %.2f, \"ticket_wait\": %.2f, "
-                "\"launch_plus_wait\": %.2f, \"kernel_back_to_back\": %.2f, \"bare_launch\": %.2f}, "
+                "\"launch_plus_wait\": %.2f, \"kernel_back_to_back\": %.2f, \"bare_launch\": %.2f, "
+                "\"resident_call\": %.2f, \"resident_served\": %s}, "
                 "\"interleaved_with_mpich\": {\"mpi_pack_device_us\": %.2f, \"launch\": %.2f}, \"errors\": %d}",
                 reps, median(api), median(lib), median(api) > 0 ? median(lib) / median(api) : 0.0, median(ptr),
-                median(launch), median(wait), median(total), double(ms) * 1e3 / nk, median(bare), median(apiMixed),
+                median(launch), median(wait), median(total), double(ms) * 1e3 / nk, median(bare), median(res),
+                resServed ? "true" : "false", median(apiMixed),
                 median(launchMixed), errs);
   return errs ? 1 : 0;
 }

@@ -116,6 +116,25 @@ int tempi_hip_unpack_batch_ticket(const tempi_hip_batch_item *items, int n, void
                                   uint32_t *ticket);
 int tempi_hip_copy_batch_ticket(const tempi_hip_copy_item *items, int n, void *stream, const uint32_t **flag,
                                 uint32_t *ticket);
+/* synchronous forms served by the RESIDENT packer (pack_kernels.hip,
+   "resident packer"): a kernel kept running between the calls of a burst
+   takes the request from pinned host memory -- no launch per call. On return
+   0 with *served = 1 the work is complete and visible device-wide; *served = 0
+   means it was not taken (narrow words, > 3 dims, larger than
+   TEMPI_RESIDENT_MAX_BYTES, TEMPI_RESIDENT=0) and the caller launches on
+   `stream` as before. Replaces the launch + cudaStreamSynchronize of
+   /root/reference/src/internal/packer_2d.cu:101-118 for small objects. */
+int tempi_hip_pack_resident(void *packed, const void *first, const tempi_hip_desc *d, void *stream, int *served);
+int tempi_hip_unpack_resident(void *first, const void *packed, const tempi_hip_desc *d, void *stream, int *served);
+/* requests served, server launches, requests posted again after crossing a
+   server's idle exit */
+void tempi_hip_resident_stats(uint64_t *served, uint64_t *launches, uint64_t *reposts);
+/* an EXIT request to every running server; returns once they have left
+   (MPI_Finalize) */
+void tempi_hip_resident_stop(void);
+/* turn the resident packer on (1) or off (0) for later calls; returns the
+   previous setting (initially TEMPI_RESIDENT, default on) */
+int tempi_hip_resident_enable(int on);
 
 /* number of packed bytes a descriptor describes */
 int64_t tempi_hip_desc_bytes(const tempi_hip_desc *d);

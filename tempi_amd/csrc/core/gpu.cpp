@@ -83,6 +83,7 @@ void init() {
 }
 
 void finalize() {
+  tempi_hip_resident_stop(); // (before the streams go: nothing may outlive MPI_Finalize)
   std::lock_guard<std::mutex> g(mtx);
   for (void *s : streams)
     if (s) tempi_hip_stream_destroy(s);

@@ -111,6 +111,19 @@ int Packer::launch(bool pack, char *packed, char *origin, int64_t count, void *s
       d.counts[k] = tmp.dims[k].count;
       d.strides[k] = tmp.dims[k].stride;
     }
+    // a small object: the resident packer, if it takes it, needs no launch (and
+    // no wait: the call returns once the work is done). Not while kernels are
+    // timed by events on the stream (kernelProfiling): it launches nothing there
+    if (!kernelProfiling) {
+      int served = 0;
+      const int e = pack ? tempi_hip_pack_resident(packed, first, &d, stream, &served)
+                         : tempi_hip_unpack_resident(first, packed, &d, stream, &served);
+      if (e) return e;
+      if (served) {
+        done->flag = nullptr;
+        return 0;
+      }
+    }
     counters.launches++;
     return pack ? tempi_hip_pack_ticket(packed, first, &d, stream, &done->flag, &done->ticket)
                 : tempi_hip_unpack_ticket(first, packed, &d, stream, &done->flag, &done->ticket);

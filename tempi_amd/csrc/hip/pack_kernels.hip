@@ -36,9 +36,12 @@
 #include "tempi_hip.h"
 #include "ticket.hpp"
 
+#include <algorithm>
+#include <atomic>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -1959,6 +1962,417 @@ template <typename F> int batch_with_ticket(hipStream_t s, const uint32_t **flag
   return 0;
 }
 
+// ------------------------------------------------------------ resident packer
+//
+// A synchronous MPI_Pack / MPI_Unpack of a small object (config 1: 512 KiB)
+// was ~9 us, of which the kernel's gather is ~2: hipLaunchKernel 2.2-3.0 us,
+// dispatch 2.2-2.6 before a wave runs, one-way visibility of the completion
+// 1.2-1.35. The reference pays the same (a launch and a
+// cudaStreamSynchronize: /root/reference/src/internal/packer_2d.cu:101-118).
+// Here no launch is made per call: a kernel stays RESIDENT while calls keep
+// coming. The host writes the request into pinned host memory; the kernel's
+// leader wave polls it over the host link and hands it to the worker
+// workgroups through device memory; each worker invalidates its caches (an
+// acquire: the object may have been written by any other kernel, copy or the
+// host since it last looked) and runs the same gather / scatter body as the
+// launched kernels (pack_body / unpack_body, grid-stride over the workers);
+// the last worker to finish stores the completion to pinned host memory.
+// Measured on MI355X (tools/resident.hip, profiles/r06/resident_proto_s15.jsonl):
+// 5.1 us per config-1 call against 9.2 through a launch.
+//
+// Records are 64 tagged 8-byte granules {data dword, sequence number}: one
+// wave-wide load reads a whole record, and it is complete when every lane's
+// tag is the number expected -- no separate flag, no ordering between the
+// granule stores. Completion is the ticket fold (ticket.hpp): workers count
+// themselves on kShards shard counters, the last of a shard on the top
+// counter, the last of all stores the sequence number; the host keeps the
+// counts and puts each request's targets in its record.
+//
+// Lifetime: the server is launched by the first call that can use it (that
+// call pays about a launch, as before) on a stream of its own, and leaves after
+// TEMPI_RESIDENT_IDLE_US (default 1 000) without a request, after 2 s in any
+// case, or on an EXIT request (MPI_Finalize). Every wave has a bounded exit:
+// the leader hands the workers an EXIT record as it leaves, and workers give
+// up on their own 4 x idle + 1 ms after their last request. A leader leaving
+// stores the first sequence number it did not serve; a request that crossed
+// its exit is posted again to a new instance (stream order puts the new one
+// behind the old). The server runs only between calls of a burst: an
+// application's hipDeviceSynchronize may wait up to the idle time for it.
+//
+// Taken: single descriptors of <= 3 dims, words of 4-16 bytes (narrower words
+// keep their interleaved / dense kernels), at most TEMPI_RESIDENT_MAX_BYTES
+// (default 2 MiB), not under TEMPI_LAUNCH_CHECK. TEMPI_RESIDENT=0 (or
+// tempi_hip_resident_enable(0)) turns it off.
+namespace resident {
+using tempi_ticket::kCounterStride;
+using tempi_ticket::kShards;
+constexpr uint32_t kOpPack = 1, kOpUnpack = 2, kOpExit = 3;
+constexpr int kGranules = 64; // one per lane of a wave
+// data dwords of a record
+constexpr int kOp = 0;         // op | W << 8 | ND << 16 | kAgentAcquire
+constexpr uint32_t kAgentAcquire = 1u << 24; // (A/B: TEMPI_RESIDENT_ACQUIRE=agent)
+constexpr int kWorkers = 1;    // workers taking part (a multiple of kShards)
+constexpr int kArgs = 2;       // KArgs<ND> (8-byte aligned)
+constexpr int kLastWorker = 40; // the worker holding the object's last (partial) chunk
+constexpr int kReleaseAll = 41; // every worker stored through L2 (not write-through)
+constexpr int kTargets = 42;    // the shard counters' targets, then the top counter's
+static_assert(kArgs * 4 + sizeof(KArgs<3>) <= kLastWorker * 4, "record layout");
+static_assert(kTargets + kShards + 1 <= kGranules, "record layout");
+constexpr uint64_t kTicksPerUs = 100; // wall_clock64 (s_memrealtime): 100 MHz
+constexpr uint64_t kGrace = 1000 * kTicksPerUs;
+
+struct Mail {                 // pinned, coherent, mapped host memory
+  uint64_t req[kGranules];    // the request, tagged with its sequence number
+  uint32_t done;              // the last request served
+  uint32_t pad0[31];
+  uint32_t exitw;             // the first request an exiting server left unserved
+  uint32_t pad1[31];
+};
+struct Dev {                  // device memory, zeroed once
+  uint64_t bcast[kGranules];  // the leader's hand-off to the workers
+  uint32_t counter[(kShards + 1) * kCounterStride];
+};
+
+template <bool PACK, int W, int ND>
+__device__ __forceinline__ void serve(const uint32_t *rec, uint32_t w, uint32_t nw) {
+  KArgs<ND> a;
+  __builtin_memcpy(&a, rec + kArgs, sizeof a);
+  if constexpr (PACK)
+    pack_body<W, ND, true>(a, w, nw);
+  else
+    unpack_body<W, ND, W == 16>(a, w, nw);
+}
+
+template <bool PACK, int W> __device__ __forceinline__ void serve_nd(uint32_t nd, const uint32_t *rec, uint32_t w,
+                                                                    uint32_t nw) {
+  switch (nd) {
+  case 0: return serve<PACK, W, 0>(rec, w, nw);
+  case 1: return serve<PACK, W, 1>(rec, w, nw);
+  case 2: return serve<PACK, W, 2>(rec, w, nw);
+  default: return serve<PACK, W, 3>(rec, w, nw);
+  }
+}
+
+template <bool PACK> __device__ __forceinline__ void serve_w(uint32_t op, const uint32_t *rec, uint32_t w,
+                                                            uint32_t nw) {
+  const uint32_t W = (op >> 8) & 31, nd = (op >> 16) & 7;
+  if (W == 16)
+    serve_nd<PACK, 16>(nd, rec, w, nw);
+  else if (W == 8)
+    serve_nd<PACK, 8>(nd, rec, w, nw);
+  else
+    serve_nd<PACK, 4>(nd, rec, w, nw);
+}
+
+// block 0: the leader (one wave); blocks 1 .. gridDim.x - 1: the workers
+__global__ __launch_bounds__(kBlock) void server_kernel(Mail *m, Dev *dv, uint32_t firstSeq, uint64_t idle,
+                                                        uint64_t cap) {
+  __shared__ __attribute__((aligned(16))) uint32_t rec[kGranules];
+  const uint64_t t0 = wall_clock64();
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t expect = firstSeq;
+  uint64_t last = t0;
+  if (blockIdx.x == 0) {
+    if (wave) return;
+    for (;;) {
+      const uint64_t g = __hip_atomic_load(&m->req[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (__ballot(uint32_t(g >> 32) == expect) == ~0ull) {
+        const uint32_t op = __shfl(uint32_t(g), 0);
+        __hip_atomic_store(&dv->bcast[lane], g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ++expect;
+        last = wall_clock64();
+        if ((op & 3) == kOpExit) break;
+        continue;
+      }
+      const uint64_t now = wall_clock64();
+      if (now - last > idle || now - t0 > cap) {
+        __hip_atomic_store(&dv->bcast[lane], (uint64_t(expect) << 32) | (lane == 0 ? kOpExit : 0u),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_store(&m->exitw, expect, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return;
+  }
+  const uint32_t w = blockIdx.x - 1;
+  for (;;) {
+    if (wave == 0) {
+      uint32_t d;
+      for (;;) {
+        const uint64_t g = __hip_atomic_load(&dv->bcast[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (__ballot(uint32_t(g >> 32) == expect) == ~0ull) {
+          d = uint32_t(g);
+          break;
+        }
+        const uint64_t now = wall_clock64();
+        if (now - last > 4 * idle + kGrace || now - t0 > cap + kGrace) { // (a lost leader)
+          d = lane == 0 ? kOpExit : 0u;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      rec[lane] = d;
+    }
+    __syncthreads();
+    const uint32_t op = rec[kOp], nw = rec[kWorkers], seq = expect;
+    if ((op & 3) == kOpExit) return;
+    ++expect;
+    if (w < nw) {
+      // acquire: nothing this CU cached before the request may be read
+      if (threadIdx.x == 0) {
+        if (op & kAgentAcquire)
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        else
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if ((op & 3) == kOpPack)
+        serve_w<true>(op, rec, w, nw);
+      else
+        serve_w<false>(op, rec, w, nw);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        // workers that stored through L2 (partial first / last chunks, scatters
+        // of narrower words) write it back first (as wg_signal)
+        if (rec[kReleaseAll] || w == 0 || w == rec[kLastWorker]) {
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        const uint32_t k = w % kShards;
+        const uint32_t old = __hip_atomic_fetch_add(dv->counter + k * kCounterStride, 1u, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_SYSTEM);
+        if (old + 1u == rec[kTargets + k]) {
+          const uint32_t top = __hip_atomic_fetch_add(dv->counter + kShards * kCounterStride, 1u, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_SYSTEM);
+          if (top + 1u == rec[kTargets + kShards])
+            __hip_atomic_store(&m->done, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+      }
+    }
+    last = wall_clock64();
+    __syncthreads(); // (every wave has read the record before wave 0 writes the next)
+  }
+}
+
+bool env_flag(const char *name, bool dflt) {
+  const char *e = std::getenv(name);
+  return e ? std::strtol(e, nullptr, 10) != 0 : dflt;
+}
+int64_t env_int(const char *name, int64_t dflt) {
+  const char *e = std::getenv(name);
+  return e ? int64_t(std::strtoll(e, nullptr, 10)) : dflt;
+}
+std::atomic<int> &switched_on() { // TEMPI_RESIDENT, then tempi_hip_resident_enable
+  static std::atomic<int> v{env_flag("TEMPI_RESIDENT", true) ? 1 : 0};
+  return v;
+}
+bool enabled() { return switched_on().load(std::memory_order_relaxed) != 0; }
+int64_t max_bytes() {
+  static const int64_t v = env_int("TEMPI_RESIDENT_MAX_BYTES", int64_t(2) << 20);
+  return v;
+}
+// workers of a server: a multiple of kShards (a request takes up to all of them)
+uint32_t workers() {
+  static const uint32_t v = [] {
+    int64_t n = env_int("TEMPI_RESIDENT_WORKERS", 128);
+    n = n < kShards ? kShards : (n > 1024 ? 1024 : n);
+    return uint32_t(n / kShards * kShards);
+  }();
+  return v;
+}
+uint64_t idle_ticks() {
+  static const uint64_t v = uint64_t(std::max<int64_t>(env_int("TEMPI_RESIDENT_IDLE_US", 1000), 1)) * kTicksPerUs;
+  return v;
+}
+constexpr uint64_t kCapTicks = uint64_t(2000000) * kTicksPerUs; // 2 s
+bool agent_acquire() {
+  static const bool v = [] {
+    const char *e = std::getenv("TEMPI_RESIDENT_ACQUIRE");
+    return e && std::strcmp(e, "agent") == 0;
+  }();
+  return v;
+}
+
+struct Server {
+  bool ready = false, broken = false, running = false;
+  hipStream_t stream = nullptr;
+  Mail *host = nullptr, *mapped = nullptr;
+  Dev *dev = nullptr;
+  uint32_t seq = 0;                   // the last request posted
+  uint32_t counted[kShards + 1] = {}; // the host's totals of the device counters
+};
+struct Stats {
+  uint64_t served = 0, launches = 0, reposts = 0;
+};
+std::mutex &mutex() {
+  static std::mutex m;
+  return m;
+}
+Stats &stats() {
+  static Stats s;
+  return s;
+}
+Server &server(int device) {
+  static Server s[64];
+  return s[device & 63];
+}
+
+bool ready(Server &sv) {
+  if (sv.ready || sv.broken) return sv.ready;
+  void *h = nullptr, *d = nullptr, *dv = nullptr;
+  hipError_t e = hipStreamCreateWithFlags(&sv.stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipHostMalloc(&h, sizeof(Mail), hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable);
+  if (e == hipSuccess) e = hipHostGetDevicePointer(&d, h, 0);
+  if (e == hipSuccess) e = hipMalloc(&dv, sizeof(Dev));
+  if (e == hipSuccess) e = hipMemsetAsync(dv, 0, sizeof(Dev), sv.stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(sv.stream);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    sv.broken = true;
+    return false;
+  }
+  std::memset(h, 0, sizeof(Mail));
+  sv.host = static_cast<Mail *>(h);
+  sv.mapped = static_cast<Mail *>(d);
+  sv.dev = static_cast<Dev *>(dv);
+  sv.ready = true;
+  return true;
+}
+
+void post(Server &sv, uint32_t seq, const uint32_t *d) {
+  for (int i = 0; i < kGranules; ++i)
+    __atomic_store_n(&sv.host->req[i], (uint64_t(seq) << 32) | d[i], __ATOMIC_RELAXED);
+}
+
+// 0: served; 1: the server left without serving it; else a HIP error
+int wait(Server &sv, uint32_t seq) {
+  for (uint32_t spins = 1;; ++spins) {
+    if (__atomic_load_n(&sv.host->done, __ATOMIC_ACQUIRE) == seq) return 0;
+    if (__atomic_load_n(&sv.host->exitw, __ATOMIC_ACQUIRE) == seq) return 1;
+    if ((spins & 1023) == 0) { // ~20 us of pause loops: a faulted server ends the wait
+      const hipError_t e = hipStreamQuery(sv.stream);
+      if (e == hipSuccess) { // ended: its last stores are visible now
+        if (__atomic_load_n(&sv.host->done, __ATOMIC_ACQUIRE) == seq) return 0;
+        if (__atomic_load_n(&sv.host->exitw, __ATOMIC_ACQUIRE) == seq) return 1;
+        return int(hipErrorUnknown);
+      }
+      if (e != hipErrorNotReady) return int(e);
+      (void)hipGetLastError();
+    }
+    __builtin_ia32_pause();
+  }
+}
+
+template <int W, int ND>
+void make_record(bool pack, char *packed, char *first, const Norm &n, uint32_t *d) {
+  KArgs<ND> a;
+  uint32_t blocks;
+  make_args<W, ND>(packed, first, n, &a, &blocks);
+  if (pack || (W == 16 && scatter_write_through(n))) a.flags |= kWriteThrough;
+  constexpr uint32_t tile = uint32_t(kBlock) * Unroll<W>::U; // chunks per worker step
+  const uint32_t tiles = (a.nchunks + tile - 1) / tile;
+  uint32_t nw = std::min<uint32_t>(workers(), (tiles + kShards - 1) / kShards * kShards);
+  d[kOp] = (pack ? kOpPack : kOpUnpack) | uint32_t(W) << 8 | uint32_t(ND) << 16 | (agent_acquire() ? kAgentAcquire : 0u);
+  d[kWorkers] = nw;
+  std::memcpy(d + kArgs, &a, sizeof a);
+  d[kLastWorker] = (tiles - 1) % nw;
+  d[kReleaseAll] = (a.flags & kWriteThrough) ? 0u : 1u;
+}
+
+template <int W>
+void make_record_w(bool pack, char *packed, char *first, const Norm &n, uint32_t *d) {
+  switch (n.nd) {
+  case 0: return make_record<W, 0>(pack, packed, first, n, d);
+  case 1: return make_record<W, 1>(pack, packed, first, n, d);
+  case 2: return make_record<W, 2>(pack, packed, first, n, d);
+  default: return make_record<W, 3>(pack, packed, first, n, d);
+  }
+}
+
+// serve one synchronous pack / unpack; *served = false: not taken (the caller
+// launches as before)
+int run(bool pack, char *packed, char *first, const Norm &n, hipStream_t s, bool *served) {
+  *served = false;
+  if (!enabled() || launch_check() || n.nd > 3) return 0;
+  const int64_t bytes = norm_bytes(n);
+  if (bytes == 0 || bytes > max_bytes()) return 0;
+  for (int k = 0; k < n.nd; ++k)
+    if (n.cnt[k] >= (int64_t(1) << 32)) return 0;
+  const int w = word_width(reinterpret_cast<uintptr_t>(packed), reinterpret_cast<uintptr_t>(first), n);
+  if (w < 4) return 0;
+  // (no order with TEMPI's earlier work on `s` is needed: a synchronous call
+  // waited for its own, and an MPI_Isend / MPI_Irecv still in flight may not
+  // share a buffer this call writes -- MPI's rule for the application --
+  // while readers of one buffer do not conflict. HIP reports a stream busy for
+  // ~5 us after a launched call's ticket is seen, so waiting for it here would
+  // hand every call of a burst to a launch.)
+  (void)s;
+  int device = 0;
+  if (hipGetDevice(&device) != hipSuccess) return 0;
+  std::lock_guard<std::mutex> lock(mutex());
+  Server &sv = server(device);
+  if (!ready(sv)) return 0;
+  uint32_t d[kGranules] = {};
+  if (w == 16)
+    make_record_w<16>(pack, packed, first, n, d);
+  else if (w == 8)
+    make_record_w<8>(pack, packed, first, n, d);
+  else
+    make_record_w<4>(pack, packed, first, n, d);
+  const uint32_t perShard = d[kWorkers] / kShards;
+  for (int k = 0; k < kShards; ++k) d[kTargets + k] = sv.counted[k] + perShard;
+  d[kTargets + kShards] = sv.counted[kShards] + kShards;
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    if (!sv.running) {
+      hipLaunchKernelGGL(server_kernel, dim3(1 + workers()), dim3(kBlock), 0, sv.stream, sv.mapped, sv.dev,
+                         sv.seq + 1, idle_ticks(), kCapTicks);
+      const hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return int(e);
+      sv.running = true;
+      stats().launches++;
+    }
+    const uint32_t seq = ++sv.seq;
+    post(sv, seq, d);
+    const int r = wait(sv, seq);
+    if (r == 0) {
+      for (int k = 0; k <= kShards; ++k) sv.counted[k] = d[kTargets + k];
+      stats().served++;
+      *served = true;
+      return 0;
+    }
+    sv.running = false;
+    if (r != 1) { // a fault: the counters are unknown from here on
+      sv.broken = true;
+      return r;
+    }
+    stats().reposts++; // it crossed the server's exit: post it to a new one
+  }
+  return 0;
+}
+
+// MPI_Finalize: an EXIT request to every running server, then its stream drains
+void stop_all() {
+  std::lock_guard<std::mutex> lock(mutex());
+  for (int dv = 0; dv < 64; ++dv) {
+    Server &sv = server(dv);
+    if (!sv.ready || !sv.running) continue;
+    uint32_t d[kGranules] = {};
+    d[kOp] = kOpExit;
+    post(sv, ++sv.seq, d);
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    (void)hipSetDevice(dv);
+    (void)hipStreamSynchronize(sv.stream);
+    (void)hipSetDevice(cur);
+    (void)hipGetLastError();
+    sv.running = false;
+  }
+}
+} // namespace resident
+
 } // namespace
 
 extern "C" {
@@ -1992,6 +2406,39 @@ int tempi_hip_copy_batch_ticket(const tempi_hip_copy_item *items, int n, void *s
   hipStream_t s = static_cast<hipStream_t>(stream);
   return batch_with_ticket(s, flag, ticket, [&](tempi_ticket::Fold *f) { return copy_batch(items, n, stream, f); });
 }
+
+int tempi_hip_pack_resident(void *packed, const void *first, const tempi_hip_desc *d, void *stream, int *served) {
+  *served = 0;
+  Norm n;
+  if (!normalise(d, &n)) return int(hipErrorInvalidValue);
+  bool s = false;
+  const int e = resident::run(true, static_cast<char *>(packed), const_cast<char *>(static_cast<const char *>(first)),
+                              n, static_cast<hipStream_t>(stream), &s);
+  *served = s ? 1 : 0;
+  return e;
+}
+
+int tempi_hip_unpack_resident(void *first, const void *packed, const tempi_hip_desc *d, void *stream, int *served) {
+  *served = 0;
+  Norm n;
+  if (!normalise(d, &n)) return int(hipErrorInvalidValue);
+  bool s = false;
+  const int e = resident::run(false, const_cast<char *>(static_cast<const char *>(packed)), static_cast<char *>(first),
+                              n, static_cast<hipStream_t>(stream), &s);
+  *served = s ? 1 : 0;
+  return e;
+}
+
+void tempi_hip_resident_stats(uint64_t *served, uint64_t *launches, uint64_t *reposts) {
+  std::lock_guard<std::mutex> lock(resident::mutex());
+  if (served) *served = resident::stats().served;
+  if (launches) *launches = resident::stats().launches;
+  if (reposts) *reposts = resident::stats().reposts;
+}
+
+void tempi_hip_resident_stop(void) { resident::stop_all(); }
+
+int tempi_hip_resident_enable(int on) { return resident::switched_on().exchange(on ? 1 : 0); }
 
 int tempi_hip_pack_batch(const tempi_hip_batch_item *items, int n, void *stream) {
   return run_batch(true, items, n, static_cast<hipStream_t>(stream));

@@ -654,6 +654,10 @@ def test_synchronous_ticket_visible_device_wide(mpi, gpu, rows, block, stride, f
     the result: the bytes must already be visible device-wide. 60 rounds
     with fresh contents each, so a stale line would show."""
     torch = _torch()
+    import tempi_amd
+
+    H = ctypes.CDLL(tempi_amd.LIBTEMPI_HIP)
+    prev = H.tempi_hip_resident_enable(0)  # (launched calls only: the resident packer has its own test file)
     t = mpi.Type_commit(mpi.Type_vector(rows, block, stride, mpi.BYTE))
     ext = (rows - 1) * stride + block
     try:
@@ -677,6 +681,7 @@ def test_synchronous_ticket_visible_device_wide(mpi, gpu, rows, block, stride, f
         assert c1["ticket_waits"] - c0["ticket_waits"] == 120 and c1["sync_waits"] == c0["sync_waits"]
         assert f1[0] - f0[0] == sum(folds) and f1[1] - f0[1] == 120 - sum(folds)
     finally:
+        H.tempi_hip_resident_enable(prev)
         mpi.Type_free(t)
 
 

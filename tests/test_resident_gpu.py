@@ -1,0 +1,207 @@
+"""The resident packer (tempi_amd/csrc/hip/pack_kernels.hip, "resident
+packer"): synchronous MPI_Pack / MPI_Unpack of small objects served by a
+kernel that stays running between calls instead of a launch per call.
+
+Parity is the same bar as every other GPU path: bit-exact against the
+MPICH 3.3.2 goldens and against torch gathers of fresh random data, with
+the result visible on another stream (torch's) the moment the call returns.
+Coherence is what a resident kernel can get wrong (it does not get the cache
+invalidate a launch does), so every round rewrites the source -- by a
+kernel, by a host-to-device copy -- and re-checks.
+"""
+import ctypes
+import os
+import subprocess
+import sys
+
+import pytest
+
+from tests import golden_data as G
+from tests import typezoo
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+
+
+def _hip():
+    import tempi_amd
+
+    return ctypes.CDLL(tempi_amd.LIBTEMPI_HIP)
+
+
+def resident_stats():
+    H = _hip()
+    a, b, c = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+    H.tempi_hip_resident_stats(ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
+    return a.value, b.value, c.value
+
+
+class resident_switch:
+    """with resident_switch(on): ... -- the packer on / off, restored after"""
+
+    def __init__(self, on):
+        self.on = on
+
+    def __enter__(self):
+        self.prev = _hip().tempi_hip_resident_enable(1 if self.on else 0)
+        return self
+
+    def __exit__(self, *a):
+        _hip().tempi_hip_resident_enable(self.prev)
+
+
+# rows, block, stride, packed offset, served: 16-byte words (config 1 and
+# smaller), 8-byte words (halo x-face rows), 4-byte words, a packed side 4
+# bytes into its buffer (partial first / last chunks), 1-byte words (not
+# taken: their interleaved / dense kernels stay), 8 MiB (not taken: above
+# TEMPI_RESIDENT_MAX_BYTES)
+SHAPES = [(1024, 512, 1024, 0, True), (300, 512, 1024, 0, True), (2, 512, 1024, 0, True),
+          (4096, 24, 4608, 0, True), (100, 500, 1000, 0, True), (257, 48, 80, 4, True),
+          (4095, 16, 4112, 0, True), (20000, 3, 7, 0, False), (16384, 512, 1024, 0, False)]
+
+
+@pytest.mark.parametrize("rows,block,stride,off,served", SHAPES,
+                         ids=[f"{r}x{b}s{s}o{o}" for r, b, s, o, _ in SHAPES])
+def test_resident_visible_device_wide(mpi, gpu, rows, block, stride, off, served):
+    """60 rounds of fresh random contents (written by torch's kernels on
+    torch's stream, then synchronised): MPI_Pack into a device buffer, the
+    packed bytes compared on torch's stream right after the call returns;
+    MPI_Unpack into a buffer filled with a marker, the strided bytes and the
+    gaps compared. The objects the packer takes are served by it (no launch
+    counted), the others launch as before."""
+    import torch
+
+    t = mpi.Type_commit(mpi.Type_vector(rows, block, stride, mpi.BYTE))
+    ext = (rows - 1) * stride + block
+    try:
+        src = torch.empty(ext, dtype=torch.uint8, device=gpu)
+        packed = torch.zeros(rows * block + off, dtype=torch.uint8, device=gpu)
+        back = torch.empty(ext, dtype=torch.uint8, device=gpu)
+        idx = (torch.arange(rows, device=gpu).unsqueeze(1) * stride + torch.arange(block, device=gpu)).reshape(-1)
+        gaps = torch.ones(ext, dtype=torch.bool, device=gpu)
+        gaps[idx] = False
+        g = torch.Generator(device=gpu).manual_seed(rows * 7 + block)
+        s0, c0 = resident_stats(), mpi.counters()
+        for r in range(60):
+            src.random_(0, 256, generator=g)
+            exp = src[idx]
+            torch.cuda.synchronize()
+            mpi.Pack(src.data_ptr(), 1, t, packed.data_ptr() + off, rows * block, 0)
+            assert torch.equal(packed[off:], exp), f"round {r}: packed bytes wrong or not visible"
+            back.fill_(r & 0xFF)
+            torch.cuda.synchronize()
+            mpi.Unpack(packed.data_ptr() + off, rows * block, 0, back.data_ptr(), 1, t)
+            assert torch.equal(back[idx], exp), f"round {r}: unpacked bytes wrong or not visible"
+            assert bool((back[gaps] == (r & 0xFF)).all()), f"round {r}: a gap byte was written"
+        s1, c1 = resident_stats(), mpi.counters()
+        assert c1["packs"] - c0["packs"] == 60 and c1["unpacks"] - c0["unpacks"] == 60
+        if served:
+            assert s1[0] - s0[0] == 120
+            assert c1["launches"] == c0["launches"]
+        else:
+            assert s1[0] == s0[0]
+            assert c1["launches"] - c0["launches"] >= 120
+    finally:
+        mpi.Type_free(t)
+
+
+def test_resident_source_from_host_copy(mpi, gpu):
+    """The source rewritten by host-to-device copies (DMA, not a kernel)
+    between calls: the packer must not serve a line it cached from the
+    previous contents. 16-byte and 4-byte words, 80 rounds."""
+    import numpy as np
+    import torch
+
+    rng = np.random.default_rng(5)
+    for rows, block, stride in ((1024, 512, 1024), (100, 500, 1000)):
+        t = mpi.Type_commit(mpi.Type_vector(rows, block, stride, mpi.BYTE))
+        ext = (rows - 1) * stride + block
+        try:
+            src = torch.zeros(ext, dtype=torch.uint8, device=gpu)
+            packed = torch.zeros(rows * block, dtype=torch.uint8, device=gpu)
+            idx = (np.arange(rows)[:, None] * stride + np.arange(block)).reshape(-1)
+            s0 = resident_stats()
+            for r in range(80):
+                host = rng.integers(0, 256, ext, dtype=np.uint8)
+                src.copy_(torch.from_numpy(host))
+                torch.cuda.synchronize()
+                mpi.Pack(src.data_ptr(), 1, t, packed.data_ptr(), packed.numel(), 0)
+                exp = host[idx]
+                assert np.array_equal(packed.cpu().numpy(), exp), f"round {r}: stale or wrong bytes"
+            assert resident_stats()[0] - s0[0] == 80
+        finally:
+            mpi.Type_free(t)
+
+
+def test_resident_off_launches(mpi, gpu):
+    """tempi_hip_resident_enable(0): the same calls launch (and wait by ticket)
+    as before; on again: served again."""
+    import torch
+
+    t = mpi.Type_commit(mpi.Type_vector(1024, 512, 1024, mpi.BYTE))
+    try:
+        src = (torch.arange(1023 * 1024 + 512, device=gpu) & 0xFF).to(torch.uint8)
+        packed = torch.zeros(512 * 1024, dtype=torch.uint8, device=gpu)
+        torch.cuda.synchronize()
+        with resident_switch(False):
+            s0, c0 = resident_stats(), mpi.counters()
+            for _ in range(10):
+                mpi.Pack(src.data_ptr(), 1, t, packed.data_ptr(), packed.numel(), 0)
+            s1, c1 = resident_stats(), mpi.counters()
+            assert s1[0] == s0[0] and c1["launches"] - c0["launches"] == 10
+            assert c1["ticket_waits"] - c0["ticket_waits"] == 10
+        with resident_switch(True):
+            for _ in range(10):
+                mpi.Pack(src.data_ptr(), 1, t, packed.data_ptr(), packed.numel(), 0)
+            assert resident_stats()[0] - s1[0] == 10
+        idx = (torch.arange(1024, device=gpu).unsqueeze(1) * 1024 + torch.arange(512, device=gpu)).reshape(-1)
+        assert torch.equal(packed, src[idx])
+    finally:
+        mpi.Type_free(t)
+
+
+def test_resident_goldens(mpi, gpu):
+    """Every MPICH 3.3.2 golden case through MPI_Pack / MPI_Unpack on device
+    buffers with the packer on: bit-exact packed bytes, positions and
+    unpacked buffers; the cases it can take (4-16-byte words, <= 3 dims) are
+    served by it."""
+    import torch
+
+    served = 0
+    with resident_switch(True):
+        for c in G.cases():
+            t, temps, basic = typezoo.build(mpi, c["recipe"])
+            try:
+                src = (torch.arange(c["buflen"], dtype=torch.int64, device=gpu) & 0xFF).to(torch.uint8)
+                out = torch.zeros(max(c["pack_size"], 1), dtype=torch.uint8, device=gpu)
+                torch.cuda.synchronize()
+                s0 = resident_stats()
+                pos = mpi.Pack(src.data_ptr() + c["origin"], c["count"], t, out.data_ptr(), c["pack_size"], 0)
+                assert pos == c["position"], c["name"]
+                G.check_packed(c, out[:pos].cpu().numpy())
+                dst = torch.zeros(c["buflen"], dtype=torch.uint8, device=gpu)
+                torch.cuda.synchronize()
+                upos = mpi.Unpack(out.data_ptr(), c["pack_size"], 0, dst.data_ptr() + c["origin"], c["count"], t)
+                assert upos == c["unpack_position"], c["name"]
+                G.check_unpacked(c, dst.cpu().numpy())
+                served += resident_stats()[0] - s0[0]
+            finally:
+                typezoo.free(mpi, t, temps, basic)
+    assert served > 0
+
+
+@pytest.mark.parametrize("idle_us", [5, 40])
+def test_resident_exit_race(gpu, idle_us):
+    """Requests crossing the server's idle exit (tests/mpi_progs/
+    resident_race.py): with the idle time a few microseconds and random gaps
+    of up to three idle times between calls, requests are served, reposted to
+    a new instance or taken by a fresh launch -- every byte still right, and
+    more than one server instance launched."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "mpi_progs", "resident_race.py"), str(idle_us),
+                        "400"], cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=240)
+    line = [l for l in r.stdout.splitlines() if l.startswith("RESULT")]
+    assert r.returncode == 0 and line, r.stdout[-3000:]
+    f = dict(kv.split("=") for kv in line[0].split()[1:])
+    assert int(f["errors"]) == 0, r.stdout[-3000:]
+    assert int(f["served"]) == 800 and int(f["launches"]) > 1, line[0]
