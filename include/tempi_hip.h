@@ -135,6 +135,10 @@ void tempi_hip_resident_stop(void);
 /* turn the resident packer on (1) or off (0) for later calls; returns the
    previous setting (initially TEMPI_RESIDENT, default on) */
 int tempi_hip_resident_enable(int on);
+/* diagnostic (TEMPI_RESIDENT_STAMPS=1): the GPU clock (wall_clock64, 100 MHz)
+   at five points of the last request -- the leader saw it; worker 0 saw the
+   hand-off, finished its acquire, finished its share; the completion stored */
+int tempi_hip_resident_stamps(uint64_t *out);
 
 /* number of packed bytes a descriptor describes */
 int64_t tempi_hip_desc_bytes(const tempi_hip_desc *d);

@@ -2011,14 +2011,29 @@ constexpr int kGranules = 64; // one per lane of a wave
 // data dwords of a record
 constexpr int kOp = 0;         // op | W << 8 | ND << 16 | kAgentAcquire
 constexpr uint32_t kAgentAcquire = 1u << 24; // (A/B: TEMPI_RESIDENT_ACQUIRE=agent)
+constexpr uint32_t kStamp = 1u << 25;        // (diagnostic: TEMPI_RESIDENT_STAMPS=1, Dev::stamp)
 constexpr int kWorkers = 1;    // workers taking part (a multiple of kShards)
 constexpr int kArgs = 2;       // KArgs<ND> (8-byte aligned)
-constexpr int kLastWorker = 40; // the worker holding the object's last (partial) chunk
-constexpr int kReleaseAll = 41; // every worker stored through L2 (not write-through)
-constexpr int kTargets = 42;    // the shard counters' targets, then the top counter's
+constexpr int kLastWorker = 40;  // the worker holding the object's last chunk when it is partial (else ~0)
+constexpr int kReleaseAll = 41;  // every worker stored through L2 (not write-through)
+constexpr int kReleaseFirst = 42; // the first chunk is partial (worker 0 holds it)
+constexpr int kTargets = 43;     // the shard counters' targets, then the top counter's
 static_assert(kArgs * 4 + sizeof(KArgs<3>) <= kLastWorker * 4, "record layout");
 static_assert(kTargets + kShards + 1 <= kGranules, "record layout");
 constexpr uint64_t kTicksPerUs = 100; // wall_clock64 (s_memrealtime): 100 MHz
+// chunks a lane has in flight per pass (A/B, profiles/r06/resident_u_ab_s19.jsonl:
+// 1, 2 and 4 within noise of each other at config 1)
+#ifndef TEMPI_RESIDENT_U
+#define TEMPI_RESIDENT_U 1
+#endif
+constexpr int kResidentU = TEMPI_RESIDENT_U;
+// one completion counter for all workers (a request has at most a few
+// hundred) instead of the launched kernels' sharded fold: one atomic on the
+// path instead of two, no slower in the A/B
+#ifndef TEMPI_RESIDENT_FLAT
+#define TEMPI_RESIDENT_FLAT 1
+#endif
+constexpr bool kResidentFlat = TEMPI_RESIDENT_FLAT != 0;
 constexpr uint64_t kGrace = 1000 * kTicksPerUs;
 
 struct Mail {                 // pinned, coherent, mapped host memory
@@ -2031,6 +2046,10 @@ struct Mail {                 // pinned, coherent, mapped host memory
 struct Dev {                  // device memory, zeroed once
   uint64_t bcast[kGranules];  // the leader's hand-off to the workers
   uint32_t counter[(kShards + 1) * kCounterStride];
+  // wall_clock64 of the last stamped request: the leader saw it; worker 0 saw
+  // the hand-off, finished its acquire, finished its body; the completing
+  // worker stored the completion
+  uint64_t stamp[8];
 };
 
 template <bool PACK, int W, int ND>
@@ -2038,9 +2057,9 @@ __device__ __forceinline__ void serve(const uint32_t *rec, uint32_t w, uint32_t 
   KArgs<ND> a;
   __builtin_memcpy(&a, rec + kArgs, sizeof a);
   if constexpr (PACK)
-    pack_body<W, ND, true>(a, w, nw);
+    pack_body<W, ND, true, kResidentU>(a, w, nw);
   else
-    unpack_body<W, ND, W == 16>(a, w, nw);
+    unpack_body<W, ND, W == 16, kResidentU>(a, w, nw);
 }
 
 template <bool PACK, int W> __device__ __forceinline__ void serve_nd(uint32_t nd, const uint32_t *rec, uint32_t w,
@@ -2074,16 +2093,27 @@ __global__ __launch_bounds__(kBlock) void server_kernel(Mail *m, Dev *dv, uint32
   uint64_t last = t0;
   if (blockIdx.x == 0) {
     if (wave) return;
+    // two polls of the host link in flight, so a request is seen about half
+    // a round trip sooner; a poll older than the request it overlapped holds
+    // an old tag and is passed over
+    bool leave = false;
+    auto take = [&](uint64_t g) {
+      if (__ballot(uint32_t(g >> 32) == expect) != ~0ull) return;
+      const uint32_t op = __shfl(uint32_t(g), 0);
+      if ((op & kStamp) && lane == 0) dv->stamp[0] = wall_clock64();
+      __hip_atomic_store(&dv->bcast[lane], g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      ++expect;
+      last = wall_clock64();
+      leave = (op & 3) == kOpExit;
+    };
+    uint64_t ga = __hip_atomic_load(&m->req[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     for (;;) {
-      const uint64_t g = __hip_atomic_load(&m->req[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      if (__ballot(uint32_t(g >> 32) == expect) == ~0ull) {
-        const uint32_t op = __shfl(uint32_t(g), 0);
-        __hip_atomic_store(&dv->bcast[lane], g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ++expect;
-        last = wall_clock64();
-        if ((op & 3) == kOpExit) break;
-        continue;
-      }
+      const uint64_t gb = __hip_atomic_load(&m->req[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      take(ga);
+      if (leave) break;
+      ga = __hip_atomic_load(&m->req[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      take(gb);
+      if (leave) break;
       const uint64_t now = wall_clock64();
       if (now - last > idle || now - t0 > cap) {
         __hip_atomic_store(&dv->bcast[lane], (uint64_t(expect) << 32) | (lane == 0 ? kOpExit : 0u),
@@ -2119,6 +2149,8 @@ __global__ __launch_bounds__(kBlock) void server_kernel(Mail *m, Dev *dv, uint32
     if ((op & 3) == kOpExit) return;
     ++expect;
     if (w < nw) {
+      const bool stamp = (op & kStamp) && w == 0 && threadIdx.x == 0;
+      if (stamp) dv->stamp[1] = wall_clock64();
       // acquire: nothing this CU cached before the request may be read
       if (threadIdx.x == 0) {
         if (op & kAgentAcquire)
@@ -2128,27 +2160,34 @@ __global__ __launch_bounds__(kBlock) void server_kernel(Mail *m, Dev *dv, uint32
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
+      if (stamp) dv->stamp[2] = wall_clock64();
       if ((op & 3) == kOpPack)
         serve_w<true>(op, rec, w, nw);
       else
         serve_w<false>(op, rec, w, nw);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
+      if (stamp) dv->stamp[3] = wall_clock64();
       if (threadIdx.x == 0) {
         // workers that stored through L2 (partial first / last chunks, scatters
-        // of narrower words) write it back first (as wg_signal)
-        if (rec[kReleaseAll] || w == 0 || w == rec[kLastWorker]) {
+        // of narrower words) write it back first (as wg_signal; an L2
+        // write-back costs ~1.5 us on the call's path, so only those)
+        if (rec[kReleaseAll] || (w == 0 && rec[kReleaseFirst]) || w == rec[kLastWorker]) {
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
-        const uint32_t k = w % kShards;
+        const uint32_t k = kResidentFlat ? 0u : w % kShards;
+        // (device counters only the GPU touches: agent scope)
         const uint32_t old = __hip_atomic_fetch_add(dv->counter + k * kCounterStride, 1u, __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_SYSTEM);
+                                                    __HIP_MEMORY_SCOPE_AGENT);
         if (old + 1u == rec[kTargets + k]) {
-          const uint32_t top = __hip_atomic_fetch_add(dv->counter + kShards * kCounterStride, 1u, __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_SYSTEM);
-          if (top + 1u == rec[kTargets + kShards])
+          const uint32_t top = kResidentFlat ? 0u
+                                             : __hip_atomic_fetch_add(dv->counter + kShards * kCounterStride, 1u,
+                                                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (kResidentFlat || top + 1u == rec[kTargets + kShards]) {
+            if (op & kStamp) dv->stamp[4] = wall_clock64();
             __hip_atomic_store(&m->done, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          }
         }
       }
     }
@@ -2177,7 +2216,7 @@ int64_t max_bytes() {
 // workers of a server: a multiple of kShards (a request takes up to all of them)
 uint32_t workers() {
   static const uint32_t v = [] {
-    int64_t n = env_int("TEMPI_RESIDENT_WORKERS", 128);
+    int64_t n = env_int("TEMPI_RESIDENT_WORKERS", 96);
     n = n < kShards ? kShards : (n > 1024 ? 1024 : n);
     return uint32_t(n / kShards * kShards);
   }();
@@ -2188,6 +2227,10 @@ uint64_t idle_ticks() {
   return v;
 }
 constexpr uint64_t kCapTicks = uint64_t(2000000) * kTicksPerUs; // 2 s
+bool stamps() {
+  static const bool v = env_flag("TEMPI_RESIDENT_STAMPS", false);
+  return v;
+}
 bool agent_acquire() {
   static const bool v = [] {
     const char *e = std::getenv("TEMPI_RESIDENT_ACQUIRE");
@@ -2272,14 +2315,18 @@ void make_record(bool pack, char *packed, char *first, const Norm &n, uint32_t *
   uint32_t blocks;
   make_args<W, ND>(packed, first, n, &a, &blocks);
   if (pack || (W == 16 && scatter_write_through(n))) a.flags |= kWriteThrough;
-  constexpr uint32_t tile = uint32_t(kBlock) * Unroll<W>::U; // chunks per worker step
+  constexpr uint32_t tile = uint32_t(kBlock) * kResidentU; // chunks per worker step
   const uint32_t tiles = (a.nchunks + tile - 1) / tile;
   uint32_t nw = std::min<uint32_t>(workers(), (tiles + kShards - 1) / kShards * kShards);
-  d[kOp] = (pack ? kOpPack : kOpUnpack) | uint32_t(W) << 8 | uint32_t(ND) << 16 | (agent_acquire() ? kAgentAcquire : 0u);
+  d[kOp] = (pack ? kOpPack : kOpUnpack) | uint32_t(W) << 8 | uint32_t(ND) << 16 | (agent_acquire() ? kAgentAcquire : 0u) |
+             (stamps() ? kStamp : 0u);
   d[kWorkers] = nw;
   std::memcpy(d + kArgs, &a, sizeof a);
-  d[kLastWorker] = (tiles - 1) % nw;
+  constexpr uint32_t CW = 16 / W;
+  const bool tailPartial = (uint64_t(a.head) + a.nwords) % CW != 0;
+  d[kLastWorker] = tailPartial ? (tiles - 1) % nw : ~0u;
   d[kReleaseAll] = (a.flags & kWriteThrough) ? 0u : 1u;
+  d[kReleaseFirst] = a.head != 0 ? 1u : 0u;
 }
 
 template <int W>
@@ -2322,9 +2369,10 @@ int run(bool pack, char *packed, char *first, const Norm &n, hipStream_t s, bool
     make_record_w<8>(pack, packed, first, n, d);
   else
     make_record_w<4>(pack, packed, first, n, d);
-  const uint32_t perShard = d[kWorkers] / kShards;
+  const uint32_t perShard = kResidentFlat ? 0u : d[kWorkers] / kShards;
   for (int k = 0; k < kShards; ++k) d[kTargets + k] = sv.counted[k] + perShard;
-  d[kTargets + kShards] = sv.counted[kShards] + kShards;
+  d[kTargets + kShards] = sv.counted[kShards] + (kResidentFlat ? 0u : uint32_t(kShards));
+  if (kResidentFlat) d[kTargets] = sv.counted[0] + d[kWorkers];
   for (int attempt = 0; attempt < 2; ++attempt) {
     if (!sv.running) {
       hipLaunchKernelGGL(server_kernel, dim3(1 + workers()), dim3(kBlock), 0, sv.stream, sv.mapped, sv.dev,
@@ -2439,6 +2487,16 @@ void tempi_hip_resident_stats(uint64_t *served, uint64_t *launches, uint64_t *re
 void tempi_hip_resident_stop(void) { resident::stop_all(); }
 
 int tempi_hip_resident_enable(int on) { return resident::switched_on().exchange(on ? 1 : 0); }
+
+int tempi_hip_resident_stamps(uint64_t *out) {
+  int device = 0;
+  hipError_t e = hipGetDevice(&device);
+  std::lock_guard<std::mutex> lock(resident::mutex());
+  resident::Server &sv = resident::server(device);
+  if (e == hipSuccess && !sv.ready) e = hipErrorNotReady;
+  if (e == hipSuccess) e = hipMemcpy(out, sv.dev->stamp, 5 * sizeof(uint64_t), hipMemcpyDeviceToHost);
+  return int(e);
+}
 
 int tempi_hip_pack_batch(const tempi_hip_batch_item *items, int n, void *stream) {
   return run_batch(true, items, n, static_cast<hipStream_t>(stream));

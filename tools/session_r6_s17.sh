@@ -3,8 +3,8 @@ set -o pipefail
 O=gpurun_out/config1_variants.jsonl
 rm -f $O
 for r in 1 2; do
-  for v in "P128_sys" "P128_agent:TEMPI_RESIDENT_ACQUIRE=agent" "P64_sys:TEMPI_RESIDENT_WORKERS=64" \
-           "P256_sys:TEMPI_RESIDENT_WORKERS=256" "P32_sys:TEMPI_RESIDENT_WORKERS=32"; do
+  for v in "P128_sys" "P128_agent:TEMPI_RESIDENT_ACQUIRE=agent" "P64_sys:TEMPI_RESIDENT_WORKERS=64" "P96_sys:TEMPI_RESIDENT_WORKERS=96" \
+           "P64_agent:TEMPI_RESIDENT_WORKERS=64 TEMPI_RESIDENT_ACQUIRE=agent"; do
     name=${v%%:*}; envs=""; [ "$v" != "$name" ] && envs=${v#*:}
     env VARIANT=$name $envs timeout -k 10 120 python -u tools/config1_ab.py 1 on >> $O 2>&1 || exit 2
   done
