@@ -1999,9 +1999,10 @@ template <typename F> int batch_with_ticket(hipStream_t s, const uint32_t **flag
 // behind the old). The server runs only between calls of a burst: an
 // application's hipDeviceSynchronize may wait up to the idle time for it.
 //
-// Taken: single descriptors of <= 3 dims, words of 4-16 bytes (narrower words
-// keep their interleaved / dense kernels), at most TEMPI_RESIDENT_MAX_BYTES
-// (default 2 MiB), not under TEMPI_LAUNCH_CHECK. TEMPI_RESIDENT=0 (or
+// Taken: single descriptors of <= 3 dims, at most TEMPI_RESIDENT_MAX_BYTES
+// (default 2 MiB; 1- and 2-byte words TEMPI_RESIDENT_NARROW_MAX_BYTES, default
+// 256 KiB: beyond, their interleaved / dense launches win), not under
+// TEMPI_LAUNCH_CHECK. TEMPI_RESIDENT=0 (or
 // tempi_hip_resident_enable(0)) turns it off.
 namespace resident {
 using tempi_ticket::kCounterStride;
@@ -2079,8 +2080,12 @@ template <bool PACK> __device__ __forceinline__ void serve_w(uint32_t op, const 
     serve_nd<PACK, 16>(nd, rec, w, nw);
   else if (W == 8)
     serve_nd<PACK, 8>(nd, rec, w, nw);
-  else
+  else if (W == 4)
     serve_nd<PACK, 4>(nd, rec, w, nw);
+  else if (W == 2)
+    serve_nd<PACK, 2>(nd, rec, w, nw);
+  else
+    serve_nd<PACK, 1>(nd, rec, w, nw);
 }
 
 // block 0: the leader (one wave); blocks 1 .. gridDim.x - 1: the workers
@@ -2211,6 +2216,10 @@ std::atomic<int> &switched_on() { // TEMPI_RESIDENT, then tempi_hip_resident_ena
 bool enabled() { return switched_on().load(std::memory_order_relaxed) != 0; }
 int64_t max_bytes() {
   static const int64_t v = env_int("TEMPI_RESIDENT_MAX_BYTES", int64_t(2) << 20);
+  return v;
+}
+int64_t narrow_max_bytes() {
+  static const int64_t v = env_int("TEMPI_RESIDENT_NARROW_MAX_BYTES", int64_t(256) << 10);
   return v;
 }
 // workers of a server: a multiple of kShards (a request takes up to all of them)
@@ -2348,8 +2357,10 @@ int run(bool pack, char *packed, char *first, const Norm &n, hipStream_t s, bool
   if (bytes == 0 || bytes > max_bytes()) return 0;
   for (int k = 0; k < n.nd; ++k)
     if (n.cnt[k] >= (int64_t(1) << 32)) return 0;
+  // 1- and 2-byte words move at a fraction of the rate on the chunk-per-lane
+  // body (their launched kernels interleave through LDS): only small objects
   const int w = word_width(reinterpret_cast<uintptr_t>(packed), reinterpret_cast<uintptr_t>(first), n);
-  if (w < 4) return 0;
+  if (w < 4 && bytes > narrow_max_bytes()) return 0;
   // (no order with TEMPI's earlier work on `s` is needed: a synchronous call
   // waited for its own, and an MPI_Isend / MPI_Irecv still in flight may not
   // share a buffer this call writes -- MPI's rule for the application --
@@ -2363,12 +2374,13 @@ int run(bool pack, char *packed, char *first, const Norm &n, hipStream_t s, bool
   Server &sv = server(device);
   if (!ready(sv)) return 0;
   uint32_t d[kGranules] = {};
-  if (w == 16)
-    make_record_w<16>(pack, packed, first, n, d);
-  else if (w == 8)
-    make_record_w<8>(pack, packed, first, n, d);
-  else
-    make_record_w<4>(pack, packed, first, n, d);
+  switch (w) {
+  case 16: make_record_w<16>(pack, packed, first, n, d); break;
+  case 8: make_record_w<8>(pack, packed, first, n, d); break;
+  case 4: make_record_w<4>(pack, packed, first, n, d); break;
+  case 2: make_record_w<2>(pack, packed, first, n, d); break;
+  default: make_record_w<1>(pack, packed, first, n, d); break;
+  }
   const uint32_t perShard = kResidentFlat ? 0u : d[kWorkers] / kShards;
   for (int k = 0; k < kShards; ++k) d[kTargets + k] = sv.counted[k] + perShard;
   d[kTargets + kShards] = sv.counted[kShards] + (kResidentFlat ? 0u : uint32_t(kShards));

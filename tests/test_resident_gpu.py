@@ -53,12 +53,13 @@ class resident_switch:
 
 # rows, block, stride, packed offset, served: 16-byte words (config 1 and
 # smaller), 8-byte words (halo x-face rows), 4-byte words, a packed side 4
-# bytes into its buffer (partial first / last chunks), 1-byte words (not
-# taken: their interleaved / dense kernels stay), 8 MiB (not taken: above
-# TEMPI_RESIDENT_MAX_BYTES)
+# bytes into its buffer (partial first / last chunks), 1- and 2-byte words
+# (taken up to TEMPI_RESIDENT_NARROW_MAX_BYTES = 256 KiB, above it their
+# interleaved / dense launches), 8 MiB (not taken: above TEMPI_RESIDENT_MAX_BYTES)
 SHAPES = [(1024, 512, 1024, 0, True), (300, 512, 1024, 0, True), (2, 512, 1024, 0, True),
           (4096, 24, 4608, 0, True), (100, 500, 1000, 0, True), (257, 48, 80, 4, True),
-          (4095, 16, 4112, 0, True), (20000, 3, 7, 0, False), (16384, 512, 1024, 0, False)]
+          (4095, 16, 4112, 0, True), (20000, 3, 7, 0, True), (5000, 2, 18, 1, True),
+          (100000, 3, 7, 0, False), (16384, 512, 1024, 0, False)]
 
 
 @pytest.mark.parametrize("rows,block,stride,off,served", SHAPES,
