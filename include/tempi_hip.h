@@ -126,6 +126,9 @@ int tempi_hip_copy_batch_ticket(const tempi_hip_copy_item *items, int n, void *s
    /root/reference/src/internal/packer_2d.cu:101-118 for small objects. */
 int tempi_hip_pack_resident(void *packed, const void *first, const tempi_hip_desc *d, void *stream, int *served);
 int tempi_hip_unpack_resident(void *first, const void *packed, const tempi_hip_desc *d, void *stream, int *served);
+/* one batch item (pack != 0: gather) the same way; TEMPI's transport uses it
+   for a batch of one object that a blocking call waits for */
+int tempi_hip_resident_item(int pack, const tempi_hip_batch_item *item, void *stream, int *served);
 /* requests served, server launches, requests posted again after crossing a
    server's idle exit */
 void tempi_hip_resident_stats(uint64_t *served, uint64_t *launches, uint64_t *reposts);

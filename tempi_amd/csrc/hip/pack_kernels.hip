@@ -2489,6 +2489,19 @@ int tempi_hip_unpack_resident(void *first, const void *packed, const tempi_hip_d
   return e;
 }
 
+int tempi_hip_resident_item(int pack, const tempi_hip_batch_item *item, void *stream, int *served) {
+  *served = 0;
+  Norm n;
+  if (!normalise(&item->desc, &n)) return int(hipErrorInvalidValue);
+  bool s = false;
+  gItemFlags = item->flags; // (a REMOTE item keeps its system-scope loads)
+  const int e = resident::run(pack != 0, static_cast<char *>(item->packed), static_cast<char *>(item->first), n,
+                              static_cast<hipStream_t>(stream), &s);
+  gItemFlags = 0;
+  *served = s ? 1 : 0;
+  return e;
+}
+
 void tempi_hip_resident_stats(uint64_t *served, uint64_t *launches, uint64_t *reposts) {
   std::lock_guard<std::mutex> lock(resident::mutex());
   if (served) *served = resident::stats().served;
