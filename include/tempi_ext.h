@@ -58,8 +58,6 @@ typedef struct tempi_counters_t {
   /* payload bytes of device-object sends by route: IPC (IPC COPY included,
      and counted again on its own), ONESHOT, STAGED, DEVICE, DIRECT (this process) */
   uint64_t bytes_ipc, bytes_ipc_copy, bytes_oneshot, bytes_staged, bytes_device, bytes_direct;
-  uint64_t resident_items; /* transport batches of one object that a blocking call (MPI_Send / MPI_Recv /
-                              MPI_Wait) had served by the resident packer instead of a launch */
 } tempi_counters_t;
 void tempi_get_counters(tempi_counters_t *out);
 void tempi_reset_counters(void);

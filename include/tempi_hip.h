@@ -126,12 +126,12 @@ int tempi_hip_copy_batch_ticket(const tempi_hip_copy_item *items, int n, void *s
    /root/reference/src/internal/packer_2d.cu:101-118 for small objects. */
 int tempi_hip_pack_resident(void *packed, const void *first, const tempi_hip_desc *d, void *stream, int *served);
 int tempi_hip_unpack_resident(void *first, const void *packed, const tempi_hip_desc *d, void *stream, int *served);
-/* one batch item (pack != 0: gather) the same way; TEMPI's transport uses it
-   for a batch of one object that a blocking call waits for */
-int tempi_hip_resident_item(int pack, const tempi_hip_batch_item *item, void *stream, int *served);
 /* requests served, server launches, requests posted again after crossing a
    server's idle exit */
 void tempi_hip_resident_stats(uint64_t *served, uint64_t *launches, uint64_t *reposts);
+/* requests whose server ended with them neither served nor refused (its
+   counters were then reset and the request posted again; 0 in every test) */
+uint64_t tempi_hip_resident_lost(void);
 /* an EXIT request to every running server; returns once they have left
    (MPI_Finalize) */
 void tempi_hip_resident_stop(void);

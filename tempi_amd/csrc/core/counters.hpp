@@ -40,7 +40,6 @@ struct Counters {
   // DEVICE (a GPU-aware library) and DIRECT (this same process)
   uint64_t bytes_ipc = 0, bytes_ipc_copy = 0, bytes_oneshot = 0, bytes_staged = 0, bytes_device = 0,
            bytes_direct = 0;
-  uint64_t resident_items = 0; // transport batches of one object a blocking call served by the resident packer
   // kernel time of synchronous MPI_Pack / MPI_Unpack while profiling is on
   double pack_kernel_ms = 0, unpack_kernel_ms = 0;
   uint64_t pack_timed = 0, unpack_timed = 0;

@@ -91,7 +91,6 @@ TEMPI_EXPORT void tempi_get_counters(tempi_counters_t *o) {
   o->bytes_staged = c.bytes_staged;
   o->bytes_device = c.bytes_device;
   o->bytes_direct = c.bytes_direct;
-  o->resident_items = c.resident_items;
 }
 
 TEMPI_EXPORT void tempi_reset_counters(void) {

@@ -35,6 +35,16 @@ void choose_lanes(int ranksOnNode) {
   nLanes = ranksOnNode > nDevices ? 1 : 3;
   if (const char *e = std::getenv("TEMPI_STREAMS")) nLanes = std::min(kMaxLanes, std::max(1, std::atoi(e)));
   LOG_DEBUG("stream lanes: " << nLanes);
+  // The resident packer's kernel keeps a hardware queue busy while it waits
+  // for calls. With more than two processes on one GPU, those queues
+  // oversubscribe the scheduler, which then time-slices every process's
+  // queues: the 8-rank halo on one GPU went from 4.3 to 53.6 ms/iter
+  // (profiles/r06/h8_resident_s29.txt). So it is off there unless
+  // TEMPI_RESIDENT asks for it.
+  if (nDevices > 0 && ranksOnNode > 2 * nDevices && !std::getenv("TEMPI_RESIDENT")) {
+    tempi_hip_resident_enable(0);
+    LOG_DEBUG("resident packer off: " << ranksOnNode << " ranks on " << nDevices << " GPU(s)");
+  }
 }
 
 bool available() { return nDevices > 0 || hostOnlyTest; }

@@ -646,11 +646,6 @@ int wait(MPI_Request *req, MPI_Status *status) {
   if (PersistentOp *p = op->persistent()) return persistent_wait(p, status);
   if (!op->done) {
     ScopedNs timer(counters.ns_wait);
-    struct Sync { // (restored, not cleared: a wait may nest inside a callback of another)
-      bool prev = syncWaiting;
-      Sync() { syncWaiting = true; }
-      ~Sync() { syncWaiting = prev; }
-    } sync;
     while (!op->done) {
       progress();
       if (!op->done) op->stalled();

@@ -371,9 +371,6 @@ constexpr size_t kEarlyFlush = 32;
 constexpr size_t kFirstFlush = 16;
 extern int batchesInFlight;    // batches launched and not yet seen complete (any kind)
 extern int scattersInFlight;   // scatter / copy batches launched and not yet seen complete
-// a blocking call (p2p::wait) is spinning for an operation: a batch of one
-// object is then served by the resident packer instead of launched (flush_list)
-extern thread_local bool syncWaiting;
 void flush_list(PendingList &list, bool pack);
 // counters.ns_gpu_inflight bookkeeping: a batch launched / observed complete
 void batch_launched();

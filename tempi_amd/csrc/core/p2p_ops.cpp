@@ -177,7 +177,6 @@ void Op::settle_buffered() {
   unpostedBuffered = false;
 }
 int scattersInFlight = 0;
-thread_local bool syncWaiting = false;
 int batchesInFlight = 0;
 uint64_t inflightSince = 0; // (ns) the first of the batches now in flight was launched
 
@@ -223,46 +222,6 @@ void flush_list(PendingList &list, bool pack) {
     if (k == ndev && ndev < 64) devices[ndev++] = op->device;
   }
   const bool all = ndev == 1;
-  // one object that a blocking call (MPI_Send / MPI_Recv / MPI_Wait) is about
-  // to wait for: the resident packer does it now, with no launch (DESIGN
-  // §6.4; 4-5 us instead of ~8 for a launch and its ticket). Not a scatter
-  // that must follow a gather still in flight (afterPack), nor with copies or
-  // staged pieces; a batch it serves is complete as it returns (but is seen
-  // complete in its lane's order, as any batch)
-  if (syncWaiting && all && list.items.size() == 1 && list.copies.empty() && list.stages.empty() &&
-      (pack || !list.afterPack)) {
-    const int dev = devices[0];
-    void *s = gpu::stream(dev, lane);
-    int cur = 0;
-    tempi_hip_get_device(&cur);
-    if (cur != dev) tempi_hip_set_device(dev);
-    int served = 0;
-    gpu::check(tempi_hip_resident_item(pack ? 1 : 0, &list.items[0], s, &served), "resident batch item");
-    if (served) {
-      static const uint32_t kServed = 0; // (a ticket that is always reached)
-      counters.batches++;
-      counters.batched_items++;
-      counters.resident_items++;
-      auto b = std::make_shared<GpuBatch>();
-      b->device = dev;
-      b->lane = lane;
-      b->scatter = !pack;
-      b->stream = s;
-      b->flag = &kServed;
-      b->ticket = 0;
-      if (!pack) ++scattersInFlight;
-      for (Op *op : list.ops) {
-        op->queued = false;
-        b->ops.push_back(op);
-      }
-      batches.push_back(b);
-      batch_launched();
-      if (cur != dev) tempi_hip_set_device(cur);
-      list.clear();
-      return;
-    }
-    if (cur != dev) tempi_hip_set_device(cur);
-  }
   std::vector<tempi_hip_batch_item> itmp;
   std::vector<tempi_hip_copy_item> ctmp;
   for (int di = 0; di < ndev; ++di) {

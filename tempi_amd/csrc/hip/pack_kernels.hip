@@ -46,6 +46,8 @@
 #include <string>
 #include <vector>
 
+#include <unistd.h>
+
 namespace {
 
 struct Magic {
@@ -1990,13 +1992,15 @@ template <typename F> int batch_with_ticket(hipStream_t s, const uint32_t **flag
 //
 // Lifetime: the server is launched by the first call that can use it (that
 // call pays about a launch, as before) on a stream of its own, and leaves after
-// TEMPI_RESIDENT_IDLE_US (default 1 000) without a request, after 2 s in any
+// TEMPI_RESIDENT_IDLE_US (default 200) without a request, after 2 s in any
 // case, or on an EXIT request (MPI_Finalize). Every wave has a bounded exit:
-// the leader hands the workers an EXIT record as it leaves, and workers give
-// up on their own 4 x idle + 1 ms after their last request. A leader leaving
-// stores the first sequence number it did not serve; a request that crossed
-// its exit is posted again to a new instance (stream order puts the new one
-// behind the old). The server runs only between calls of a burst: an
+// the leader hands the workers an EXIT record as it leaves, and workers leave
+// on that record alone (or 1 ms past the 2 s cap). A leader leaving stores the
+// first sequence number it did not serve; a request that crossed its exit is
+// posted again to a new instance (stream order puts the new one behind the
+// old). A server that ended with a request neither served nor refused (never
+// seen so far) has its counters reset and the request posted again: packs and
+// unpacks are idempotent. The server runs only between calls of a burst: an
 // application's hipDeviceSynchronize may wait up to the idle time for it.
 //
 // Taken: single descriptors of <= 3 dims, at most TEMPI_RESIDENT_MAX_BYTES
@@ -2120,7 +2124,9 @@ __global__ __launch_bounds__(kBlock) void server_kernel(Mail *m, Dev *dv, uint32
       take(gb);
       if (leave) break;
       const uint64_t now = wall_clock64();
-      if (now - last > idle || now - t0 > cap) {
+      // (signed: a wave restored onto another XCD after a preemption reads
+      // another XCD's clock, which may be behind the one it last read)
+      if (int64_t(now - last) > int64_t(idle) || int64_t(now - t0) > int64_t(cap)) {
         __hip_atomic_store(&dv->bcast[lane], (uint64_t(expect) << 32) | (lane == 0 ? kOpExit : 0u),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
@@ -2141,7 +2147,11 @@ __global__ __launch_bounds__(kBlock) void server_kernel(Mail *m, Dev *dv, uint32
           break;
         }
         const uint64_t now = wall_clock64();
-        if (now - last > 4 * idle + kGrace || now - t0 > cap + kGrace) { // (a lost leader)
+        // workers leave on the leader's EXIT record alone: one that left on a
+        // clock of its own could miss a request the leader then hands out.
+        // The cap is only the bound every wave reaches, a grace period after
+        // the leader's own
+        if (int64_t(now - t0) > int64_t(cap + kGrace)) {
           d = lane == 0 ? kOpExit : 0u;
           break;
         }
@@ -2232,7 +2242,7 @@ uint32_t workers() {
   return v;
 }
 uint64_t idle_ticks() {
-  static const uint64_t v = uint64_t(std::max<int64_t>(env_int("TEMPI_RESIDENT_IDLE_US", 1000), 1)) * kTicksPerUs;
+  static const uint64_t v = uint64_t(std::max<int64_t>(env_int("TEMPI_RESIDENT_IDLE_US", 200), 1)) * kTicksPerUs;
   return v;
 }
 constexpr uint64_t kCapTicks = uint64_t(2000000) * kTicksPerUs; // 2 s
@@ -2257,7 +2267,7 @@ struct Server {
   uint32_t counted[kShards + 1] = {}; // the host's totals of the device counters
 };
 struct Stats {
-  uint64_t served = 0, launches = 0, reposts = 0;
+  uint64_t served = 0, launches = 0, reposts = 0, lost = 0;
 };
 std::mutex &mutex() {
   static std::mutex m;
@@ -2275,7 +2285,15 @@ Server &server(int device) {
 bool ready(Server &sv) {
   if (sv.ready || sv.broken) return sv.ready;
   void *h = nullptr, *d = nullptr, *dv = nullptr;
-  hipError_t e = hipStreamCreateWithFlags(&sv.stream, hipStreamNonBlocking);
+  // A kernel that stays running holds its hardware queue: any stream HIP maps
+  // onto the same queue (at most GPU_MAX_HW_QUEUES = 4 per process) waits
+  // behind it. Made at normal priority after TEMPI's streams, the server's
+  // stream shared the null stream's queue (a kernel there waited out the
+  // server); at high priority it shared none of the process's streams
+  // (tools/queue_probe.hip, profiles/r06/queue_probe_s30.jsonl).
+  int least = 0, greatest = 0;
+  hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+  if (e == hipSuccess) e = hipStreamCreateWithPriority(&sv.stream, hipStreamNonBlocking, greatest);
   if (e == hipSuccess) e = hipHostMalloc(&h, sizeof(Mail), hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable);
   if (e == hipSuccess) e = hipHostGetDevicePointer(&d, h, 0);
   if (e == hipSuccess) e = hipMalloc(&dv, sizeof(Dev));
@@ -2299,7 +2317,8 @@ void post(Server &sv, uint32_t seq, const uint32_t *d) {
     __atomic_store_n(&sv.host->req[i], (uint64_t(seq) << 32) | d[i], __ATOMIC_RELAXED);
 }
 
-// 0: served; 1: the server left without serving it; else a HIP error
+// 0: served; 1: the server left without serving it; 2: the server ended
+// with it neither served nor refused; else a HIP error
 int wait(Server &sv, uint32_t seq) {
   for (uint32_t spins = 1;; ++spins) {
     if (__atomic_load_n(&sv.host->done, __ATOMIC_ACQUIRE) == seq) return 0;
@@ -2309,7 +2328,7 @@ int wait(Server &sv, uint32_t seq) {
       if (e == hipSuccess) { // ended: its last stores are visible now
         if (__atomic_load_n(&sv.host->done, __ATOMIC_ACQUIRE) == seq) return 0;
         if (__atomic_load_n(&sv.host->exitw, __ATOMIC_ACQUIRE) == seq) return 1;
-        return int(hipErrorUnknown);
+        return 2;
       }
       if (e != hipErrorNotReady) return int(e);
       (void)hipGetLastError();
@@ -2350,7 +2369,22 @@ void make_record_w(bool pack, char *packed, char *first, const Norm &n, uint32_t
 
 // serve one synchronous pack / unpack; *served = false: not taken (the caller
 // launches as before)
+int run_inner(bool pack, char *packed, char *first, const Norm &n, hipStream_t s, bool *served);
+// (TEMPI_RESIDENT_DEBUG=1: report a HIP error the call left behind)
 int run(bool pack, char *packed, char *first, const Norm &n, hipStream_t s, bool *served) {
+  static const bool debug = env_flag("TEMPI_RESIDENT_DEBUG", false);
+  const hipError_t pre = debug ? hipPeekAtLastError() : hipSuccess;
+  const int e = run_inner(pack, packed, first, n, s, served);
+  if (debug) {
+    const hipError_t post = hipPeekAtLastError();
+    if (post != hipSuccess)
+      std::fprintf(stderr, "[resident] pid %d: HIP error %s (%d) pending after a call (before: %s), rc %d served %d, "
+                   "%d dims, block %lld\n", int(getpid()), hipGetErrorString(post), int(post),
+                   hipGetErrorString(pre), e, int(*served), n.nd, (long long)n.block);
+  }
+  return e;
+}
+int run_inner(bool pack, char *packed, char *first, const Norm &n, hipStream_t s, bool *served) {
   *served = false;
   if (!enabled() || launch_check() || n.nd > 3) return 0;
   const int64_t bytes = norm_bytes(n);
@@ -2404,7 +2438,20 @@ int run(bool pack, char *packed, char *first, const Norm &n, hipStream_t s, bool
       return 0;
     }
     sv.running = false;
-    if (r != 1) { // a fault: the counters are unknown from here on
+    if (r == 2) { // workers may have counted part of it: start the counts again
+      stats().lost++;
+      hipError_t e = hipMemsetAsync(sv.dev->counter, 0, sizeof(sv.dev->counter), sv.stream);
+      if (e == hipSuccess) e = hipStreamSynchronize(sv.stream);
+      if (e != hipSuccess) {
+        (void)hipGetLastError();
+        sv.broken = true;
+        return int(e);
+      }
+      for (uint32_t &c : sv.counted) c = 0;
+      for (int k = 0; k < kShards; ++k) d[kTargets + k] = perShard;
+      d[kTargets + kShards] = kResidentFlat ? 0u : uint32_t(kShards);
+      if (kResidentFlat) d[kTargets] = d[kWorkers];
+    } else if (r != 1) { // a fault: the counters are unknown from here on
       sv.broken = true;
       return r;
     }
@@ -2489,24 +2536,16 @@ int tempi_hip_unpack_resident(void *first, const void *packed, const tempi_hip_d
   return e;
 }
 
-int tempi_hip_resident_item(int pack, const tempi_hip_batch_item *item, void *stream, int *served) {
-  *served = 0;
-  Norm n;
-  if (!normalise(&item->desc, &n)) return int(hipErrorInvalidValue);
-  bool s = false;
-  gItemFlags = item->flags; // (a REMOTE item keeps its system-scope loads)
-  const int e = resident::run(pack != 0, static_cast<char *>(item->packed), static_cast<char *>(item->first), n,
-                              static_cast<hipStream_t>(stream), &s);
-  gItemFlags = 0;
-  *served = s ? 1 : 0;
-  return e;
-}
-
 void tempi_hip_resident_stats(uint64_t *served, uint64_t *launches, uint64_t *reposts) {
   std::lock_guard<std::mutex> lock(resident::mutex());
   if (served) *served = resident::stats().served;
   if (launches) *launches = resident::stats().launches;
   if (reposts) *reposts = resident::stats().reposts;
+}
+
+uint64_t tempi_hip_resident_lost(void) {
+  std::lock_guard<std::mutex> lock(resident::mutex());
+  return resident::stats().lost;
 }
 
 void tempi_hip_resident_stop(void) { resident::stop_all(); }

@@ -44,7 +44,6 @@ _COUNTER_FIELDS = [
     "self_matched", "staged_packs", "staged_unpacks", "ticket_waits", "sync_waits",
     "ticket_batches", "persistent_starts", "batches", "gpu_inflight_ns",
     "bytes_ipc", "bytes_ipc_copy", "bytes_oneshot", "bytes_staged", "bytes_device", "bytes_direct",
-    "resident_items",
 ]
 
 

@@ -71,4 +71,7 @@ s1 = stats()
 for t in types:
     mpi.Type_free(t)
 mpi.Finalize()
-print(f"RESULT errors={errors} served={s1[0] - s0[0]} launches={s1[1] - s0[1]} reposts={s1[2] - s0[2]}", flush=True)
+H.tempi_hip_resident_lost.restype = ctypes.c_uint64
+lost = H.tempi_hip_resident_lost()
+print(f"RESULT errors={errors} served={s1[0] - s0[0]} launches={s1[1] - s0[1]} reposts={s1[2] - s0[2]} lost={lost}",
+      flush=True)

@@ -205,4 +205,26 @@ def test_resident_exit_race(gpu, idle_us):
     assert r.returncode == 0 and line, r.stdout[-3000:]
     f = dict(kv.split("=") for kv in line[0].split()[1:])
     assert int(f["errors"]) == 0, r.stdout[-3000:]
-    assert int(f["served"]) == 800 and int(f["launches"]) > 1, line[0]
+    assert int(f["served"]) == 800 and int(f["launches"]) > 1 and int(f["lost"]) == 0, line[0]
+
+
+@pytest.mark.parametrize("forced", [True, False])
+def test_resident_many_processes(gpu, forced):
+    """Four processes on one GPU making bursts of synchronous packs /
+    unpacks with random gaps around the idle time (tests/mpi_progs/
+    resident_race.py under mpiexec -n 4). By default the packer is off with
+    more than two ranks per GPU (its waiting kernels oversubscribe the
+    scheduler: core/gpu.cpp choose_lanes), so nothing is served. Forced on
+    (TEMPI_RESIDENT=1), every process runs its own server; their queues are
+    time-sliced, so server waves are preempted and restored (possibly onto
+    another XCD, whose clock differs): every byte right, nothing lost."""
+    from tests import mpi_launch
+
+    env = {"TEMPI_RESIDENT": "1"} if forced else {}
+    rc, out = mpi_launch.run(4, mpi_launch.py("resident_race.py", "20", "300"), env=env, timeout=240)
+    lines = [l for l in out.splitlines() if l.startswith("RESULT")]
+    assert rc == 0 and len(lines) == 4, out[-4000:]
+    for l in lines:
+        f = dict(kv.split("=") for kv in l.split()[1:])
+        assert int(f["errors"]) == 0 and int(f["lost"]) == 0, l
+        assert int(f["served"]) == (600 if forced else 0), l
