@@ -2032,6 +2032,10 @@ constexpr uint64_t kTicksPerUs = 100; // wall_clock64 (s_memrealtime): 100 MHz
 #define TEMPI_RESIDENT_U 1
 #endif
 constexpr int kResidentU = TEMPI_RESIDENT_U;
+// polls of the host link the leader keeps in flight (2 or 4; A/B)
+#ifndef TEMPI_RESIDENT_POLLS
+#define TEMPI_RESIDENT_POLLS 2
+#endif
 // one completion counter for all workers (a request has at most a few
 // hundred) instead of the launched kernels' sharded fold: one atomic on the
 // path instead of two, no slower in the A/B
@@ -2115,14 +2119,32 @@ __global__ __launch_bounds__(kBlock) void server_kernel(Mail *m, Dev *dv, uint32
       last = wall_clock64();
       leave = (op & 3) == kOpExit;
     };
-    uint64_t ga = __hip_atomic_load(&m->req[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    auto poll = [&]() { return __hip_atomic_load(&m->req[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); };
+#if TEMPI_RESIDENT_POLLS >= 4
+    uint64_t g0 = poll(), g1 = poll(), g2 = poll();
     for (;;) {
-      const uint64_t gb = __hip_atomic_load(&m->req[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      const uint64_t g3 = poll();
+      take(g0);
+      if (leave) break;
+      g0 = poll();
+      take(g1);
+      if (leave) break;
+      g1 = poll();
+      take(g2);
+      if (leave) break;
+      g2 = poll();
+      take(g3);
+      if (leave) break;
+#else
+    uint64_t ga = poll();
+    for (;;) {
+      const uint64_t gb = poll();
       take(ga);
       if (leave) break;
-      ga = __hip_atomic_load(&m->req[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      ga = poll();
       take(gb);
       if (leave) break;
+#endif
       const uint64_t now = wall_clock64();
       // (signed: a wave restored onto another XCD after a preemption reads
       // another XCD's clock, which may be behind the one it last read)
