@@ -228,3 +228,16 @@ def test_resident_many_processes(gpu, forced):
         f = dict(kv.split("=") for kv in l.split()[1:])
         assert int(f["errors"]) == 0 and int(f["lost"]) == 0, l
         assert int(f["served"]) == (600 if forced else 0), l
+
+
+def test_resident_threads(gpu):
+    """MPI_THREAD_MULTIPLE: four threads' synchronous packs / unpacks meet at
+    the resident packer (tests/mpi_progs/resident_threads.py): bit-exact,
+    every call served (config 1, 8-, 4- and 1-byte-word shapes, all under the
+    limits)."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "mpi_progs", "resident_threads.py"), "100"],
+                       cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=240)
+    line = [l for l in r.stdout.splitlines() if l.startswith("RESULT")]
+    assert r.returncode == 0 and line, r.stdout[-3000:]
+    f = dict(kv.split("=") for kv in line[0].split()[1:])
+    assert int(f["errors"]) == 0 and int(f["served"]) == 800, line[0]
