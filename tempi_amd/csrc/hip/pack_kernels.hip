@@ -2299,9 +2299,10 @@ Stats &stats() {
   static Stats s;
   return s;
 }
+constexpr int kMaxServers = 64; // devices a process may have a server on
 Server &server(int device) {
-  static Server s[64];
-  return s[device & 63];
+  static Server s[kMaxServers];
+  return s[device];
 }
 
 bool ready(Server &sv) {
@@ -2322,6 +2323,11 @@ bool ready(Server &sv) {
   if (e == hipSuccess) e = hipMemsetAsync(dv, 0, sizeof(Dev), sv.stream);
   if (e == hipSuccess) e = hipStreamSynchronize(sv.stream);
   if (e != hipSuccess) {
+    (void)hipGetLastError();
+    if (dv) (void)hipFree(dv);
+    if (h) (void)hipHostFree(h);
+    if (sv.stream) (void)hipStreamDestroy(sv.stream);
+    sv.stream = nullptr;
     (void)hipGetLastError();
     sv.broken = true;
     return false;
@@ -2425,7 +2431,7 @@ int run_inner(bool pack, char *packed, char *first, const Norm &n, hipStream_t s
   // hand every call of a burst to a launch.)
   (void)s;
   int device = 0;
-  if (hipGetDevice(&device) != hipSuccess) return 0;
+  if (hipGetDevice(&device) != hipSuccess || device < 0 || device >= kMaxServers) return 0;
   std::lock_guard<std::mutex> lock(mutex());
   Server &sv = server(device);
   if (!ready(sv)) return 0;
@@ -2485,7 +2491,7 @@ int run_inner(bool pack, char *packed, char *first, const Norm &n, hipStream_t s
 // MPI_Finalize: an EXIT request to every running server, then its stream drains
 void stop_all() {
   std::lock_guard<std::mutex> lock(mutex());
-  for (int dv = 0; dv < 64; ++dv) {
+  for (int dv = 0; dv < kMaxServers; ++dv) {
     Server &sv = server(dv);
     if (!sv.ready || !sv.running) continue;
     uint32_t d[kGranules] = {};
@@ -2577,6 +2583,8 @@ int tempi_hip_resident_enable(int on) { return resident::switched_on().exchange(
 int tempi_hip_resident_stamps(uint64_t *out) {
   int device = 0;
   hipError_t e = hipGetDevice(&device);
+  if (e == hipSuccess && (device < 0 || device >= resident::kMaxServers)) e = hipErrorInvalidDevice;
+  if (e != hipSuccess) return int(e);
   std::lock_guard<std::mutex> lock(resident::mutex());
   resident::Server &sv = resident::server(device);
   if (e == hipSuccess && !sv.ready) e = hipErrorNotReady;
