@@ -1998,10 +1998,20 @@ template <typename F> int batch_with_ticket(hipStream_t s, const uint32_t **flag
 // on that record alone (or 1 ms past the 2 s cap). A leader leaving stores the
 // first sequence number it did not serve; a request that crossed its exit is
 // posted again to a new instance (stream order puts the new one behind the
-// old). A server that ended with a request neither served nor refused (never
-// seen so far) has its counters reset and the request posted again: packs and
-// unpacks are idempotent. The server runs only between calls of a burst: an
+// old). A server that ended with a request neither served nor refused has its
+// counters reset and the request posted again: packs and unpacks are
+// idempotent. The server runs only between calls of a burst: an
 // application's hipDeviceSynchronize may wait up to the idle time for it.
+//
+// The hand-off slot holds one record, so the leader overwrites it (with the
+// next request or EXIT) only once every worker has counted itself on
+// Dev::seen for the record there: a worker preempted or dispatched late would
+// otherwise find a later tag than the one it waits for and sit out the cap,
+// while a request that needed it never completed (four processes
+// time-slicing one GPU: profiles/r06/NOTES.md s36). A worker counts itself
+// right after its part of the completion, long before the host has seen the
+// completion and posted the next request, so the leader's check (a load kept
+// in flight beside its polls) costs a call nothing.
 //
 // Taken: single descriptors of <= 3 dims, at most TEMPI_RESIDENT_MAX_BYTES
 // (default 2 MiB; 1- and 2-byte words TEMPI_RESIDENT_NARROW_MAX_BYTES, default
@@ -2032,10 +2042,6 @@ constexpr uint64_t kTicksPerUs = 100; // wall_clock64 (s_memrealtime): 100 MHz
 #define TEMPI_RESIDENT_U 1
 #endif
 constexpr int kResidentU = TEMPI_RESIDENT_U;
-// polls of the host link the leader keeps in flight (2 or 4; A/B)
-#ifndef TEMPI_RESIDENT_POLLS
-#define TEMPI_RESIDENT_POLLS 2
-#endif
 // one completion counter for all workers (a request has at most a few
 // hundred) instead of the launched kernels' sharded fold: one atomic on the
 // path instead of two, no slower in the A/B
@@ -2059,6 +2065,9 @@ struct Dev {                  // device memory, zeroed once
   // the hand-off, finished its acquire, finished its body; the completing
   // worker stored the completion
   uint64_t stamp[8];
+  // records read, summed over the workers (a line of its own: one atomic per
+  // worker and request, none of them on a call's path)
+  uint32_t seen[32];
 };
 
 template <bool PACK, int W, int ND>
@@ -2108,49 +2117,62 @@ __global__ __launch_bounds__(kBlock) void server_kernel(Mail *m, Dev *dv, uint32
     if (wave) return;
     // two polls of the host link in flight, so a request is seen about half
     // a round trip sooner; a poll older than the request it overlapped holds
-    // an old tag and is passed over
+    // an old tag and is passed over (four: no gain)
     bool leave = false;
-    auto take = [&](uint64_t g) {
+    const uint32_t nWorkers = gridDim.x - 1;
+    auto seen = [&]() { return __hip_atomic_load(&dv->seen[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+    const uint32_t seen0 = seen(); // (the previous instance has ended: stream order)
+    uint32_t handed = 0;           // records this leader handed out
+    // every worker has read the record in the slot (s: a recent Dev::seen);
+    // else wait for them, up to the cap
+    auto all_read = [&](uint32_t s) {
+      while (s - seen0 != handed * nWorkers) {
+        if (int64_t(wall_clock64() - t0) > int64_t(cap)) return false;
+        __builtin_amdgcn_s_sleep(1);
+        s = seen();
+      }
+      return true;
+    };
+    auto take = [&](uint64_t g, uint32_t s) {
       if (__ballot(uint32_t(g >> 32) == expect) != ~0ull) return;
+      leave = true;
+      if (!all_read(s)) return; // (past the cap: left unserved, so posted again)
       const uint32_t op = __shfl(uint32_t(g), 0);
       if ((op & kStamp) && lane == 0) dv->stamp[0] = wall_clock64();
       __hip_atomic_store(&dv->bcast[lane], g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       ++expect;
+      ++handed;
       last = wall_clock64();
       leave = (op & 3) == kOpExit;
     };
     auto poll = [&]() { return __hip_atomic_load(&m->req[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); };
-#if TEMPI_RESIDENT_POLLS >= 4
-    uint64_t g0 = poll(), g1 = poll(), g2 = poll();
-    for (;;) {
-      const uint64_t g3 = poll();
-      take(g0);
-      if (leave) break;
-      g0 = poll();
-      take(g1);
-      if (leave) break;
-      g1 = poll();
-      take(g2);
-      if (leave) break;
-      g2 = poll();
-      take(g3);
-      if (leave) break;
-#else
+    // each poll travels with a load of Dev::seen issued just after it, so
+    // the count a request is checked against left no earlier than the poll
     uint64_t ga = poll();
+    uint32_t sa = seen();
     for (;;) {
       const uint64_t gb = poll();
-      take(ga);
+      const uint32_t sb = seen();
+      take(ga, sa);
       if (leave) break;
       ga = poll();
-      take(gb);
+      sa = seen();
+      take(gb, sb);
       if (leave) break;
-#endif
       const uint64_t now = wall_clock64();
       // (signed: a wave restored onto another XCD after a preemption reads
       // another XCD's clock, which may be behind the one it last read)
       if (int64_t(now - last) > int64_t(idle) || int64_t(now - t0) > int64_t(cap)) {
-        __hip_atomic_store(&dv->bcast[lane], (uint64_t(expect) << 32) | (lane == 0 ? kOpExit : 0u),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // one fresh poll first: a request posted as the idle time ran out is
+        // served, not refused (a refusal costs its call a launch)
+        const uint32_t before = expect;
+        const uint64_t g = poll();
+        take(g, seen());
+        if (leave) break;
+        if (expect != before) continue;
+        if (all_read(seen())) // (else past the cap: workers leave on theirs)
+          __hip_atomic_store(&dv->bcast[lane], (uint64_t(expect) << 32) | (lane == 0 ? kOpExit : 0u),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
     }
@@ -2228,6 +2250,8 @@ __global__ __launch_bounds__(kBlock) void server_kernel(Mail *m, Dev *dv, uint32
         }
       }
     }
+    // this worker is done with the record: the leader may overwrite it
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(&dv->seen[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     last = wall_clock64();
     __syncthreads(); // (every wave has read the record before wave 0 writes the next)
   }
