@@ -2050,6 +2050,11 @@ constexpr int kResidentU = TEMPI_RESIDENT_U;
 #endif
 constexpr bool kResidentFlat = TEMPI_RESIDENT_FLAT != 0;
 constexpr uint64_t kGrace = 1000 * kTicksPerUs;
+// a fresh instance waits at least this long for its first request: the call
+// that launched it posts right after the launch, and a host thread
+// descheduled in between must not see its request refused twice (the call
+// would then launch after all)
+constexpr uint64_t kFirstIdle = 100 * kTicksPerUs;
 
 struct Mail {                 // pinned, coherent, mapped host memory
   uint64_t req[kGranules];    // the request, tagged with its sequence number
@@ -2162,7 +2167,8 @@ __global__ __launch_bounds__(kBlock) void server_kernel(Mail *m, Dev *dv, uint32
       const uint64_t now = wall_clock64();
       // (signed: a wave restored onto another XCD after a preemption reads
       // another XCD's clock, which may be behind the one it last read)
-      if (int64_t(now - last) > int64_t(idle) || int64_t(now - t0) > int64_t(cap)) {
+      const uint64_t limit = handed || idle >= kFirstIdle ? idle : kFirstIdle;
+      if (int64_t(now - last) > int64_t(limit) || int64_t(now - t0) > int64_t(cap)) {
         // one fresh poll first: a request posted as the idle time ran out is
         // served, not refused (a refusal costs its call a launch)
         const uint32_t before = expect;
