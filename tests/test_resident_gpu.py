@@ -198,14 +198,17 @@ def test_resident_exit_race(gpu, idle_us):
     resident_race.py): with the idle time a few microseconds and random gaps
     of up to three idle times between calls, requests are served, reposted to
     a new instance or taken by a fresh launch -- every byte still right, and
-    more than one server instance launched."""
+    more than one server instance launched. (A call whose request two
+    instances refuse launches instead, bytes checked all the same; with a
+    fresh instance waiting 100 us for its first record that takes a host
+    thread descheduled between launch and post, so at most a few.)"""
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "mpi_progs", "resident_race.py"), str(idle_us),
                         "400"], cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=240)
     line = [l for l in r.stdout.splitlines() if l.startswith("RESULT")]
     assert r.returncode == 0 and line, r.stdout[-3000:]
     f = dict(kv.split("=") for kv in line[0].split()[1:])
     assert int(f["errors"]) == 0, r.stdout[-3000:]
-    assert int(f["served"]) == 800 and int(f["launches"]) > 1 and int(f["lost"]) == 0, line[0]
+    assert 796 <= int(f["served"]) <= 800 and int(f["launches"]) > 1 and int(f["lost"]) == 0, line[0]
 
 
 @pytest.mark.parametrize("forced", [True, False])
